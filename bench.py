@@ -1,0 +1,263 @@
+"""bench.py -- scenario-QP solves/sec of the PH hot path (farmer cm=10, 10k scenarios) on MI355X.
+
+One "step" = one PH iteration over all scenarios: fused xbar / W / convergence update
+(phbase.py:976-1000) + one batched prox-QP solve of every scenario (phbase.py:1023-1030).
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N>1 is launched by torch.distributed.run
+(one rank per GPU, RCCL).  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 dense peak (vector == matrix), MI355X_MICROARCH / spec
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scen", type=int, default=10000, help="scenarios PER GPU (weak scaling)")
+    ap.add_argument("--cm", type=int, default=10)
+    ap.add_argument("--rho", type=float, default=1.0)
+    ap.add_argument("--eps", type=float, default=1e-9)
+    ap.add_argument("--conv-iters", type=int, default=3000, help="PH iteration cap for time-to-conv (0: skip)")
+    ap.add_argument("--conv-time", type=float, default=90.0, help="wall cap (s) for time-to-conv")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0: skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def pdhg_flops_per_iter(n, m, nnz):
+    # A x (2 nnz) + A^T y (2 nnz); primal update per column: c - A^T y, *tau, x -, /(1+tau q)
+    # (incl. 1 mul for tau q, 1 add), clamp (2), running sum (1) = 9; dual update per row:
+    # 2 Ax+ - Ax (2), *sig (1), y - (1), + sig*l (2), + sig*u (2), max/min (2), add (1),
+    # running sums of y and Ax (2) = 13; A^T y running sum per column (1)
+    return 4 * nnz + 10 * n + 13 * m
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    comm = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(f"cuda:{local_rank}"))
+    import _pkg
+    _pkg.load()
+    from mpisppy_amd import _lib
+    from mpisppy_amd.comm import TorchComm
+    from mpisppy_amd.examples import farmer
+    from mpisppy_amd.ph import PH
+    if world > 1:
+        comm = TorchComm()
+
+    S = args.scen * world
+    names = farmer.scenario_names_creator(S)
+    opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
+            "convthresh": 1e-4, "verbose": False, "display_progress": False,
+            "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps}}
+    t_setup = time.perf_counter()
+    ph = PH(dict(opts), names, farmer.scenario_creator, mpicomm=comm,
+            scenario_creator_kwargs={"crops_multiplier": args.cm, "num_scens": S})
+    ph.PH_Prep()
+    t_iter0 = time.perf_counter()
+    ph.Iter0()
+    torch.cuda.synchronize()
+    t_iter0 = time.perf_counter() - t_iter0
+    t_setup = time.perf_counter() - t_setup
+    eng = ph.engine
+    b = eng.batch
+    S_loc = eng.S
+
+    def step():
+        ph.Compute_Xbar()
+        ph.Update_W()
+        conv = ph.convergence_diff()
+        ph.solve_loop(solver_options=ph.iterk_solver_options)
+        return conv
+
+    for _ in range(args.warmup):
+        step()
+    # timed region
+    pdhg_ms = 0.0
+    upd_ms = 0.0
+    pdhg_iters = 0
+    max_iters = 0
+    if comm is not None:
+        comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        conv = step()
+        pdhg_ms += eng.last_ms(0)
+        upd_ms += eng.last_ms(1)
+        its = eng.get_i32(_lib.I_ITERS)
+        pdhg_iters += int(its.sum())
+        max_iters = max(max_iters, int(its.max()))
+    torch.cuda.synchronize()
+    if comm is not None:
+        comm.barrier()
+    el = time.perf_counter() - t0
+    if comm is not None:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        tot = torch.tensor([float(pdhg_iters)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tot)
+        pdhg_iters_all = int(tot.item())
+    else:
+        pdhg_iters_all = pdhg_iters
+    S_all = S
+    value = S_all * args.steps / el
+    ms_per_step = el / args.steps * 1e3
+
+    # roofline of the dominant kernel (batched PDHG), per launch, from HIP events on its stream
+    f_it = pdhg_flops_per_iter(b.n, b.m, b.nnz)
+    flops_per_launch = f_it * pdhg_iters / args.steps
+    avg_launch_s = pdhg_ms / args.steps / 1e3
+    achieved_tf = flops_per_launch / avg_launch_s / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("pdhg_bytes_per_launch")
+        except Exception:
+            traffic = None
+    # fused xbar/W/conv kernels: algorithmic bytes: 8 S N (x read, W read+write,
+    # rho read) + 8 S + 16 N_tot
+    ph_bytes = 8 * S_loc * b.N * 4 + 8 * S_loc + 16 * b.N_tot
+    ph_gbs = ph_bytes / (upd_ms / args.steps / 1e3) / 1e9
+
+    out = {
+        "metric": "scenario-QP solves/sec (PH iteration: batched prox-QP solve of every scenario + fused xbar/W/conv)",
+        "value": round(value, 2),
+        "unit": "scenario-QP solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (farmer generator of examples/farmer/farmer.py, seeded per scenario)",
+        "config": {"workload": f"farmer crops_multiplier={args.cm}, {S} scenarios ({args.scen} per GPU), PH rho={args.rho}, "
+                               f"PDHG eps_rel={args.eps}",
+                   "scenarios": S, "n": b.n, "m": b.m, "nnz": b.nnz, "nonants": b.N,
+                   "parallelism": f"scenario shards over {world} GPU(s)"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 4), "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 5),
+                     "traffic": traffic,
+                     "kernel": "pdhg_kernel (fp64 VALU; fp64 vector peak == fp64 matrix peak on MI355X)",
+                     "flops_per_pdhg_iter_per_scen": f_it,
+                     "pdhg_iters_per_scen_per_step": round(pdhg_iters / args.steps / S_loc, 2),
+                     "max_pdhg_iters": max_iters,
+                     "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
+        "roofline_ph_update": {"bound": "hbm", "achieved": round(ph_gbs, 2), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(ph_gbs / HBM_PEAK_GBS, 5),
+                               "bytes_per_launch": ph_bytes, "avg_ms": round(upd_ms / args.steps, 4)},
+        "setup_s": round(t_setup, 3),
+        "iter0_s": round(t_iter0, 4),
+        "conv_at_end": conv,
+    }
+    if rank == 0:
+        print("[bench] timed region done", file=sys.stderr, flush=True)
+
+    # wall time to PH convergence < 1e-4 (fresh run, same instance)
+    if args.conv_iters > 0:
+        ph2 = PH(dict(opts, PHIterLimit=args.conv_iters, convthresh=1e-4,
+                      time_limit=args.conv_time), names, farmer.scenario_creator, mpicomm=comm,
+                 scenario_creator_kwargs={"crops_multiplier": args.cm, "num_scens": S})
+        ph2.PH_Prep()
+        torch.cuda.synchronize()
+        if comm is not None:
+            comm.barrier()
+        tc = time.perf_counter()
+        conv2, _, tb2 = ph2.ph_main(finalize=False)
+        torch.cuda.synchronize()
+        tc = time.perf_counter() - tc
+        out["time_to_conv"] = {"seconds": round(tc, 3), "ph_iters": ph2._PHIter, "conv": conv2,
+                               "converged": bool(conv2 is not None and conv2 < 1e-4),
+                               "trivial_bound": tb2, "cap_iters": args.conv_iters, "cap_s": args.conv_time}
+        ph2.engine.close()
+
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(ph, args)
+        if out["cpu_baseline"].get("value"):
+            out["cpu_baseline"]["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _cpu_worker(payload):
+    """Solve scenario prox-QPs with HiGHS (oracle restatement, threads=1) until the time budget."""
+    import time as _t
+    sys.path.insert(0, ROOT)
+    from oracle import highs
+    from oracle import models as om
+    names, cm, S, W, xbar, rho, budget = payload
+    cnt = 0
+    t0 = _t.perf_counter()
+    for k, nm in enumerate(names):
+        sc = om.farmer(nm, crops_multiplier=cm, num_scens=S)
+        a = sc.arrays()
+        cols = np.array(sc.nonant_cols())
+        c = a["c"].copy()
+        c[cols] += W[k] - rho * xbar
+        q = np.zeros_like(c)
+        q[cols] = rho
+        t1 = _t.perf_counter()
+        highs.solve(c, a["rowptr"], a["colidx"], a["vals"], a["row_lo"], a["row_hi"], a["col_lo"],
+                    a["col_hi"], qdiag=q, offset=float(np.sum(rho / 2 * xbar * xbar)), do_polish=False)
+        cnt += 1
+        if _t.perf_counter() - t0 > budget:
+            break
+    return cnt, _t.perf_counter() - t0
+
+
+def cpu_baseline(ph, args):
+    """The reference's CPU path restated (oracle): one HiGHS QP solve per scenario, P processes,
+    on the same W / xbar the GPU just used; bounded sample."""
+    import multiprocessing as mp
+    from mpisppy_amd import _lib
+    try:
+        P = max(1, min(len(os.sched_getaffinity(0)), 16))
+        eng = ph.engine
+        W = eng.get(_lib.F_W).reshape(eng.S, eng.N)
+        xbar = eng.get(_lib.F_XBAR)
+        names = ph.local_scenario_names
+        per = max(1, len(names) // P)
+        payloads = [(names[i * per:(i + 1) * per], args.cm, len(ph.all_scenario_names), W[i * per:(i + 1) * per], xbar,
+                     args.rho, args.cpu_seconds) for i in range(P)]
+        ctx = mp.get_context("spawn")
+        with ctx.Pool(P) as pool:
+            res = pool.map(_cpu_worker, payloads)
+        n = sum(r[0] for r in res)
+        t = max(r[1] for r in res)
+        return {"value": round(n / t, 2), "unit": "scenario-QP solves/s", "cores": P, "kind": "port",
+                "sample": f"{n} farmer cm={args.cm} prox-QPs (HiGHS 1.8 via scipy, threads=1 each) "
+                          f"on {P} processes for ~{args.cpu_seconds:.0f} s, same W/xbar as the GPU step; "
+                          "excludes Pyomo model/objective overhead (lower bound on mpi-sppy CPU time)"}
+    except Exception as e:  # the baseline must never sink the GPU measurement
+        return {"value": None, "error": repr(e)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/*
+ * phg.h -- C ABI of the MI355X (gfx950) Progressive Hedging engine (libphg.so).
+ *
+ * Replaces, for a batch of scenario subproblems held on one GPU:
+ *   - the per-scenario external-solver loop     SPOpt.solve_loop / solve_one
+ *                                               (mpisppy/spopt.py:250-341, :99-247)
+ *   - PHBase._Compute_Xbar                      (mpisppy/phbase.py:32-112)
+ *   - PHBase.Update_W                           (mpisppy/phbase.py:301-326)
+ *   - PHBase.convergence_diff                   (mpisppy/phbase.py:349-371)
+ *   - the per-scenario bound/objective bookkeeping read by Ebound / Eobjective
+ *                                               (mpisppy/spopt.py:225-230, :344-422)
+ *
+ * Conventions
+ *   - return 0 on success, < 0 on error; phg_last_error() gives a thread-local message.
+ *   - host arrays are caller-owned and copied in; device memory is owned by the handle.
+ *   - all work is ordered on one HIP stream (the handle's own, or one given with
+ *     phg_set_stream, e.g. torch.cuda.current_stream()); a handle is not thread-safe.
+ *   - "dev_*" pointer arguments are DEVICE pointers (e.g. a torch CUDA tensor's data_ptr) used
+ *     for the cross-GPU exchange buffers; every other pointer is a host pointer.
+ *   - all floating point is IEEE fp64.
+ */
+#ifndef PHG_H
+#define PHG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct phg_handle phg_handle;
+
+/* A batch of S scenario LPs in standard form sharing one sparsity pattern:
+ *     min/max c_s^T x  s.t.  row_lo_s <= A_s x <= row_hi_s,  col_lo_s <= x <= col_hi_s
+ * plus the scenario-tree index maps (mpisppy/spbase.py:297-395).  Infinite bounds are +-HUGE_VAL.
+ * The xbar vector holds one block per non-leaf tree node: node g's block starts at node_off[g]
+ * and has level_len[level of g] entries; the xbar slot of nonant k of scenario s is
+ *     node_off[scen_node[s*L + nonant_level[k]]] + nonant_pos[k].                           */
+typedef struct phg_batch {
+    int32_t S, n, m, nnz;
+    const int32_t* rowptr;        /* [m+1] CSR row pointers, shared by all scenarios   */
+    const int32_t* colidx;        /* [nnz] column indices, sorted within each row      */
+    const double*  vals;          /* [S*nnz] values, CSR order, per scenario           */
+    const double*  c;             /* [S*n] objective, in the model's own sense         */
+    const double*  col_lo;        /* [S*n] */
+    const double*  col_hi;        /* [S*n] */
+    const double*  row_lo;        /* [S*m] */
+    const double*  row_hi;        /* [S*m] */
+    const double*  obj_offset;    /* [S] constant objective term (may be NULL)          */
+    int32_t sense;                /* +1 minimize, -1 maximize                           */
+    /* scenario tree (non-leaf nodes only, as in mpi-sppy) */
+    int32_t N;                    /* nonants per scenario                               */
+    const int32_t* nonant_col;    /* [N] column of each nonant (same for all scenarios) */
+    int32_t L;                    /* non-leaf levels (1 for two-stage)                  */
+    const int32_t* nonant_level;  /* [N] */
+    const int32_t* nonant_pos;    /* [N] position inside the node's block               */
+    const int32_t* level_len;     /* [L] nonants per node at each level                 */
+    const int32_t* scen_node;     /* [S*L] global node id of scenario s at level l       */
+    int32_t n_nodes;              /* non-leaf nodes in the WHOLE tree (all ranks)        */
+    const int32_t* node_off;      /* [n_nodes] */
+    int32_t N_tot;                /* length of the xbar vector                          */
+    const double*  prob;          /* [S] scenario probabilities                         */
+    const double*  prob_coeff;    /* [S*L] p_s / P(node)  (spbase.py:382-395)            */
+    /* rank slicing of the reference run whose convergence metric is reproduced
+     * (phbase.py:349-371 averages per-rank means): scenario s of this batch is global
+     * scenario scen_global0 + s of S_global, sliced over virt_nproc ranks
+     * (sputils.py:819-826).                                                                */
+    int32_t scen_global0;
+    int32_t S_global;
+    int32_t virt_nproc;
+} phg_batch;
+
+typedef struct phg_opts {
+    double  eps_rel;       /* relative KKT tolerance (PDLP-style), e.g. 1e-9            */
+    int32_t max_iter;      /* PDHG iteration limit per scenario                         */
+    int32_t check_every;   /* iterations between restart/termination checks (e.g. 64)   */
+    int32_t warm_start;    /* 1: start from the previous solution (x, y, primal weight) */
+    int32_t fix_nonants;   /* 1: nonants fixed to the values set by phg_set_fixed (xhat) */
+} phg_opts;
+
+/* solve modes (mpisppy/phbase.py:670-760: W_on / prox_on toggles) */
+enum { PHG_W_OFF = 0, PHG_W_ON = 1 };
+enum { PHG_PROX_OFF = 0, PHG_PROX_ON = 1 };
+
+/* fields for phg_get / phg_set (host copies) */
+enum {
+    PHG_F_X = 0,        /* [S*n]  primal solution, unscaled                                 */
+    PHG_F_Y = 1,        /* [S*m]  row duals (min-form sign convention: >= 0 at lower bound) */
+    PHG_F_XN = 2,       /* [S*N]  nonant values (PH x), unscaled                           */
+    PHG_F_W = 3,        /* [S*N]  PH dual weights                                          */
+    PHG_F_RHO = 4,      /* [S*N]  PH penalties                                             */
+    PHG_F_XBAR = 5,     /* [N_tot] node averages                                           */
+    PHG_F_XSQBAR = 6,   /* [N_tot] node averages of x^2                                    */
+    PHG_F_OBJ = 7,      /* [S] primal objective of the last solve, model sense, incl. W/prox */
+    PHG_F_BOUND = 8,    /* [S] dual (outer) bound of the last solve, model sense           */
+    PHG_F_EVAL = 9,     /* [S] objective evaluated by phg_eval_objective                  */
+    PHG_F_KKT = 10,     /* [S] final relative KKT error                                    */
+    PHG_F_FIXED = 11,   /* [S*N] values nonants are fixed to when opts.fix_nonants         */
+    PHG_F_CONV_PART = 12/* [2*virt_nproc] per-virtual-rank (sum |x-xbar|, count)            */
+};
+enum {
+    PHG_I_ITERS = 0,    /* [S] PDHG iterations of the last solve                           */
+    PHG_I_STATUS = 1    /* [S] 0 optimal (KKT <= eps), 1 iteration limit, 2 numerical error */
+};
+
+int  phg_create(int device, phg_handle** out);
+void phg_destroy(phg_handle* h);
+const char* phg_last_error(void);
+int  phg_set_stream(phg_handle* h, void* hip_stream);
+int  phg_sync(phg_handle* h);
+
+int  phg_load_batch(phg_handle* h, const phg_batch* b);
+int  phg_set(phg_handle* h, int32_t field, const double* host_in);
+int  phg_get(phg_handle* h, int32_t field, double* host_out);
+int  phg_get_i32(phg_handle* h, int32_t field, int32_t* host_out);
+int  phg_info(phg_handle* h, int32_t* out8);   /* S, n, m, nnz, N, N_tot, kernel variant, lanes */
+
+/* Solve every scenario's subproblem (solve_loop):
+ *   min-form  c^T x + w_on * sum_k W_k x_k + prox_on * sum_k rho_k/2 (x_k - xbar_k)^2      */
+int  phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* opts);
+
+/* PH update, split for an external (RCCL / torch.distributed) all-reduce between steps:
+ *   1. phg_node_sums   : dev_nodesum[2*N_tot] <- local sums of prob_coeff*x, prob_coeff*x^2
+ *   2. (all-reduce SUM of dev_nodesum across GPUs)
+ *   3. phg_apply_xbar  : xbar <- nodesum; W += rho (x - xbar); dev_convpart[2*virt_nproc]
+ *   4. (all-reduce SUM of dev_convpart across GPUs)
+ *   5. phg_conv_finish : conv = (1/P) sum_v sum_v/count_v
+ * phg_ph_update does 1-5 on one GPU (no exchange).                                          */
+int  phg_node_sums(phg_handle* h, double* dev_nodesum);
+int  phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpart);
+int  phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_conv);
+int  phg_ph_update(phg_handle* h, double* host_conv);
+
+/* per-scenario objective with the CURRENT W/xbar/rho (pyo.value(objfct), spopt.py:365) */
+int  phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on);
+
+/* elapsed milliseconds (HIP events on the handle's stream) of the last phg_solve launch
+ * (which = 0) or of the last node-sum + W-update launches (which = 1) */
+int  phg_last_ms(phg_handle* h, int32_t which, double* ms);
+
+/* device pointer of the handle's own exchange buffers (2*N_tot and 2*virt_nproc doubles) */
+int  phg_exchange_buffers(phg_handle* h, double** dev_nodesum, double** dev_convpart);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHG_H */

@@ -1,0 +1,106 @@
+"""ctypes binding of libphg.so (include/phg.h).
+
+The library is built in-tree (``mpi-sppy_amd/libphg.so``, see ``__graft_entry__.build``).  There is
+deliberately NO fallback: if the shared object is missing or no HIP device is present, importing
+the engine's solver raises -- the product path never computes on the CPU.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PHG_LIB", os.path.join(_HERE, "libphg.so"))
+
+i32p = C.POINTER(C.c_int32)
+f64p = C.POINTER(C.c_double)
+
+
+class PhgBatch(C.Structure):
+    _fields_ = [
+        ("S", C.c_int32), ("n", C.c_int32), ("m", C.c_int32), ("nnz", C.c_int32),
+        ("rowptr", i32p), ("colidx", i32p), ("vals", f64p), ("c", f64p),
+        ("col_lo", f64p), ("col_hi", f64p), ("row_lo", f64p), ("row_hi", f64p),
+        ("obj_offset", f64p), ("sense", C.c_int32),
+        ("N", C.c_int32), ("nonant_col", i32p), ("L", C.c_int32), ("nonant_level", i32p),
+        ("nonant_pos", i32p), ("level_len", i32p), ("scen_node", i32p), ("n_nodes", C.c_int32),
+        ("node_off", i32p), ("N_tot", C.c_int32), ("prob", f64p), ("prob_coeff", f64p),
+        ("scen_global0", C.c_int32), ("S_global", C.c_int32), ("virt_nproc", C.c_int32),
+    ]
+
+
+class PhgOpts(C.Structure):
+    _fields_ = [("eps_rel", C.c_double), ("max_iter", C.c_int32), ("check_every", C.c_int32),
+                ("warm_start", C.c_int32), ("fix_nonants", C.c_int32)]
+
+
+F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART = range(13)
+I_ITERS, I_STATUS = 0, 1
+
+# every symbol include/phg.h declares, with its ctypes signature
+SIGNATURES = {
+    "phg_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "phg_destroy": (None, [C.c_void_p]),
+    "phg_last_error": (C.c_char_p, []),
+    "phg_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "phg_sync": (C.c_int, [C.c_void_p]),
+    "phg_load_batch": (C.c_int, [C.c_void_p, C.POINTER(PhgBatch)]),
+    "phg_set": (C.c_int, [C.c_void_p, C.c_int32, f64p]),
+    "phg_get": (C.c_int, [C.c_void_p, C.c_int32, f64p]),
+    "phg_get_i32": (C.c_int, [C.c_void_p, C.c_int32, i32p]),
+    "phg_info": (C.c_int, [C.c_void_p, i32p]),
+    "phg_solve": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(PhgOpts)]),
+    "phg_node_sums": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "phg_apply_xbar": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "phg_conv_finish": (C.c_int, [C.c_void_p, C.c_void_p, f64p]),
+    "phg_ph_update": (C.c_int, [C.c_void_p, f64p]),
+    "phg_eval_objective": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "phg_exchange_buffers": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "phg_last_ms": (C.c_int, [C.c_void_p, C.c_int32, f64p]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libphg.so and bind every exported symbol (raises if missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libphg.so not found at {LIB_PATH}: build it with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class PhgError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc != 0:
+        raise PhgError(load().phg_last_error().decode())
+
+
+def as_f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def as_i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def ptr(a):
+    if a is None:
+        return None
+    if a.dtype == np.float64:
+        return a.ctypes.data_as(f64p)
+    if a.dtype == np.int32:
+        return a.ctypes.data_as(i32p)
+    raise TypeError(a.dtype)

@@ -1,0 +1,85 @@
+"""Communicators for the PH engine (restates the role of ``mpisppy/MPI.py:10-90``).
+
+The reference moves per-node xbar sums and the convergence partials with mpi4py ``Allreduce``
+(``phbase.py:88-92, :369``; ``spopt.py:372, 417, 435, 466``).  Here one process drives one GPU and
+the same SUM reductions run through ``torch.distributed``: backend ``nccl`` (= RCCL over xGMI on
+ROCm) on device tensors, ``gloo`` on host tensors (CPU tests).  ``SingleComm`` is the 1-rank mock
+(the reference's fallback when mpi4py is absent, ``MPI.py:14-90``).
+"""
+import numpy as np
+
+
+class SingleComm:
+    rank = 0
+    size = 1
+
+    def Get_rank(self):
+        return 0
+
+    def Get_size(self):
+        return 1
+
+    def allreduce_sum_(self, t):
+        return t
+
+    def allreduce_scalar(self, v):
+        return float(v)
+
+    def allreduce_array(self, a):
+        return np.asarray(a, dtype=np.float64)
+
+    def barrier(self):
+        pass
+
+    Barrier = barrier
+
+    def bcast_object(self, obj, root=0):
+        return obj
+
+
+class TorchComm:
+    """SUM all-reduces over an initialised ``torch.distributed`` process group."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            raise RuntimeError("TorchComm needs torch.distributed.init_process_group first")
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.size = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+
+    def Get_rank(self):
+        return self.rank
+
+    def Get_size(self):
+        return self.size
+
+    def allreduce_sum_(self, t):
+        """In-place SUM of a torch tensor (device tensor under nccl/RCCL, host under gloo)."""
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def _scratch(self, a):
+        import torch
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        return torch.as_tensor(np.asarray(a, dtype=np.float64)).to(dev)
+
+    def allreduce_array(self, a):
+        t = self._scratch(a)
+        self.allreduce_sum_(t)
+        return t.cpu().numpy()
+
+    def allreduce_scalar(self, v):
+        return float(self.allreduce_array(np.array([v]))[0])
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+    Barrier = barrier
+
+    def bcast_object(self, obj, root=0):
+        lst = [obj]
+        self.dist.broadcast_object_list(lst, src=root, group=self.group)
+        return lst[0]

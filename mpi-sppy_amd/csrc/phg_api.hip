@@ -1,0 +1,581 @@
+// phg_api.hip -- host side of the C ABI declared in include/phg.h.
+//
+// Owns the device memory of one scenario batch on one GPU, builds the per-lane ownership layout
+// of the PDHG kernel from the shared sparsity pattern, the node / virtual-rank segment tables of
+// the PH update kernels, and orders every launch on one HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/phg.h"
+#include "phg_internal.h"
+
+namespace phg {
+int pdhg_num_variants();
+void pdhg_variant_shape(int v, int* out6);
+hipError_t pdhg_launch(int v, const PdhgArgs& a, hipStream_t stream);
+hipError_t prep_launch(const PrepArgs& a, hipStream_t stream);
+hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
+hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
+hipError_t eval_obj_launch(int S, int n, int N, const double* x, const double* c, const double* obj_off,
+                           const int* nonant_col, const double* xN, const double* W, const double* rho,
+                           const double* xbar, const int* xidx, int w_on, int prox_on, double sense,
+                           double* out, hipStream_t st);
+}  // namespace phg
+
+using namespace phg;
+
+static thread_local std::string g_err;
+
+static int fail(const std::string& msg) {
+    g_err = msg;
+    return -1;
+}
+
+#define CK(call)                                                                              \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(std::string(#call) + ": " + hipGetErrorString(e_));                   \
+    } while (0)
+
+struct phg_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool loaded = false;
+    int S = 0, n = 0, m = 0, nnz = 0, N = 0, L = 0, N_tot = 0, n_nodes = 0, P = 1, n_pad = 0;
+    double sense = 1.0;
+    int variant = -1;
+    int vshape[6] = {0};
+    std::vector<void*> allocs;
+    // device arrays
+    double *vals = nullptr, *c = nullptr, *cl = nullptr, *cu = nullptr, *rl = nullptr, *ru = nullptr;
+    double *dc = nullptr, *dr = nullptr, *eta = nullptr, *bnorm = nullptr, *obj_off = nullptr;
+    double *W = nullptr, *rho = nullptr, *xbar = nullptr, *xsqbar = nullptr, *fixed = nullptr;
+    int* xidx = nullptr;
+    double *xs = nullptr, *ys = nullptr, *omega = nullptr, *x_out = nullptr, *y_out = nullptr;
+    double *xN = nullptr, *obj = nullptr, *bound = nullptr, *kkt = nullptr, *eval = nullptr;
+    int *iters = nullptr, *status = nullptr;
+    int* nonant_col_d = nullptr;
+    Layout lay{};
+    PhArgs ph{};
+    double *nodesum = nullptr, *convpart = nullptr;
+    std::vector<int> nonant_col_h;
+    // timing of the last launches (HIP events on the handle's stream)
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+template <class T>
+static int dalloc(phg_handle* h, T** p, size_t count) {
+    void* q = nullptr;
+    if (count == 0) count = 1;
+    CK(hipMalloc(&q, count * sizeof(T)));
+    CK(hipMemsetAsync(q, 0, count * sizeof(T), h->stream));
+    h->allocs.push_back(q);
+    *p = (T*)q;
+    return 0;
+}
+
+template <class T>
+static int dput(phg_handle* h, T** p, const T* src, size_t count) {
+    if (dalloc(h, p, count)) return -1;
+    if (src) CK(hipMemcpyAsync(*p, src, count * sizeof(T), hipMemcpyHostToDevice, h->stream));
+    return 0;
+}
+
+extern "C" {
+
+const char* phg_last_error(void) { return g_err.c_str(); }
+
+int phg_create(int device, phg_handle** out) {
+    if (!out) return fail("phg_create: out is NULL");
+    int ndev = 0;
+    CK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail("phg_create: bad device index");
+    CK(hipSetDevice(device));
+    phg_handle* h = new phg_handle();
+    h->device = device;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail("phg_create: hipStreamCreate failed");
+    }
+    h->own_stream = true;
+    for (auto& e : h->ev) CK(hipEventCreate(&e));
+    *out = h;
+    return 0;
+}
+
+void phg_destroy(phg_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    for (void* p : h->allocs) (void)hipFree(p);
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->own_stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int phg_set_stream(phg_handle* h, void* s) {
+    if (!h) return fail("null handle");
+    CK(hipSetDevice(h->device));
+    if (h->own_stream) {
+        CK(hipStreamSynchronize(h->stream));
+        CK(hipStreamDestroy(h->stream));
+        h->own_stream = false;
+    }
+    h->stream = (hipStream_t)s;
+    return 0;
+}
+
+int phg_sync(phg_handle* h) {
+    if (!h) return fail("null handle");
+    CK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+// ------------------------------------------------------------------------------ batch loading
+static int build_layout(phg_handle* h, const phg_batch* b, const std::vector<int>& colptr,
+                        const std::vector<int>& csc_row, const std::vector<int>& csc_p) {
+    const int n = b->n, m = b->m;
+    int kcs_need = 0;
+    for (int j = 0; j < n; ++j) kcs_need = std::max(kcs_need, colptr[j + 1] - colptr[j]);
+    const int cpl_need = (n + 63) / 64, rpl_need = (m + 63) / 64;
+    int chosen = -1;
+    int sh[6];
+    for (int v = 0; v < pdhg_num_variants(); ++v) {
+        pdhg_variant_shape(v, sh);
+        const int CPL = sh[0], KCS = sh[1], RPL = sh[2], KRS = sh[3], D = sh[4], KD = sh[5];
+        if (CPL < cpl_need || RPL < rpl_need || KCS < kcs_need) continue;
+        int nd = 0, maxd = 0;
+        for (int i = 0; i < m; ++i) {
+            const int len = b->rowptr[i + 1] - b->rowptr[i];
+            if (len > KRS) { ++nd; maxd = std::max(maxd, len); }
+        }
+        if (nd > D || (maxd + 63) / 64 > KD) continue;
+        chosen = v;
+        break;
+    }
+    if (chosen < 0) {
+        char msg[256];
+        snprintf(msg, sizeof msg,
+                 "phg_load_batch: no PDHG kernel variant fits n=%d m=%d max col nnz=%d "
+                 "(wave-per-scenario variants cover n,m <= 256)", n, m, kcs_need);
+        return fail(msg);
+    }
+    pdhg_variant_shape(chosen, sh);
+    const int CPL = sh[0], KCS = sh[1], RPL = sh[2], KRS = sh[3], D = sh[4], KD = sh[5];
+    h->variant = chosen;
+    std::memcpy(h->vshape, sh, sizeof sh);
+    std::vector<int> col_of(64 * CPL, -1), cent_p(64 * CPL * KCS, -1), cent_row(64 * CPL * KCS, 0);
+    for (int j = 0; j < n; ++j) {
+        const int ln = j % 64, sl = j / 64;
+        col_of[ln * CPL + sl] = j;
+        int t = 0;
+        for (int e = colptr[j]; e < colptr[j + 1]; ++e, ++t) {
+            cent_p[(ln * CPL + sl) * KCS + t] = csc_p[e];
+            cent_row[(ln * CPL + sl) * KCS + t] = csc_row[e];
+        }
+    }
+    std::vector<int> row_of(64 * RPL, -1), row_dense(64 * RPL, -1), rent_p(64 * RPL * KRS, -1),
+        rent_col(64 * RPL * KRS, 0);
+    std::vector<int> dent_p(std::max(1, D * 64 * KD), -1), dent_col(std::max(1, D * 64 * KD), 0);
+    int nd = 0;
+    for (int i = 0; i < m; ++i) {
+        const int ln = i % 64, sl = i / 64;
+        row_of[ln * RPL + sl] = i;
+        const int len = b->rowptr[i + 1] - b->rowptr[i];
+        if (len > KRS) {
+            row_dense[ln * RPL + sl] = nd;
+            for (int e = 0; e < len; ++e) {
+                const int p = b->rowptr[i] + e;
+                const int dl = e % 64, t = e / 64;
+                dent_p[(nd * 64 + dl) * KD + t] = p;
+                dent_col[(nd * 64 + dl) * KD + t] = b->colidx[p];
+            }
+            ++nd;
+        } else {
+            for (int e = 0; e < len; ++e) {
+                const int p = b->rowptr[i] + e;
+                rent_p[(ln * RPL + sl) * KRS + e] = p;
+                rent_col[(ln * RPL + sl) * KRS + e] = b->colidx[p];
+            }
+        }
+    }
+    std::vector<int> col_nonant(n, -1);
+    for (int k = 0; k < b->N; ++k) col_nonant[b->nonant_col[k]] = k;
+    int* p;
+    if (dput(h, &p, col_of.data(), col_of.size())) return -1; h->lay.col_of = p;
+    if (dput(h, &p, cent_p.data(), cent_p.size())) return -1; h->lay.cent_p = p;
+    if (dput(h, &p, cent_row.data(), cent_row.size())) return -1; h->lay.cent_row = p;
+    if (dput(h, &p, row_of.data(), row_of.size())) return -1; h->lay.row_of = p;
+    if (dput(h, &p, row_dense.data(), row_dense.size())) return -1; h->lay.row_dense = p;
+    if (dput(h, &p, rent_p.data(), rent_p.size())) return -1; h->lay.rent_p = p;
+    if (dput(h, &p, rent_col.data(), rent_col.size())) return -1; h->lay.rent_col = p;
+    if (dput(h, &p, dent_p.data(), dent_p.size())) return -1; h->lay.dent_p = p;
+    if (dput(h, &p, dent_col.data(), dent_col.size())) return -1; h->lay.dent_col = p;
+    if (dput(h, &p, col_nonant.data(), col_nonant.size())) return -1; h->lay.col_nonant = p;
+    return 0;
+}
+
+static int build_ph_tables(phg_handle* h, const phg_batch* b) {
+    const int S = b->S, N = b->N, L = b->L;
+    // level offsets: nonants must be grouped by level in node-list order
+    std::vector<int> level_kofs(L, -1);
+    for (int k = 0; k < N; ++k) {
+        const int lv = b->nonant_level[k];
+        if (lv < 0 || lv >= L) return fail("phg_load_batch: nonant_level out of range");
+        if (level_kofs[lv] < 0) level_kofs[lv] = k;
+        if (k > 0 && b->nonant_level[k] < b->nonant_level[k - 1])
+            return fail("phg_load_batch: nonants must be ordered by tree level");
+        if (b->nonant_pos[k] != k - level_kofs[lv]) return fail("phg_load_batch: nonant_pos mismatch");
+    }
+    int maxk = 1;
+    for (int lv = 0; lv < L; ++lv) maxk = std::max(maxk, b->level_len[lv]);
+    std::vector<int> node_level(b->n_nodes, -1);
+    for (int s = 0; s < S; ++s)
+        for (int lv = 0; lv < L; ++lv) {
+            const int g = b->scen_node[s * L + lv];
+            if (g < 0 || g >= b->n_nodes) return fail("phg_load_batch: scen_node out of range");
+            node_level[g] = lv;
+        }
+    for (int g = 1; g < b->n_nodes; ++g)
+        if (b->node_off[g] < b->node_off[g - 1]) return fail("phg_load_batch: node_off must increase");
+    // node segments: contiguous scenario ranges per node, chunked
+    std::vector<std::vector<NodeSeg>> per_node(b->n_nodes);
+    for (int lv = 0; lv < L; ++lv) {
+        const int klen = b->level_len[lv];
+        const int chunk = std::max(1, 8192 / std::max(1, klen));
+        int s = 0;
+        while (s < S) {
+            const int g = b->scen_node[s * L + lv];
+            if (!per_node[g].empty() && per_node[g].back().s1 != s)
+                return fail("phg_load_batch: scenarios of a tree node must be contiguous");
+            int e = s;
+            while (e < S && b->scen_node[e * L + lv] == g && e - s < chunk) ++e;
+            per_node[g].push_back(NodeSeg{lv, g, s, e, level_kofs[lv], klen, 0});
+            s = e;
+        }
+    }
+    std::vector<NodeSeg> segs;
+    std::vector<int> first(b->n_nodes + 1, 0);
+    for (int g = 0; g < b->n_nodes; ++g) {
+        first[g] = (int)segs.size();
+        for (auto& sg : per_node[g]) segs.push_back(sg);
+    }
+    first[b->n_nodes] = (int)segs.size();
+    // conv segments: virtual-rank slices of the global scenario list (sputils.py:819-826)
+    const int P = std::max(1, b->virt_nproc);
+    const int Sg = b->S_global > 0 ? b->S_global : S;
+    std::vector<int> vr(S, 0);
+    if (P > 1) {
+        const double avg = (double)Sg / (double)P;
+        for (int s = 0; s < S; ++s) {
+            const int gs = b->scen_global0 + s;
+            int v = 0;
+            while (v + 1 < P && gs >= (int)((v + 1) * avg)) ++v;
+            vr[s] = v;
+        }
+    }
+    std::vector<int> cv, cs0, cs1, vfirst(P + 1, 0);
+    const int cchunk = std::max(1, 8192 / std::max(1, N));
+    {
+        int s = 0;
+        std::vector<std::vector<int>> tmp0(P), tmp1(P);
+        while (s < S) {
+            const int v = vr[s];
+            int e = s;
+            while (e < S && vr[e] == v && e - s < cchunk) ++e;
+            tmp0[v].push_back(s);
+            tmp1[v].push_back(e);
+            s = e;
+        }
+        for (int v = 0; v < P; ++v) {
+            vfirst[v] = (int)cv.size();
+            for (size_t i = 0; i < tmp0[v].size(); ++i) {
+                cv.push_back(v);
+                cs0.push_back(tmp0[v][i]);
+                cs1.push_back(tmp1[v][i]);
+            }
+        }
+        vfirst[P] = (int)cv.size();
+    }
+    // xbar slot of (s, k)
+    std::vector<int> xidx((size_t)S * N);
+    for (int s = 0; s < S; ++s)
+        for (int k = 0; k < N; ++k)
+            xidx[(size_t)s * N + k] = b->node_off[b->scen_node[s * L + b->nonant_level[k]]] + b->nonant_pos[k];
+    PhArgs& a = h->ph;
+    a.S = S; a.N = N; a.N_tot = b->N_tot; a.L = L; a.P = P; a.maxk = maxk; a.n_nodes = b->n_nodes;
+    a.n_seg = (int)segs.size();
+    a.n_cseg = (int)cv.size();
+    {
+        NodeSeg* p;
+        if (dput(h, &p, segs.data(), segs.size())) return -1;
+        a.seg = p;
+    }
+    int* ip;
+    double* dp;
+    if (dalloc(h, &dp, (size_t)segs.size() * 2 * maxk)) return -1; a.segpart = dp;
+    if (dput(h, &ip, first.data(), first.size())) return -1; a.node_first_seg = ip;
+    if (dput(h, &ip, b->node_off, b->n_nodes)) return -1; a.node_off = ip;
+    if (dput(h, &ip, node_level.data(), node_level.size())) return -1; a.node_level = ip;
+    if (dput(h, &ip, b->level_len, L)) return -1; a.level_len = ip;
+    if (dput(h, &ip, level_kofs.data(), L)) return -1; a.level_kofs = ip;
+    if (dput(h, &ip, b->nonant_level, N)) return -1; a.nonant_level = ip;
+    if (dput(h, &dp, b->prob_coeff, (size_t)S * L)) return -1; a.pc = dp;
+    if (dput(h, &ip, cv.data(), cv.size())) return -1; a.cseg_v = ip;
+    if (dput(h, &ip, cs0.data(), cs0.size())) return -1; a.cseg_s0 = ip;
+    if (dput(h, &ip, cs1.data(), cs1.size())) return -1; a.cseg_s1 = ip;
+    if (dalloc(h, &dp, cv.size())) return -1; a.csegpart = dp;
+    if (dput(h, &ip, vfirst.data(), vfirst.size())) return -1; a.vr_first = ip;
+    if (dput(h, &ip, xidx.data(), xidx.size())) return -1; h->xidx = ip;
+    a.xidx = h->xidx;
+    if (dalloc(h, &h->nodesum, 2 * (size_t)b->N_tot)) return -1;
+    if (dalloc(h, &h->convpart, 2 * (size_t)P)) return -1;
+    return 0;
+}
+
+int phg_load_batch(phg_handle* h, const phg_batch* b) {
+    if (!h || !b) return fail("phg_load_batch: null argument");
+    if (h->loaded) return fail("phg_load_batch: handle already holds a batch");
+    if (b->S <= 0 || b->n <= 0 || b->m <= 0 || b->nnz <= 0 || b->N <= 0 || b->L <= 0)
+        return fail("phg_load_batch: empty batch");
+    if (b->rowptr[0] != 0 || b->rowptr[b->m] != b->nnz) return fail("phg_load_batch: bad rowptr");
+    for (int i = 0; i < b->m; ++i) {
+        if (b->rowptr[i + 1] < b->rowptr[i]) return fail("phg_load_batch: rowptr not monotone");
+        for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) {
+            if (b->colidx[p] < 0 || b->colidx[p] >= b->n) return fail("phg_load_batch: colidx out of range");
+            if (p > b->rowptr[i] && b->colidx[p] <= b->colidx[p - 1])
+                return fail("phg_load_batch: colidx must be strictly increasing inside a row");
+        }
+    }
+    for (int k = 0; k < b->N; ++k)
+        if (b->nonant_col[k] < 0 || b->nonant_col[k] >= b->n) return fail("phg_load_batch: nonant_col out of range");
+    CK(hipSetDevice(h->device));
+    const int S = b->S, n = b->n, m = b->m, nnz = b->nnz, N = b->N;
+    h->S = S; h->n = n; h->m = m; h->nnz = nnz; h->N = N; h->L = b->L; h->N_tot = b->N_tot;
+    h->n_nodes = b->n_nodes; h->P = std::max(1, b->virt_nproc);
+    h->n_pad = (n + 1) & ~1;
+    h->sense = b->sense >= 0 ? 1.0 : -1.0;
+    // CSC of the shared pattern
+    std::vector<int> colptr(n + 1, 0), csc_row(nnz), csc_p(nnz), row_of_p(nnz);
+    for (int p = 0; p < nnz; ++p) colptr[b->colidx[p] + 1]++;
+    for (int j = 0; j < n; ++j) colptr[j + 1] += colptr[j];
+    {
+        std::vector<int> fill(colptr.begin(), colptr.end() - 1);
+        for (int i = 0; i < m; ++i)
+            for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) {
+                const int e = fill[b->colidx[p]]++;
+                csc_row[e] = i;
+                csc_p[e] = p;
+                row_of_p[p] = i;
+            }
+    }
+    if (build_layout(h, b, colptr, csc_row, csc_p)) return -1;
+    // min-form objective
+    std::vector<double> cmin((size_t)S * n), off((size_t)S, 0.0);
+    for (size_t e = 0; e < cmin.size(); ++e) cmin[e] = h->sense * b->c[e];
+    if (b->obj_offset)
+        for (int s = 0; s < S; ++s) off[s] = h->sense * b->obj_offset[s];
+    if (dput(h, &h->vals, b->vals, (size_t)S * nnz)) return -1;
+    if (dput(h, &h->c, cmin.data(), cmin.size())) return -1;
+    if (dput(h, &h->cl, b->col_lo, (size_t)S * n)) return -1;
+    if (dput(h, &h->cu, b->col_hi, (size_t)S * n)) return -1;
+    if (dput(h, &h->rl, b->row_lo, (size_t)S * m)) return -1;
+    if (dput(h, &h->ru, b->row_hi, (size_t)S * m)) return -1;
+    if (dput(h, &h->obj_off, off.data(), S)) return -1;
+    if (dalloc(h, &h->dc, (size_t)S * n)) return -1;
+    if (dalloc(h, &h->dr, (size_t)S * m)) return -1;
+    if (dalloc(h, &h->eta, S)) return -1;
+    if (dalloc(h, &h->bnorm, S)) return -1;
+    if (dalloc(h, &h->W, (size_t)S * N)) return -1;
+    if (dalloc(h, &h->rho, (size_t)S * N)) return -1;
+    if (dalloc(h, &h->fixed, (size_t)S * N)) return -1;
+    if (dalloc(h, &h->xbar, std::max(1, b->N_tot))) return -1;
+    if (dalloc(h, &h->xsqbar, std::max(1, b->N_tot))) return -1;
+    if (dalloc(h, &h->xs, (size_t)S * n)) return -1;
+    if (dalloc(h, &h->ys, (size_t)S * m)) return -1;
+    if (dalloc(h, &h->omega, S)) return -1;
+    if (dalloc(h, &h->x_out, (size_t)S * n)) return -1;
+    if (dalloc(h, &h->y_out, (size_t)S * m)) return -1;
+    if (dalloc(h, &h->xN, (size_t)S * N)) return -1;
+    if (dalloc(h, &h->obj, S)) return -1;
+    if (dalloc(h, &h->bound, S)) return -1;
+    if (dalloc(h, &h->kkt, S)) return -1;
+    if (dalloc(h, &h->eval, S)) return -1;
+    if (dalloc(h, &h->iters, S)) return -1;
+    if (dalloc(h, &h->status, S)) return -1;
+    h->nonant_col_h.assign(b->nonant_col, b->nonant_col + N);
+    if (dput(h, &h->nonant_col_d, b->nonant_col, N)) return -1;
+    if (build_ph_tables(h, b)) return -1;
+    h->ph.xN = h->xN; h->ph.W = h->W; h->ph.rho = h->rho; h->ph.xbar = h->xbar; h->ph.xsqbar = h->xsqbar;
+    // preconditioning
+    PrepArgs pa{};
+    pa.S = S; pa.n = n; pa.m = m; pa.nnz = nnz; pa.ruiz_iters = 10; pa.power_iters = 64;
+    int* ip;
+    if (dput(h, &ip, b->rowptr, m + 1)) return -1; pa.rowptr = ip;
+    if (dput(h, &ip, b->colidx, nnz)) return -1; pa.colidx = ip;
+    if (dput(h, &ip, colptr.data(), n + 1)) return -1; pa.colptr = ip;
+    if (dput(h, &ip, csc_p.data(), nnz)) return -1; pa.csc_p = ip;
+    if (dput(h, &ip, row_of_p.data(), nnz)) return -1; pa.row_of_p = ip;
+    double* scratch;
+    if (dalloc(h, &scratch, (size_t)S * (2 * n + 2 * m))) return -1;
+    pa.vals = h->vals; pa.dc = h->dc; pa.dr = h->dr; pa.cl = h->cl; pa.cu = h->cu; pa.rl = h->rl;
+    pa.ru = h->ru; pa.eta = h->eta; pa.bnorm = h->bnorm; pa.scratch = scratch;
+    CK(prep_launch(pa, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    h->loaded = true;
+    return 0;
+}
+
+int phg_info(phg_handle* h, int32_t* o) {
+    if (!h || !h->loaded) return fail("phg_info: no batch loaded");
+    o[0] = h->S; o[1] = h->n; o[2] = h->m; o[3] = h->nnz; o[4] = h->N; o[5] = h->N_tot;
+    o[6] = h->variant; o[7] = 64;
+    return 0;
+}
+
+static double* field_ptr(phg_handle* h, int f, size_t* count) {
+    const size_t S = h->S, n = h->n, m = h->m, N = h->N;
+    switch (f) {
+        case PHG_F_X: *count = S * n; return h->x_out;
+        case PHG_F_Y: *count = S * m; return h->y_out;
+        case PHG_F_XN: *count = S * N; return h->xN;
+        case PHG_F_W: *count = S * N; return h->W;
+        case PHG_F_RHO: *count = S * N; return h->rho;
+        case PHG_F_XBAR: *count = h->N_tot; return h->xbar;
+        case PHG_F_XSQBAR: *count = h->N_tot; return h->xsqbar;
+        case PHG_F_OBJ: *count = S; return h->obj;
+        case PHG_F_BOUND: *count = S; return h->bound;
+        case PHG_F_EVAL: *count = S; return h->eval;
+        case PHG_F_KKT: *count = S; return h->kkt;
+        case PHG_F_FIXED: *count = S * N; return h->fixed;
+        case PHG_F_CONV_PART: *count = 2 * (size_t)h->P; return h->convpart;
+        default: return nullptr;
+    }
+}
+
+int phg_set(phg_handle* h, int32_t f, const double* in) {
+    if (!h || !h->loaded) return fail("phg_set: no batch loaded");
+    size_t cnt = 0;
+    double* p = field_ptr(h, f, &cnt);
+    if (!p) return fail("phg_set: unknown field");
+    if (f == PHG_F_XBAR) {   // also keep the node-sum buffer consistent
+        CK(hipMemcpyAsync(h->nodesum, in, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    }
+    CK(hipMemcpyAsync(p, in, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int phg_get(phg_handle* h, int32_t f, double* out) {
+    if (!h || !h->loaded) return fail("phg_get: no batch loaded");
+    size_t cnt = 0;
+    double* p = field_ptr(h, f, &cnt);
+    if (!p) return fail("phg_get: unknown field");
+    CK(hipMemcpyAsync(out, p, cnt * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int phg_get_i32(phg_handle* h, int32_t f, int32_t* out) {
+    if (!h || !h->loaded) return fail("phg_get_i32: no batch loaded");
+    int* p = f == PHG_I_ITERS ? h->iters : f == PHG_I_STATUS ? h->status : nullptr;
+    if (!p) return fail("phg_get_i32: unknown field");
+    CK(hipMemcpyAsync(out, p, (size_t)h->S * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
+    if (!h || !h->loaded) return fail("phg_solve: no batch loaded");
+    if (!o) return fail("phg_solve: opts is NULL");
+    if (o->check_every <= 0 || o->max_iter <= 0) return fail("phg_solve: bad iteration options");
+    CK(hipSetDevice(h->device));
+    PdhgArgs a{};
+    a.S = h->S; a.n = h->n; a.m = h->m; a.nnz = h->nnz; a.N = h->N; a.n_pad = h->n_pad;
+    a.lay = h->lay;
+    a.vals = h->vals; a.c = h->c; a.cl = h->cl; a.cu = h->cu; a.rl = h->rl; a.ru = h->ru;
+    a.dc = h->dc; a.dr = h->dr; a.eta = h->eta; a.obj_off = h->obj_off; a.bnorm = h->bnorm;
+    a.W = h->W; a.rho = h->rho; a.xbar = h->xbar; a.xidx = h->xidx; a.fixed = h->fixed;
+    a.xs = h->xs; a.ys = h->ys; a.omega = h->omega;
+    a.x_out = h->x_out; a.y_out = h->y_out; a.xN = h->xN; a.obj = h->obj; a.bound = h->bound;
+    a.kkt = h->kkt; a.iters = h->iters; a.status = h->status;
+    a.w_on = w_on; a.prox_on = prox_on; a.fix_nonants = o->fix_nonants; a.warm = o->warm_start;
+    a.max_iter = o->max_iter; a.check_every = o->check_every; a.eps = o->eps_rel; a.sense = h->sense;
+    CK(hipEventRecord(h->ev[0], h->stream));
+    CK(pdhg_launch(h->variant, a, h->stream));
+    CK(hipEventRecord(h->ev[1], h->stream));
+    return 0;
+}
+
+int phg_node_sums(phg_handle* h, double* dev_nodesum) {
+    if (!h || !h->loaded) return fail("phg_node_sums: no batch loaded");
+    CK(hipSetDevice(h->device));
+    CK(hipEventRecord(h->ev[2], h->stream));
+    CK(node_sums_launch(h->ph, dev_nodesum ? dev_nodesum : h->nodesum, h->stream));
+    return 0;
+}
+
+int phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpart) {
+    if (!h || !h->loaded) return fail("phg_apply_xbar: no batch loaded");
+    CK(hipSetDevice(h->device));
+    CK(w_update_launch(h->ph, dev_nodesum ? dev_nodesum : h->nodesum,
+                       dev_convpart ? dev_convpart : h->convpart, h->stream));
+    CK(hipEventRecord(h->ev[3], h->stream));
+    return 0;
+}
+
+int phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_conv) {
+    if (!h || !h->loaded) return fail("phg_conv_finish: no batch loaded");
+    std::vector<double> cp(2 * (size_t)h->P);
+    CK(hipMemcpyAsync(cp.data(), dev_convpart ? dev_convpart : h->convpart, cp.size() * sizeof(double),
+                      hipMemcpyDeviceToHost, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    double tot = 0.0;
+    for (int v = 0; v < h->P; ++v)
+        if (cp[2 * v + 1] > 0.0) tot += cp[2 * v] / cp[2 * v + 1];
+    *host_conv = tot / (double)h->P;
+    return 0;
+}
+
+int phg_ph_update(phg_handle* h, double* host_conv) {
+    if (phg_node_sums(h, nullptr)) return -1;
+    if (phg_apply_xbar(h, nullptr, nullptr)) return -1;
+    return phg_conv_finish(h, nullptr, host_conv);
+}
+
+int phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on) {
+    if (!h || !h->loaded) return fail("phg_eval_objective: no batch loaded");
+    CK(hipSetDevice(h->device));
+    CK(eval_obj_launch(h->S, h->n, h->N, h->x_out, h->c, h->obj_off, h->nonant_col_d, h->xN, h->W,
+                       h->rho, h->xbar, h->xidx, w_on, prox_on, h->sense, h->eval, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int phg_exchange_buffers(phg_handle* h, double** ns, double** cp) {
+    if (!h || !h->loaded) return fail("phg_exchange_buffers: no batch loaded");
+    if (ns) *ns = h->nodesum;
+    if (cp) *cp = h->convpart;
+    return 0;
+}
+
+// elapsed ms between the events of the last phg_solve (which=0) / PH update (which=1)
+int phg_last_ms(phg_handle* h, int32_t which, double* ms) {
+    if (!h) return fail("null handle");
+    float f = 0.f;
+    CK(hipEventSynchronize(h->ev[which == 0 ? 1 : 3]));
+    CK(hipEventElapsedTime(&f, h->ev[which == 0 ? 0 : 2], h->ev[which == 0 ? 1 : 3]));
+    *ms = f;
+    return 0;
+}
+
+}  // extern "C"

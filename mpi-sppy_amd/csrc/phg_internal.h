@@ -1,0 +1,116 @@
+// phg_internal.h -- device-side structures shared by the PH engine's kernels and host API.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace phg {
+
+// Per-lane ownership tables of the wave-per-scenario PDHG kernel.  Built once per batch on the
+// host from the SHARED sparsity pattern (see phg_api.hip: build_layout):
+//   column j  -> lane j % 64, slot j / 64 ; its CSC entries in that slot (<= KCS)
+//   row i     -> lane i % 64, slot i / 64 ; sparse rows keep their CSR entries (<= KRS) in the
+//                slot, "dense" rows (> KRS entries) are computed cooperatively by the whole wave
+//                (entries dealt round-robin over lanes, <= KD per lane) and reduced with shuffles.
+// Padding entries have p = -1 (value 0, index 0).
+struct Layout {
+    const int* col_of;      // [64*CPL]
+    const int* cent_p;      // [64*CPL*KCS]  CSR position of the entry (values are per scenario)
+    const int* cent_row;    // [64*CPL*KCS]
+    const int* row_of;      // [64*RPL]
+    const int* row_dense;   // [64*RPL]      dense-row id or -1
+    const int* rent_p;      // [64*RPL*KRS]
+    const int* rent_col;    // [64*RPL*KRS]
+    const int* dent_p;      // [D*64*KD]
+    const int* dent_col;    // [D*64*KD]
+    const int* col_nonant;  // [n] nonant index of column j or -1
+};
+
+struct PdhgArgs {
+    int S, n, m, nnz, N, n_pad;
+    Layout lay;
+    // scenario data (scaled where noted)
+    const double* vals;     // [S*nnz] scaled values
+    const double* c;        // [S*n]   min-form objective, UNscaled
+    const double* cl;       // [S*n]   scaled column bounds
+    const double* cu;
+    const double* rl;       // [S*m]   scaled row bounds
+    const double* ru;
+    const double* dc;       // [S*n]   column scaling (x = dc * xhat)
+    const double* dr;       // [S*m]   row scaling    (A_hat = Dr A Dc)
+    const double* eta;      // [S]     step size 0.99 / ||A_hat||_2
+    const double* obj_off;  // [S]     min-form constant
+    const double* bnorm;    // [S]     ||finite bounds||_2 unscaled
+    // PH parameters
+    const double* W;        // [S*N]
+    const double* rho;      // [S*N]
+    const double* xbar;     // [N_tot]
+    const int*    xidx;     // [S*N]   xbar slot of (s,k)
+    const double* fixed;    // [S*N]
+    // state (scaled), persists across solves for warm starts
+    double* xs;             // [S*n]
+    double* ys;             // [S*m]
+    double* omega;          // [S]
+    // outputs
+    double* x_out;          // [S*n] unscaled
+    double* y_out;          // [S*m] unscaled
+    double* xN;             // [S*N]
+    double* obj;            // [S] model sense
+    double* bound;          // [S] model sense
+    double* kkt;            // [S]
+    int*    iters;          // [S]
+    int*    status;         // [S]
+    int w_on, prox_on, fix_nonants, warm, max_iter, check_every;
+    double eps, sense;
+};
+
+struct PrepArgs {
+    int S, n, m, nnz, ruiz_iters, power_iters;
+    const int* rowptr;      // [m+1]
+    const int* colidx;      // [nnz]
+    const int* colptr;      // [n+1]  CSC of the shared pattern
+    const int* csc_p;       // [nnz]  CSR position of CSC entry
+    const int* row_of_p;    // [nnz]
+    double* vals;           // [S*nnz] in: raw values, out: scaled values
+    double* dc;             // [S*n]
+    double* dr;             // [S*m]
+    double* cl; double* cu; // [S*n] in raw, out scaled
+    double* rl; double* ru; // [S*m] in raw, out scaled
+    double* eta;            // [S]
+    double* bnorm;          // [S]
+    double* scratch;        // [S*(2n+2m)]
+};
+
+struct NodeSeg {           // a contiguous scenario range inside one node (one level)
+    int level, node, s0, s1, kofs, klen, seg_first_of_node;
+};
+
+struct PhArgs {
+    int S, N, N_tot, n_seg, n_cseg, P;
+    const double* xN;       // [S*N]
+    double* W;              // [S*N]
+    const double* rho;      // [S*N]
+    const int* xidx;        // [S*N]
+    const double* pc;       // [S*L]
+    int L;
+    const int* nonant_level;// [N]
+    const NodeSeg* seg;     // [n_seg]
+    double* segpart;        // [n_seg * 2 * maxk]
+    int maxk;
+    const int* node_first_seg; // [n_nodes+1] segments of node g: [first[g], first[g+1])
+    const int* node_off;    // [n_nodes]
+    const int* node_level;  // [n_nodes]
+    const int* level_len;   // [L]
+    const int* level_kofs;  // [L]
+    int n_nodes;
+    double* nodesum;        // [2*N_tot]
+    double* xbar;           // [N_tot]
+    double* xsqbar;         // [N_tot]
+    const int* cseg_v;      // [n_cseg] virtual rank of conv segment
+    const int* cseg_s0;     // [n_cseg]
+    const int* cseg_s1;
+    double* csegpart;       // [n_cseg]
+    const int* vr_first;    // [P+1] conv segments of vrank v
+    double* convpart;       // [2*P]
+};
+
+}  // namespace phg

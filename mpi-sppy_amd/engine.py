@@ -1,0 +1,199 @@
+"""GPU batch engine: one ``libphg`` handle holding all local scenarios of a rank on its GPU.
+
+Builds the ``phg_batch`` C struct (include/phg.h) from the local scenario models -- the shared
+CSR pattern, per-scenario values / costs / bounds, and the scenario-tree index maps of
+``SPBase`` -- and exposes the hot-path calls the PH driver makes each iteration:
+
+* :meth:`solve`            -- ``solve_loop`` for every local scenario (``spopt.py:250-341``)
+* :meth:`node_sums` ... :meth:`conv` -- ``Compute_Xbar`` / ``Update_W`` / ``convergence_diff``
+  (``phbase.py:32-112, 301-371``) with the cross-GPU SUMs done by the communicator (RCCL)
+"""
+import numpy as np
+
+from . import _lib
+from ._lib import as_f64, as_i32, ptr
+
+
+def _node_level(name):
+    return name.count("_")
+
+
+class BatchArrays:
+    """Host-side standard-form batch (numpy) for the local scenarios, in local order."""
+
+    def __init__(self, models, all_nodenames, prob, scen_global0, S_global, virt_nproc):
+        m0 = models[0]
+        rp, ci = m0.pattern()
+        self.rowptr, self.colidx = rp, ci
+        S = len(models)
+        n, m, nnz = m0.n, m0.m, len(ci)
+        self.S, self.n, self.m, self.nnz = S, n, m, nnz
+        vals = np.empty((S, nnz))
+        c = np.empty((S, n))
+        cl = np.empty((S, n))
+        cu = np.empty((S, n))
+        rl = np.empty((S, m))
+        ru = np.empty((S, m))
+        off = np.empty(S)
+        for s, md in enumerate(models):
+            if md.n != n or md.m != m:
+                raise ValueError(f"scenario {md.name}: shape ({md.n},{md.m}) differs from ({n},{m}); "
+                                 "the batch needs one shared sparsity pattern")
+            a = md.arrays()
+            if s and (not np.array_equal(a["rowptr"], rp) or not np.array_equal(a["colidx"], ci)):
+                raise ValueError(f"scenario {md.name}: sparsity pattern differs from the first scenario")
+            vals[s] = a["vals"]
+            c[s] = a["c"]
+            cl[s], cu[s], rl[s], ru[s] = a["col_lo"], a["col_hi"], a["row_lo"], a["row_hi"]
+            off[s] = md.obj_offset
+        self.vals, self.c, self.cl, self.cu, self.rl, self.ru, self.off = vals, c, cl, cu, rl, ru, off
+        self.sense = m0.sense
+        # scenario tree
+        nodes0 = m0._mpisppy_node_list
+        self.L = len(nodes0)
+        self.level_len = np.array([len(nd.nonant_vardata_list) for nd in nodes0], np.int32)
+        cols0 = [v.col for nd in nodes0 for v in nd.nonant_vardata_list]
+        self.nonant_col = np.array(cols0, np.int32)
+        self.N = len(cols0)
+        self.nonant_level = np.concatenate([np.full(ln, l, np.int32) for l, ln in enumerate(self.level_len)])
+        self.nonant_pos = np.concatenate([np.arange(ln, dtype=np.int32) for ln in self.level_len])
+        self.all_nodenames = list(all_nodenames)
+        node_id = {nm: g for g, nm in enumerate(self.all_nodenames)}
+        lvl = [_node_level(nm) for nm in self.all_nodenames]
+        self.node_off = np.zeros(len(self.all_nodenames), np.int32)
+        tot = 0
+        for g, nm in enumerate(self.all_nodenames):
+            self.node_off[g] = tot
+            if lvl[g] < self.L:
+                tot += int(self.level_len[lvl[g]])
+        self.N_tot = tot
+        self.scen_node = np.zeros((S, self.L), np.int32)
+        self.prob_coeff = np.zeros((S, self.L))
+        for s, md in enumerate(models):
+            nl = md._mpisppy_node_list
+            if len(nl) != self.L:
+                raise ValueError("all scenarios must have the same number of tree levels")
+            if [v.col for nd in nl for v in nd.nonant_vardata_list] != cols0:
+                raise ValueError(f"scenario {md.name}: nonant columns differ from the first scenario")
+            for l, nd in enumerate(nl):
+                if nd.name not in node_id:
+                    raise RuntimeError(f"Tree node '{nd.name}' not in all_nodenames")
+                self.scen_node[s, l] = node_id[nd.name]
+                self.prob_coeff[s, l] = md._mpisppy_data.prob_coeff[nd.name]
+        self.prob = np.asarray(prob, np.float64)
+        self.scen_global0, self.S_global, self.virt_nproc = scen_global0, S_global, virt_nproc
+
+    def c_struct(self):
+        keep = []
+
+        def k(a):
+            keep.append(a)
+            return ptr(a)
+        b = _lib.PhgBatch()
+        b.S, b.n, b.m, b.nnz = self.S, self.n, self.m, self.nnz
+        b.rowptr, b.colidx = k(as_i32(self.rowptr)), k(as_i32(self.colidx))
+        b.vals, b.c = k(as_f64(self.vals)), k(as_f64(self.c))
+        b.col_lo, b.col_hi = k(as_f64(self.cl)), k(as_f64(self.cu))
+        b.row_lo, b.row_hi = k(as_f64(self.rl)), k(as_f64(self.ru))
+        b.obj_offset = k(as_f64(self.off))
+        b.sense = int(self.sense)
+        b.N, b.nonant_col, b.L = self.N, k(as_i32(self.nonant_col)), self.L
+        b.nonant_level, b.nonant_pos = k(as_i32(self.nonant_level)), k(as_i32(self.nonant_pos))
+        b.level_len, b.scen_node = k(as_i32(self.level_len)), k(as_i32(self.scen_node))
+        b.n_nodes, b.node_off, b.N_tot = len(self.all_nodenames), k(as_i32(self.node_off)), self.N_tot
+        b.prob, b.prob_coeff = k(as_f64(self.prob)), k(as_f64(self.prob_coeff))
+        b.scen_global0, b.S_global, b.virt_nproc = self.scen_global0, self.S_global, self.virt_nproc
+        return b, keep
+
+
+class Engine:
+    """One libphg handle on one GPU (no CPU fallback: raises if the library or device is missing)."""
+
+    def __init__(self, batch, device=0, stream=None, exchange=None):
+        self.lib = _lib.load()
+        self.batch = batch
+        import ctypes
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.phg_create(int(device), ctypes.byref(h)))
+        self.h = h
+        if stream is not None:
+            _lib.check(self.lib.phg_set_stream(self.h, ctypes.c_void_p(int(stream))))
+        b, keep = batch.c_struct()
+        _lib.check(self.lib.phg_load_batch(self.h, ctypes.byref(b)))
+        del keep
+        self.S, self.N, self.N_tot, self.P = batch.S, batch.N, batch.N_tot, batch.virt_nproc
+        self.exchange = exchange            # (nodesum tensor, convpart tensor) for multi-GPU, or None
+        info = np.zeros(8, np.int32)
+        _lib.check(self.lib.phg_info(self.h, ptr(info)))
+        self.variant = int(info[6])
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.phg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ data movement
+    _SIZES = None
+
+    def _count(self, field):
+        S, n, m, N = self.batch.S, self.batch.n, self.batch.m, self.N
+        return {_lib.F_X: S * n, _lib.F_Y: S * m, _lib.F_XN: S * N, _lib.F_W: S * N, _lib.F_RHO: S * N,
+                _lib.F_XBAR: self.N_tot, _lib.F_XSQBAR: self.N_tot, _lib.F_OBJ: S, _lib.F_BOUND: S,
+                _lib.F_EVAL: S, _lib.F_KKT: S, _lib.F_FIXED: S * N, _lib.F_CONV_PART: 2 * self.P}[field]
+
+    def get(self, field):
+        out = np.empty(self._count(field))
+        _lib.check(self.lib.phg_get(self.h, field, ptr(out)))
+        return out
+
+    def set(self, field, values):
+        a = as_f64(np.broadcast_to(np.asarray(values, np.float64), (self._count(field),)).copy())
+        _lib.check(self.lib.phg_set(self.h, field, ptr(a)))
+
+    def get_i32(self, field):
+        out = np.empty(self.S, np.int32)
+        _lib.check(self.lib.phg_get_i32(self.h, field, ptr(out)))
+        return out
+
+    # ------------------------------------------------------------------ hot path
+    def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=64, warm_start=True,
+              fix_nonants=False):
+        o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(bool(warm_start)),
+                         int(bool(fix_nonants)))
+        import ctypes
+        _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))
+
+    def sync(self):
+        _lib.check(self.lib.phg_sync(self.h))
+
+    def node_sums(self):
+        dev = None if self.exchange is None else self.exchange[0].data_ptr()
+        _lib.check(self.lib.phg_node_sums(self.h, dev))
+
+    def apply_xbar(self):
+        ns = None if self.exchange is None else self.exchange[0].data_ptr()
+        cp = None if self.exchange is None else self.exchange[1].data_ptr()
+        _lib.check(self.lib.phg_apply_xbar(self.h, ns, cp))
+
+    def conv_finish(self):
+        import ctypes
+        v = ctypes.c_double()
+        cp = None if self.exchange is None else self.exchange[1].data_ptr()
+        _lib.check(self.lib.phg_conv_finish(self.h, cp, ctypes.byref(v)))
+        return v.value
+
+    def eval_objective(self, w_on, prox_on):
+        _lib.check(self.lib.phg_eval_objective(self.h, int(w_on), int(prox_on)))
+        return self.get(_lib.F_EVAL)
+
+    def last_ms(self, which):
+        import ctypes
+        v = ctypes.c_double()
+        _lib.check(self.lib.phg_last_ms(self.h, int(which), ctypes.byref(v)))
+        return v.value

@@ -1,0 +1,407 @@
+"""PHBase on the MI355X engine (restates ``mpisppy/phbase.py`` + the solve plumbing of
+``mpisppy/spopt.py``).
+
+The public surface matches the reference -- ``PHBase(options, all_scenario_names,
+scenario_creator, scenario_denouement=None, all_nodenames=None, mpicomm=None,
+scenario_creator_kwargs=None, extensions=None, extension_kwargs=None, ph_converger=None,
+rho_setter=None, variable_probability=None)``, ``Iter0``, ``iterk_loop``, ``post_loops``,
+``Compute_Xbar``, ``Update_W``, ``convergence_diff``, ``Ebound``, ``Eobjective``, ``_update_E1``,
+``feas_prob``, ``_populate_W_cache``, ``W_from_flat_list``, ``disable_W_and_prox`` ... -- and the
+order of operations in ``Iter0`` / ``iterk_loop`` (``phbase.py:829-1061``) is kept line for line.
+What changes is underneath: every local scenario lives in one GPU batch (``engine.Engine``), the
+solve loop is one batched PDHG launch, and xbar / W / conv are device kernels whose cross-rank SUMs
+go through the communicator (RCCL).  Nothing of size S x n crosses PCIe inside the PH loop; each
+iteration reads back one convergence scalar (2 x virtual-rank doubles).
+
+Documented deviations: per-subproblem extension hooks ``pre_solve``/``post_solve`` cannot run
+inside a batched launch (``pre_solve_loop``/``post_solve_loop`` do); ``smoothed``,
+``linearize_proximal_terms``, bundles and ``variable_probability`` are not supported yet.
+"""
+import math
+import time
+
+import numpy as np
+
+from . import _lib
+from .engine import BatchArrays, Engine
+from .spbase import SPBase
+
+# PDHG controls read from iter0_solver_options / iterk_solver_options (other solver options,
+# e.g. "mipgap" or "threads", belong to CPU solvers and are ignored)
+_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": 64}
+
+
+class PHBase(SPBase):
+    def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
+                 all_nodenames=None, mpicomm=None, scenario_creator_kwargs=None, extensions=None,
+                 extension_kwargs=None, ph_converger=None, rho_setter=None,
+                 variable_probability=None):
+        self._PHIter = 0
+        super().__init__(options, all_scenario_names, scenario_creator,
+                         scenario_denouement=scenario_denouement, all_nodenames=all_nodenames,
+                         mpicomm=mpicomm, scenario_creator_kwargs=scenario_creator_kwargs,
+                         variable_probability=variable_probability)
+        self.options = options
+        self.options_check()
+        self.ph_converger = ph_converger
+        self.rho_setter = rho_setter
+        self.iter0_solver_options = options.get("iter0_solver_options") or {}
+        self.iterk_solver_options = options.get("iterk_solver_options") or {}
+        self.current_solver_options = self.iter0_solver_options
+        self.convobject = None
+        self.extensions = extensions
+        self.extension_kwargs = extension_kwargs
+        self.extobject = None
+        if extensions is not None:
+            self.extobject = extensions(self) if extension_kwargs is None else extensions(self, **extension_kwargs)
+        self.engine = None
+        self.W_on = 0
+        self.prox_on = 0
+        self.start_time = time.perf_counter()
+        self.conv = None
+        self.solve_count = 0
+
+    # ------------------------------------------------------------------------------- options
+    def options_check(self):
+        """``phbase.py:791-826``."""
+        required = ["solver_name", "PHIterLimit", "defaultPHrho", "convthresh", "verbose", "display_progress"]
+        missing = [k for k in required if k not in self.options]
+        if missing:
+            raise ValueError(f"Missing option(s): {missing}")
+        self.options.setdefault("display_timing", False)
+        self.options.setdefault("display_convergence_detail", False)
+        self.options.setdefault("smoothed", 0)
+        self.options.setdefault("time_limit", None)
+        if self.options["smoothed"]:
+            raise NotImplementedError("smoothed PH is not supported by the GPU engine yet")
+        if self.options.get("linearize_proximal_terms"):
+            raise NotImplementedError("linearize_proximal_terms: the engine solves the exact prox QP")
+        if self.options.get("bundles_per_rank", 0):
+            raise NotImplementedError("bundles are not supported by the GPU engine yet")
+
+    # ------------------------------------------------------------------------------- engine
+    def _virt_nproc(self):
+        return int(self.options.get("virtual_nproc", self.n_proc))
+
+    def _create_solvers(self):
+        """Build the GPU batch (replaces SolverFactory per subproblem, ``spopt.py:876-913``)."""
+        if self.engine is not None:
+            return
+        models = [self.local_scenarios[n] for n in self.local_scenario_names]
+        prob = [m._mpisppy_probability for m in models]
+        batch = BatchArrays(models, self.all_nodenames, prob, self.scen_global0,
+                            len(self.all_scenario_names), self._virt_nproc())
+        device, stream, exchange = self._device_setup(batch)
+        self.engine = Engine(batch, device=device, stream=stream, exchange=exchange)
+        self.engine.set(_lib.F_RHO, float(self.options["defaultPHrho"]))
+
+    def _device_setup(self, batch):
+        device = int(self.options.get("device", 0))
+        stream = None
+        exchange = None
+        try:
+            import torch
+            if torch.cuda.is_available():
+                device = torch.cuda.current_device() if "device" not in self.options else device
+                stream = torch.cuda.current_stream(device).cuda_stream
+                if self.n_proc > 1:
+                    exchange = (torch.zeros(2 * batch.N_tot, dtype=torch.float64, device=f"cuda:{device}"),
+                                torch.zeros(2 * batch.virt_nproc, dtype=torch.float64, device=f"cuda:{device}"))
+        except ImportError:
+            pass
+        return device, stream, exchange
+
+    def _solver_opts(self):
+        o = dict(_SOLVER_DEFAULTS)
+        for k in _SOLVER_DEFAULTS:
+            if k in self.options:
+                o[k] = self.options[k]
+            if self.current_solver_options and k in self.current_solver_options:
+                o[k] = self.current_solver_options[k]
+        return o
+
+    # ------------------------------------------------------------------------------- W / prox
+    def attach_Ws_and_prox(self):
+        self.W_on = 0
+        self.prox_on = 0
+
+    def PH_Prep(self, attach_duals=True, attach_prox=True, attach_smooth=0):
+        """``phbase.py:763-788``: W, rho, xbar live on the device; W_on = prox_on = 0."""
+        self.attach_Ws_and_prox()
+        self._attach_duals = attach_duals
+        self._attach_prox = attach_prox
+        self._create_solvers()
+
+    def _disable_prox(self):
+        self.prox_on = 0
+
+    def _disable_W(self):
+        self.W_on = 0
+
+    def disable_W_and_prox(self):
+        self._disable_W()
+        self._disable_prox()
+
+    def _reenable_prox(self):
+        self.prox_on = 1
+
+    def _reenable_W(self):
+        self.W_on = 1
+
+    def reenable_W_and_prox(self):
+        self._reenable_W()
+        self._reenable_prox()
+
+    @property
+    def W_disabled(self):
+        return not bool(self.W_on)
+
+    @property
+    def prox_disabled(self):
+        return not bool(self.prox_on)
+
+    # ------------------------------------------------------------------------------- solves
+    def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,
+                   dis_W=False, dis_prox=False, gripe=False, disable_pyomo_signal_handling=False,
+                   tee=False, verbose=False, need_solution=True, warm_start=True):
+        """``phbase.py:522-603`` + ``spopt.py:250-341``: one batched launch for all local scenarios."""
+        saved = (self.W_on, self.prox_on)
+        if dis_W:
+            self._disable_W()
+        if dis_prox:
+            self._disable_prox()
+        if self.extobject is not None:
+            self.extobject.pre_solve_loop()
+        if solver_options is not None:
+            self.current_solver_options = solver_options
+        o = self._solver_opts()
+        w_on = int(self.W_on and getattr(self, "_attach_duals", True))
+        prox_on = int(self.prox_on and getattr(self, "_attach_prox", True))
+        t0 = time.perf_counter()
+        self.engine.solve(w_on, prox_on, eps=o["pdhg_eps"], max_iter=o["pdhg_max_iter"],
+                          check_every=o["pdhg_check_every"], warm_start=warm_start)
+        self.engine.sync()
+        self.solve_count += self.engine.S
+        status = self.engine.get_i32(_lib.I_STATUS)
+        self._feasible = status != 2
+        if gripe and (status != 0).any():
+            bad = [self.local_scenario_names[i] for i in np.nonzero(status != 0)[0][:5]]
+            print(f"[{self.__class__.__name__}] {int((status != 0).sum())} subproblem(s) did not reach "
+                  f"the KKT tolerance (first: {bad})")
+        if need_solution and (status == 2).any():
+            raise RuntimeError("PDHG numerical failure (NaN) in scenario(s) "
+                               f"{[self.local_scenario_names[i] for i in np.nonzero(status == 2)[0][:5]]}")
+        if dtiming and self.cylinder_rank == 0:
+            print(f"batched solve of {self.engine.S} subproblems: {time.perf_counter() - t0:.4f} s")
+        if self.extobject is not None:
+            self.extobject.post_solve_loop()
+        self.W_on, self.prox_on = saved if (dis_W or dis_prox) else (self.W_on, self.prox_on)
+
+    # ------------------------------------------------------------------------------- PH update
+    def Compute_Xbar(self, verbose=False):
+        """``phbase.py:32-112``: node sums on the device, SUM across ranks (RCCL)."""
+        self.engine.node_sums()
+        if self.engine.exchange is not None:
+            self.mpicomm.allreduce_sum_(self.engine.exchange[0])
+        self._xbar_pending = True
+
+    def Update_W(self, verbose=False):
+        """``phbase.py:301-326``: W += rho (x - xbar) (fused with the conv partials)."""
+        self.engine.apply_xbar()
+        self._xbar_pending = False
+
+    def convergence_diff(self):
+        """``phbase.py:349-371``: mean over (virtual) ranks of the per-rank mean |x - xbar|."""
+        if self.engine.exchange is not None:
+            self.mpicomm.allreduce_sum_(self.engine.exchange[1])
+        return self.engine.conv_finish()
+
+    # ------------------------------------------------------------------------------- expectations
+    def _rank_fsum(self, vals):
+        local = math.fsum(vals)
+        return self.mpicomm.allreduce_scalar(local) if self.n_proc > 1 else local
+
+    def Ebound(self, verbose=False, extra_sum_terms=None):
+        """``spopt.py:377-422`` (outer bound = the solver's dual bound)."""
+        b = self.engine.get(_lib.F_BOUND)
+        p = self.engine.batch.prob
+        vals = [p[k] * b[k] for k in range(len(b))]
+        if extra_sum_terms is None:
+            return self._rank_fsum(vals)
+        arr = np.array([math.fsum(vals)] + list(extra_sum_terms))
+        if self.n_proc > 1:
+            arr = self.mpicomm.allreduce_array(arr)
+        return arr[0], arr[1:]
+
+    def Eobjective(self, verbose=False):
+        """``spopt.py:344-374``: sum p_s * pyo.value(objfct) with the current W/prox toggles."""
+        w_on = int(self.W_on and getattr(self, "_attach_duals", True))
+        prox_on = int(self.prox_on and getattr(self, "_attach_prox", True))
+        ev = self.engine.eval_objective(w_on, prox_on)
+        p = self.engine.batch.prob
+        return self._rank_fsum([p[k] * ev[k] for k in range(len(ev))])
+
+    def _update_E1(self):
+        self.E1 = self._rank_fsum(list(self.engine.batch.prob))
+
+    def feas_prob(self):
+        p = self.engine.batch.prob
+        return self._rank_fsum([p[k] for k in range(len(p)) if self._feasible[k]])
+
+    def infeas_prob(self):
+        p = self.engine.batch.prob
+        return self._rank_fsum([p[k] for k in range(len(p)) if not self._feasible[k]])
+
+    # ------------------------------------------------------------------------------- caches
+    def _populate_W_cache(self, cache, padding):
+        """``phbase.py:374-394``: local W in local-scenario x nonant order."""
+        W = self.engine.get(_lib.F_W)
+        if len(W) + padding != len(cache):
+            raise RuntimeError(f"W cache length mismatch: total W len {len(W)} but cache len {len(cache)}")
+        cache[:len(W)] = W
+
+    def W_from_flat_list(self, flat_list):
+        """``phbase.py:397-413``."""
+        self.engine.set(_lib.F_W, np.asarray(flat_list[: self.engine.S * self.engine.N], np.float64))
+
+    def _save_nonants(self):
+        self._load_solutions()
+
+    def _save_original_nonants(self):
+        pass
+
+    def _load_solutions(self):
+        """Copy x back into the scenario models (only at finalisation / on request)."""
+        X = self.engine.get(_lib.F_X).reshape(self.engine.S, -1)
+        for k, sname in enumerate(self.local_scenario_names):
+            self.local_scenarios[sname]._solution = X[k]
+
+    # convenient views
+    def nonants(self):
+        return self.engine.get(_lib.F_XN).reshape(self.engine.S, self.engine.N)
+
+    def Ws(self):
+        return self.engine.get(_lib.F_W).reshape(self.engine.S, self.engine.N)
+
+    def xbars(self):
+        return self.engine.get(_lib.F_XBAR)
+
+    # ------------------------------------------------------------------------------- loops
+    def Iter0(self):
+        """``phbase.py:829-946``."""
+        if self.extobject is not None:
+            self.extobject.pre_iter0()
+        verbose = self.options["verbose"]
+        dprogress = self.options["display_progress"]
+        self._PHIter = 0
+        self._create_solvers()
+        if self.extobject is not None:
+            self.extobject.iter0_post_solver_creation()
+        self.solve_loop(solver_options=self.current_solver_options, dtiming=self.options["display_timing"],
+                        gripe=True, verbose=verbose, warm_start=False)
+        self._update_E1()
+        if abs(1 - self.E1) > self.E1_tolerance:
+            raise RuntimeError(f"Total probability of scenarios was {self.E1};  E1_tolerance = ", self.E1_tolerance)
+        feasP = self.feas_prob()
+        if feasP != self.E1:
+            raise RuntimeError(f"Infeasibility detected; E_feas={feasP}, E1={self.E1}")
+        if self.extobject is not None:
+            self.extobject.post_iter0()
+        if self.spcomm is not None:
+            self.spcomm.sync()
+        if self.extobject is not None:
+            self.extobject.post_iter0_after_sync()
+        if self.rho_setter is not None:
+            self._use_rho_setter(verbose and self.cylinder_rank == 0)
+        if self.ph_converger is not None:
+            self.convobject = self.ph_converger(self)
+        self.conv = None
+        self.trivial_bound = self.Ebound(verbose)
+        if dprogress and self.cylinder_rank == 0:
+            print("")
+            print("After PH Iteration", self._PHIter)
+            print("Trivial bound =", self.trivial_bound)
+            print("PHBase Convergence Metric =", self.conv)
+            print("Elapsed time: %6.2f" % (time.perf_counter() - self.start_time))
+        self.reenable_W_and_prox()
+        self.current_solver_options = self.iterk_solver_options
+        return self.trivial_bound
+
+    def _use_rho_setter(self, verbose):
+        """``phbase.py:415-434``: rho_setter(scenario) -> [(vardata, rho)] (vardata or its id)."""
+        rho = self.engine.get(_lib.F_RHO).reshape(self.engine.S, self.engine.N)
+        for k, sname in enumerate(self.local_scenario_names):
+            s = self.local_scenarios[sname]
+            pos = {}
+            i = 0
+            for nd in s._mpisppy_node_list:
+                for v in nd.nonant_vardata_list:
+                    pos[id(v)] = i
+                    i += 1
+            for v, r in self.rho_setter(s, **self.options.get("rho_setter_kwargs", {})):
+                rho[k, pos[v if isinstance(v, int) else id(v)]] = r
+        self.engine.set(_lib.F_RHO, rho.ravel())
+
+    def iterk_loop(self):
+        """``phbase.py:949-1061``."""
+        verbose = self.options["verbose"]
+        dprogress = self.options["display_progress"]
+        self.conv = None
+        max_iterations = int(self.options["PHIterLimit"])
+        self.conv_history = []
+        for self._PHIter in range(1, max_iterations + 1):
+            iteration_start_time = time.time()
+            self.Compute_Xbar(verbose)
+            self.Update_W(verbose)
+            self.conv = self.convergence_diff()
+            self.conv_history.append(self.conv)
+            if self.extobject is not None:
+                self.extobject.miditer()
+            if self.ph_converger is not None and self.convobject.is_converged():
+                break
+            if self.conv is not None and self.conv < self.options["convthresh"]:
+                break
+            if self.options["time_limit"] is not None:
+                over = (time.perf_counter() - self.start_time) >= self.options["time_limit"]
+                if self.n_proc > 1:
+                    over = self.mpicomm.allreduce_scalar(float(over)) > 0
+                if over:
+                    break
+            self.solve_loop(solver_options=self.current_solver_options, dtiming=self.options["display_timing"],
+                            gripe=verbose, verbose=verbose)
+            if self.extobject is not None:
+                self.extobject.enditer()
+            if self.spcomm is not None:
+                self.spcomm.sync()
+                if self.spcomm.is_converged():
+                    break
+            if self.extobject is not None:
+                self.extobject.enditer_after_sync()
+            if dprogress and self.cylinder_rank == 0:
+                print("")
+                print("After PH Iteration", self._PHIter)
+                print("Scaled PHBase Convergence Metric=", self.conv)
+                print("Iteration time: %6.2f" % (time.time() - iteration_start_time))
+                print("Elapsed time:   %6.2f" % (time.perf_counter() - self.start_time))
+        else:
+            self.mpicomm.Barrier()
+
+    def post_loops(self, extensions=None):
+        """``phbase.py:1064-1119``."""
+        self.mpicomm.Barrier()
+        if self.scenario_denouement is not None:
+            self._load_solutions()
+            for sname, s in self.local_scenarios.items():
+                self.scenario_denouement(self.cylinder_rank, sname, s)
+        self.mpicomm.Barrier()
+        if self.extobject is not None:
+            self.extobject.post_everything()
+        if self.ph_converger is not None and hasattr(self.convobject, "post_everything"):
+            self.convobject.post_everything()
+        Eobj = self.Eobjective(self.options["verbose"])
+        self.mpicomm.Barrier()
+        if self.options["display_progress"] and self.cylinder_rank == 0:
+            print("")
+            print("Current ***weighted*** E[objective] =", Eobj)
+            print("")
+        return Eobj

@@ -1,0 +1,146 @@
+"""SPBase restated: scenario distribution, index maps and node bookkeeping.
+
+Follows ``mpisppy/spbase.py`` (``SPBase.__init__`` :48-124, ``_calculate_scenario_ranks``
+:188-220, ``_attach_nonant_indices`` :297-306, ``_attach_nlens`` :309-324,
+``_compute_unconditional_node_probabilities`` :382-395, ``_look_and_leap`` :509-526) and
+``_ScenTree.scen_names_to_ranks`` (``mpisppy/utils/sputils.py:790-856``).  The index maps are
+bit-exact with the reference: scenario order, rank slices, ``(node_name, i)`` nonant keys in node
+list order with sorted Var keys inside a node.
+"""
+import numpy as np
+
+from .comm import SingleComm
+
+
+def scen_names_to_ranks_slices(S, n_proc):
+    """``sputils.py:819-826``: rank -> contiguous scenario index list."""
+    if n_proc == 1:
+        return [list(range(S))]
+    avg = S / n_proc
+    return [list(range(int(i * avg), int((i + 1) * avg))) for i in range(n_proc)]
+
+
+def create_nodenames_from_branching_factors(bfs):
+    """``sputils.py:992-1017``: non-leaf node names of a uniform tree."""
+    stage_nodes = ["ROOT"]
+    names = ["ROOT"]
+    for bf in bfs[:-1]:
+        nxt = []
+        for nd in stage_nodes:
+            for b in range(bf):
+                nxt.append(f"{nd}_{b}")
+        names.extend(nxt)
+        stage_nodes = nxt
+    return names
+
+
+class SPBase:
+    def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
+                 all_nodenames=None, mpicomm=None, scenario_creator_kwargs=None,
+                 variable_probability=None, E1_tolerance=1e-5):
+        self.options = options
+        self.all_scenario_names = list(all_scenario_names)
+        self.scenario_creator = scenario_creator
+        self.scenario_denouement = scenario_denouement
+        self.all_nodenames = list(all_nodenames) if all_nodenames is not None else ["ROOT"]
+        self.mpicomm = mpicomm if mpicomm is not None else SingleComm()
+        self.comms = {"ROOT": self.mpicomm}
+        self.n_proc = self.mpicomm.Get_size()
+        self.cylinder_rank = self.mpicomm.Get_rank()
+        self.global_rank = self.cylinder_rank
+        self.E1_tolerance = E1_tolerance
+        if variable_probability is not None:
+            raise NotImplementedError("variable_probability is not supported by the GPU engine yet")
+        self.variable_probability = None
+        self.bundling = False
+        self._calculate_scenario_ranks()
+        self._create_scenarios(scenario_creator_kwargs or {})
+        self._look_and_leap()
+        self._compute_unconditional_node_probabilities()
+        self._attach_nlens()
+        self._attach_nonant_indices()
+        self._verify_nonant_lengths()
+        self._set_sense()
+        self._spcomm = None
+
+    # ---------------------------------------------------------------------------------------
+    def _calculate_scenario_ranks(self):
+        S = len(self.all_scenario_names)
+        self._rank_slices = scen_names_to_ranks_slices(S, self.n_proc)
+        self._scenario_slices = [r for r, sl in enumerate(self._rank_slices) for _ in sl]
+        self.local_scenario_names = [self.all_scenario_names[i] for i in self._rank_slices[self.cylinder_rank]]
+        self.scen_global0 = self._rank_slices[self.cylinder_rank][0] if self._rank_slices[self.cylinder_rank] else 0
+
+    def _create_scenarios(self, kw):
+        self.local_scenarios = {}
+        for sname in self.local_scenario_names:
+            s = self.scenario_creator(sname, **kw)
+            self.local_scenarios[sname] = s
+        self.local_subproblems = self.local_scenarios
+        self.scenarios_constructed = True
+
+    def _look_and_leap(self):
+        S = len(self.all_scenario_names)
+        for sname, s in self.local_scenarios.items():
+            pspec = getattr(s, "_mpisppy_probability", None)
+            if pspec is None or pspec == "uniform":
+                s._mpisppy_probability = 1.0 / S
+            if not hasattr(s, "_mpisppy_node_list"):
+                raise RuntimeError(f"_mpisppy_node_list not found on scenario {sname}")
+            if not hasattr(s, "_mpisppy_data"):
+                s._mpisppy_data = type("MpisppyData", (), {})()
+
+    def _compute_unconditional_node_probabilities(self):
+        for s in self.local_scenarios.values():
+            nodes = s._mpisppy_node_list
+            nodes[0].uncond_prob = 1.0
+            for parent, child in zip(nodes[:-1], nodes[1:]):
+                child.uncond_prob = parent.uncond_prob * child.cond_prob
+            s._mpisppy_data.prob_coeff = {nd.name: s._mpisppy_probability / nd.uncond_prob for nd in nodes}
+            s._mpisppy_data.prob0_mask = {nd.name: 1.0 for nd in nodes}
+            s._mpisppy_data.has_variable_probability = False
+
+    def _attach_nlens(self):
+        for s in self.local_scenarios.values():
+            s._mpisppy_data.nlens = {nd.name: len(nd.nonant_vardata_list) for nd in s._mpisppy_node_list}
+            s._mpisppy_data.cistart = {}
+            sofar = 0
+            for ndn, ln in s._mpisppy_data.nlens.items():
+                s._mpisppy_data.cistart[ndn] = sofar
+                sofar += ln
+
+    def _attach_nonant_indices(self):
+        for s in self.local_scenarios.values():
+            ni = {}
+            for nd in s._mpisppy_node_list:
+                for i in range(s._mpisppy_data.nlens[nd.name]):
+                    ni[(nd.name, i)] = nd.nonant_vardata_list[i]
+            s._mpisppy_data.nonant_indices = ni
+            s._mpisppy_data.varid_to_nonant_index = {id(v): k for k, v in ni.items()}
+        self.nonant_length = len(ni) if self.local_scenarios else 0
+
+    def _verify_nonant_lengths(self):
+        lens = {}
+        for s in self.local_scenarios.values():
+            for nd in s._mpisppy_node_list:
+                L = s._mpisppy_data.nlens[nd.name]
+                if lens.setdefault(nd.name, L) != L:
+                    raise RuntimeError(f"Tree node {nd.name} has scenarios with different numbers of "
+                                       f"non-anticipative variables: {L} vs. {lens[nd.name]}")
+        for nd in set().union(*[[n.name for n in s._mpisppy_node_list] for s in self.local_scenarios.values()]):
+            if nd not in self.all_nodenames:
+                raise RuntimeError(f"Tree node '{nd}' not in all_nodenames list {self.all_nodenames}")
+
+    def _set_sense(self):
+        senses = {s.sense for s in self.local_scenarios.values()}
+        if len(senses) > 1:
+            raise RuntimeError("All scenario models must have the same model sense (minimize or maximize)")
+        self.is_minimizing = senses.pop() == 1 if senses else True
+
+    @property
+    def spcomm(self):
+        return self._spcomm
+
+    @spcomm.setter
+    def spcomm(self, value):
+        self._spcomm = value
