@@ -30,8 +30,8 @@ def parse():
     ap.add_argument("--cm", type=int, default=10)
     ap.add_argument("--rho", type=float, default=1.0)
     ap.add_argument("--eps", type=float, default=1e-9)
-    ap.add_argument("--conv-iters", type=int, default=3000, help="PH iteration cap for time-to-conv (0: skip)")
-    ap.add_argument("--conv-time", type=float, default=90.0, help="wall cap (s) for time-to-conv")
+    ap.add_argument("--conv-iters", type=int, default=20000, help="PH iteration cap for time-to-conv (0: skip)")
+    ap.add_argument("--conv-time", type=float, default=120.0, help="wall cap (s) for time-to-conv")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0: skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()

@@ -74,7 +74,7 @@ typedef struct phg_opts {
     double  eps_rel;       /* relative KKT tolerance (PDLP-style), e.g. 1e-9            */
     int32_t max_iter;      /* PDHG iteration limit per scenario                         */
     int32_t check_every;   /* iterations between restart/termination checks (e.g. 64)   */
-    int32_t warm_start;    /* 1: start from the previous solution (x, y, primal weight) */
+    int32_t warm_start;    /* bit 0: start from the previous x, y; bit 1: keep its primal weight */
     int32_t fix_nonants;   /* 1: nonants fixed to the values set by phg_set_fixed (xhat) */
 } phg_opts;
 
@@ -96,7 +96,8 @@ enum {
     PHG_F_EVAL = 9,     /* [S] objective evaluated by phg_eval_objective                  */
     PHG_F_KKT = 10,     /* [S] final relative KKT error                                    */
     PHG_F_FIXED = 11,   /* [S*N] values nonants are fixed to when opts.fix_nonants         */
-    PHG_F_CONV_PART = 12/* [2*virt_nproc] per-virtual-rank (sum |x-xbar|, count)            */
+    PHG_F_CONV_PART = 12,/* [2*virt_nproc] per-virtual-rank (sum |x-xbar|, count)           */
+    PHG_F_OMEGA = 13    /* [S] PDHG primal weight carried between solves                    */
 };
 enum {
     PHG_I_ITERS = 0,    /* [S] PDHG iterations of the last solve                           */

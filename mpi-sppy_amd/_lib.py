@@ -34,7 +34,7 @@ class PhgOpts(C.Structure):
                 ("warm_start", C.c_int32), ("fix_nonants", C.c_int32)]
 
 
-F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART = range(13)
+F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART, F_OMEGA = range(14)
 I_ITERS, I_STATUS = 0, 1
 
 # every symbol include/phg.h declares, with its ctypes signature

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
             q[k] = qq * d * d;
             lo[k] = lo_;
             hi[k] = hi_;
-            x[k] = clampd(a.warm ? a.xs[b] : 0.0, lo_, hi_);
+            x[k] = clampd((a.warm & 1) ? a.xs[b] : 0.0, lo_, hi_);
 #pragma unroll
             for (int t = 0; t < KCS; ++t) {
                 const int idx = (l * CPL + k) * KCS + t;
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
             rlo[r] = a.rl[b];
             rhi[r] = a.ru[b];
             drs[r] = a.dr[b];
-            y[r] = a.warm ? a.ys[b] : 0.0;
+            y[r] = (a.warm & 1) ? a.ys[b] : 0.0;
 #pragma unroll
             for (int t = 0; t < KRS; ++t) {
                 const int idx = (l * RPL + r) * KRS + t;
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
     const double bnorm = a.bnorm[s];
     const double eta = a.eta[s];
     double omega;
-    if (a.warm && a.omega[s] > 0.0) {
+    if ((a.warm & 2) && a.omega[s] > 0.0) {
         omega = a.omega[s];
     } else {
         // PDLP init: ||c_hat|| / ||b_hat|| in the scaled space

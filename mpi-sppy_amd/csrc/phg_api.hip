@@ -458,6 +458,7 @@ static double* field_ptr(phg_handle* h, int f, size_t* count) {
         case PHG_F_KKT: *count = S; return h->kkt;
         case PHG_F_FIXED: *count = S * N; return h->fixed;
         case PHG_F_CONV_PART: *count = 2 * (size_t)h->P; return h->convpart;
+        case PHG_F_OMEGA: *count = S; return h->omega;
         default: return nullptr;
     }
 }

@@ -145,7 +145,8 @@ class Engine:
         S, n, m, N = self.batch.S, self.batch.n, self.batch.m, self.N
         return {_lib.F_X: S * n, _lib.F_Y: S * m, _lib.F_XN: S * N, _lib.F_W: S * N, _lib.F_RHO: S * N,
                 _lib.F_XBAR: self.N_tot, _lib.F_XSQBAR: self.N_tot, _lib.F_OBJ: S, _lib.F_BOUND: S,
-                _lib.F_EVAL: S, _lib.F_KKT: S, _lib.F_FIXED: S * N, _lib.F_CONV_PART: 2 * self.P}[field]
+                _lib.F_EVAL: S, _lib.F_KKT: S, _lib.F_FIXED: S * N, _lib.F_CONV_PART: 2 * self.P,
+                _lib.F_OMEGA: S}[field]
 
     def get(self, field):
         out = np.empty(self._count(field))
@@ -162,9 +163,9 @@ class Engine:
         return out
 
     # ------------------------------------------------------------------ hot path
-    def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=64, warm_start=True,
+    def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=64, warm_start=3,
               fix_nonants=False):
-        o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(bool(warm_start)),
+        o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(warm_start),
                          int(bool(fix_nonants)))
         import ctypes
         _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))

@@ -28,7 +28,7 @@ from .spbase import SPBase
 
 # PDHG controls read from iter0_solver_options / iterk_solver_options (other solver options,
 # e.g. "mipgap" or "threads", belong to CPU solvers and are ignored)
-_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": 64}
+_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": 64, "pdhg_keep_omega": False}
 
 
 class PHBase(SPBase):
@@ -179,7 +179,8 @@ class PHBase(SPBase):
         prox_on = int(self.prox_on and getattr(self, "_attach_prox", True))
         t0 = time.perf_counter()
         self.engine.solve(w_on, prox_on, eps=o["pdhg_eps"], max_iter=o["pdhg_max_iter"],
-                          check_every=o["pdhg_check_every"], warm_start=warm_start)
+                          check_every=o["pdhg_check_every"],
+                          warm_start=(1 | (2 if o["pdhg_keep_omega"] else 0)) if warm_start else 0)
         self.engine.sync()
         self.solve_count += self.engine.S
         status = self.engine.get_i32(_lib.I_STATUS)

@@ -108,7 +108,7 @@ class PDHG:
         xs, ys = x.copy(), y.copy()           # last restart point
         xa, ya = np.zeros_like(x), np.zeros_like(y)
         na = np.zeros(S)                      # number averaged
-        kkt_restart = None
+        kkt_restart = self.kkt(x, y, cs, qs, cl, cu, rl, ru, omega) if getattr(self, "init_kkt", False) else None
         kkt_prev_cand = np.full(S, np.inf)
         since = np.zeros(S, int)
         total = 0
