@@ -33,6 +33,8 @@ def parse():
     ap.add_argument("--conv-iters", type=int, default=20000, help="PH iteration cap for time-to-conv (0: skip)")
     ap.add_argument("--conv-time", type=float, default=120.0, help="wall cap (s) for time-to-conv")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0: skip)")
+    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local"],
+                    help="PDHG data layout (include/phg.h: phg_set_layout)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
 
@@ -70,7 +72,7 @@ def main():
     S = args.scen * world
     names = farmer.scenario_names_creator(S)
     opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
-            "convthresh": 1e-4, "verbose": False, "display_progress": False,
+            "convthresh": 1e-4, "verbose": False, "display_progress": False, "pdhg_layout": args.layout,
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps}}
     t_setup = time.perf_counter()
     ph = PH(dict(opts), names, farmer.scenario_creator, mpicomm=comm,
@@ -159,7 +161,8 @@ def main():
         "config": {"workload": f"farmer crops_multiplier={args.cm}, {S} scenarios ({args.scen} per GPU), PH rho={args.rho}, "
                                f"PDHG eps_rel={args.eps}",
                    "scenarios": S, "n": b.n, "m": b.m, "nnz": b.nnz, "nonants": b.N,
-                   "parallelism": f"scenario shards over {world} GPU(s)"},
+                   "parallelism": f"scenario shards over {world} GPU(s)",
+                   "pdhg_layout": eng.layout, "lanes_per_scenario": eng.lanes_per_scenario},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 4), "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 5),
                      "traffic": traffic,

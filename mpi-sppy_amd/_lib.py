@@ -44,6 +44,8 @@ SIGNATURES = {
     "phg_last_error": (C.c_char_p, []),
     "phg_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "phg_sync": (C.c_int, [C.c_void_p]),
+    "phg_set_layout": (C.c_int, [C.c_void_p, C.c_int32]),
+    "phg_plan": (C.c_int, [C.POINTER(PhgBatch), i32p]),
     "phg_load_batch": (C.c_int, [C.c_void_p, C.POINTER(PhgBatch)]),
     "phg_set": (C.c_int, [C.c_void_p, C.c_int32, f64p]),
     "phg_get": (C.c_int, [C.c_void_p, C.c_int32, f64p]),

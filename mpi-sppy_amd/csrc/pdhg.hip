@@ -5,8 +5,8 @@
 //   * the scenario's scaled matrix lives in VGPRs for the whole solve (CSR slots for A x,
 //     CSC slots for A^T y, "dense" rows dealt round-robin over the wave),
 //   * the iterates x, y are staged in LDS only for the two gathers per iteration,
-//   * every reduction (dense rows, KKT norms, objectives) is a 64-lane xor-shuffle butterfly
-//     (deterministic: all lanes end with the same bits),
+//   * every reduction (dense rows, KKT norms, objectives) is a 64-lane DPP/permlane all-reduce
+//     (wave_ops.h; deterministic: all lanes end with the same bits),
 //   * each wave restarts / terminates on its own, so scenarios never wait for each other.
 //
 // Problem per scenario (min-form, PH terms of mpisppy/phbase.py:670-760):
@@ -17,32 +17,12 @@
 // adaptive restarts to the average/current iterate (beta 0.2 / 0.8 / 0.36) with primal-weight
 // updates, and a relative KKT termination test on the UNscaled problem.
 #include "phg_internal.h"
+#include "wave_ops.h"
 
 namespace phg {
 
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
 template <int K>
-__device__ __forceinline__ void wsum_many(double (&v)[K]) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        double t[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) t[k] = __shfl_xor(v[k], o, 64);
-#pragma unroll
-        for (int k = 0; k < K; ++k) v[k] += t[k];
-    }
-}
-
-__device__ __forceinline__ double clampd(double v, double lo, double hi) {
-    return fmin(fmax(v, lo), hi);
-}
-
-__device__ __forceinline__ bool fin(double v) { return fabs(v) < 1e300; }
+__device__ __forceinline__ void wsum_many(double (&v)[K]) { gsum_many<64, K>(v); }
 
 template <int CPL, int KCS, int RPL, int KRS, int D, int KD>
 __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
@@ -371,7 +351,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
             for (int r = 0; r < RPL; ++r) { const double d = y[r] - yr[r]; mv[1] += d * d; }
             wsum_many<2>(mv);
             const double dx = sqrt(mv[0]), dy = sqrt(mv[1]);
-            if (dx > 1e-10 && dy > 1e-10) omega = exp(0.5 * log(dy / dx) + 0.5 * log(omega));
+            if (dx > 1e-10 && dy > 1e-10) omega = sqrt(dy / dx * omega);
             tau = eta / omega;
             sig = eta * omega;
             // exact products at the restart point

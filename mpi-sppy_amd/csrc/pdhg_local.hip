@@ -1,0 +1,523 @@
+// pdhg_local.hip -- register-resident batched PDHG for block-structured scenario LPs/QPs (gfx950).
+//
+// Same algorithm and outputs as pdhg.hip (restarted PDHG, PDLP-style restarts and primal weight,
+// relative-KKT termination on the unscaled problem; it replaces SPOpt.solve_one,
+// mpisppy/spopt.py:184-231, for every local scenario at once), but with a different mapping of a
+// scenario onto the wavefront, chosen when the sparsity pattern allows it:
+//
+//   * a scenario owns an aligned group of LPS = 16, 32 or 64 lanes, so one wave solves 64/LPS
+//     scenarios side by side (farmer cm=10: 30 crop blocks -> 32 lanes, two scenarios per wave);
+//   * every non-coupling row sits in the lane that owns ALL of its columns, so A x and A^T y for it
+//     are register FMAs over a dense RPL x CPL block -- no LDS, no gathers, no barriers;
+//   * the D coupling rows are replicated in every lane of the group; their A x is one
+//     gsum<LPS> all-reduce (DPP row rotations + gfx950 permlane swaps, wave_ops.h) per iteration.
+//
+// So one PDHG iteration is ~100 fp64 VALU instructions and one short DPP chain per wave, with no
+// memory traffic at all between the prologue (load the scenario) and the epilogue (store x, y).
+#include "phg_internal.h"
+#include "wave_ops.h"
+
+namespace phg {
+
+// Per-lane "cold" state (read only at the every-`check_every` restart/termination test) lives in
+// LDS as [item][lane] doubles -- conflict-free ds_read_b64 -- so the registers hold only what the
+// PDHG iteration itself touches.
+template <int CPL, int RPL, int D>
+struct Cold {
+    static constexpr int DD = D > 0 ? D : 1;
+    static constexpr int XR = 0, Q = CPL, IDC = 2 * CPL, YR = 3 * CPL, IDR = 3 * CPL + RPL,
+                         YDR = 3 * CPL + 2 * RPL, IDRD = 3 * CPL + 2 * RPL + DD,
+                         SC = 3 * CPL + 2 * RPL + 2 * DD;
+    enum { CNORM = 0, BNORM, ETA, PROX, OMEGA, KRST, KPREV, NSC };
+    static constexpr int N = SC + NSC;
+};
+
+template <int LPS, int CPL, int RPL, int D>
+__global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
+    constexpr int G = 64 / LPS;                    // scenarios per wave
+    constexpr int DD = D > 0 ? D : 1;
+    using CI = Cold<CPL, RPL, D>;
+    extern __shared__ double cold[];
+    const int lane = threadIdx.x;
+    auto CS = [&](int item) -> double& { return cold[item * 64 + lane]; };
+    const int gl = lane % LPS;                     // lane inside the scenario's group
+    const int s_raw = blockIdx.x * G + lane / LPS;
+    const bool valid = s_raw < a.S;
+    const int s = valid ? s_raw : a.S - 1;         // a tail group mirrors the last scenario, writes nothing
+    const LocalLayout& L = a.loc;
+    const int* col_nonant = a.lay.col_nonant;
+
+    // ------------------------------------------------------------------ columns of this lane
+    int cj[CPL];
+    double x[CPL], aty[CPL], c[CPL], lo[CPL], hi[CPL], ip[CPL], xsum[CPL];
+    double prox_const = 0.0, c2 = 0.0;
+    {
+        const long sn = (long)s * a.n, sN = (long)s * a.N;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            seq();
+            const int j = L.col_of[gl * CPL + k];
+            cj[k] = j;
+            x[k] = aty[k] = c[k] = lo[k] = hi[k] = xsum[k] = 0.0;
+            double qs = 0.0;
+            CS(CI::IDC + k) = 1.0;
+            if (j >= 0) {
+                const long b = sn + j;
+                const double d = a.dc[b];
+                double cc = a.c[b], qq = 0.0;
+                double lo_ = a.cl[b], hi_ = a.cu[b];
+                const int kk = col_nonant[j];
+                if (kk >= 0) {
+                    const long t = sN + kk;
+                    if (a.w_on) cc += a.W[t];
+                    if (a.prox_on) {
+                        const double r = a.rho[t];
+                        const double xb = a.xbar[a.xidx[t]];
+                        cc -= r * xb;
+                        qq = r;
+                        prox_const += 0.5 * r * xb * xb;
+                    }
+                    if (a.fix_nonants) { lo_ = hi_ = a.fixed[t] / d; }
+                }
+                c2 += cc * cc;
+                CS(CI::IDC + k) = 1.0 / d;
+                c[k] = cc * d;
+                qs = qq * d * d;
+                lo[k] = lo_;
+                hi[k] = hi_;
+                x[k] = clampd((a.warm & 1) ? a.xs[b] : 0.0, lo_, hi_);
+            }
+            CS(CI::XR + k) = x[k];
+            CS(CI::Q + k) = qs;
+        }
+    }
+    // ------------------------------------------------------------------ local rows + block
+    double y[RPL], ax[RPL], rlo[RPL], rhi[RPL], ysum[RPL];
+    double blk[RPL][CPL];
+    double b2 = 0.0;
+    {
+        const long sm = (long)s * a.m, snz = (long)s * a.nnz;
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            seq();
+            const int i = L.row_of[gl * RPL + r];
+            y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
+            CS(CI::IDR + r) = 0.0;
+            if (i >= 0) {
+                const long b = sm + i;
+                CS(CI::IDR + r) = 1.0 / a.dr[b];
+                rlo[r] = a.rl[b];
+                rhi[r] = a.ru[b];
+                double yy = (a.warm & 1) ? a.ys[b] : 0.0;
+                if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
+                if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];
+                y[r] = yy;
+            }
+            CS(CI::YR + r) = y[r];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const int p = L.blk_p[(gl * RPL + r) * CPL + k];
+                blk[r][k] = p >= 0 ? a.vals[snz + p] : 0.0;
+            }
+        }
+    }
+    // ------------------------------------------------------------------ coupling rows (replicated)
+    double yd[DD], axd[DD], dlo[DD], dhi[DD], ydsum[DD];
+    double cf[DD][CPL];
+    double b2d = 0.0;
+    {
+        const long sm = (long)s * a.m, snz = (long)s * a.nnz;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            seq();
+            const int i = L.cpl_row[d];
+            yd[d] = axd[d] = dlo[d] = dhi[d] = ydsum[d] = 0.0;
+            CS(CI::IDRD + d) = 0.0;
+            if (i >= 0) {
+                const long b = sm + i;
+                CS(CI::IDRD + d) = 1.0 / a.dr[b];
+                dlo[d] = a.rl[b];
+                dhi[d] = a.ru[b];
+                double yy = (a.warm & 1) ? a.ys[b] : 0.0;
+                if (!fin(dlo[d])) yy = fmin(yy, 0.0); else b2d += dlo[d] * dlo[d];
+                if (!fin(dhi[d])) yy = fmax(yy, 0.0); else b2d += dhi[d] * dhi[d];
+                yd[d] = yy;
+            }
+            CS(CI::YDR + d) = yd[d];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const int p = L.cpl_p[(d * LPS + gl) * CPL + k];
+                cf[d][k] = p >= 0 ? a.vals[snz + p] : 0.0;
+            }
+        }
+    }
+
+    // ------------------------------------------------------------------ products
+    auto mv_ax = [&](const double (&xx)[CPL], double (&o)[RPL], double (&od)[DD]) {
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            double acc = blk[r][0] * xx[0];
+#pragma unroll
+            for (int k = 1; k < CPL; ++k) acc = fma(blk[r][k], xx[k], acc);
+            o[r] = acc;
+        }
+        if constexpr (D > 0) {
+            double t[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                double acc = cf[d][0] * xx[0];
+#pragma unroll
+                for (int k = 1; k < CPL; ++k) acc = fma(cf[d][k], xx[k], acc);
+                t[d] = acc;
+            }
+            gsum_many<LPS, D>(t);
+#pragma unroll
+            for (int d = 0; d < D; ++d) od[d] = t[d];
+        }
+    };
+    auto mv_aty = [&](const double (&yy)[RPL], const double (&yyd)[DD], double (&o)[CPL]) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            double acc = blk[0][k] * yy[0];
+#pragma unroll
+            for (int r = 1; r < RPL; ++r) acc = fma(blk[r][k], yy[r], acc);
+#pragma unroll
+            for (int d = 0; d < D; ++d) acc = fma(cf[d][k], yyd[d], acc);
+            o[k] = acc;
+        }
+    };
+
+    // ------------------------------------------------------------------ scalars
+    // ||c'|| (unscaled, incl. PH terms), prox constant, initial primal weight ||c_hat||/||b_hat||
+    double omega;
+    {
+        double rr[4] = {c2, prox_const, 0.0, b2};
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
+        gsum_many<LPS, 4>(rr);
+        rr[3] += b2d;
+        CS(CI::SC + CI::CNORM) = sqrt(rr[0]);
+        CS(CI::SC + CI::PROX) = rr[1];
+        const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
+        omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
+        if ((a.warm & 2) && a.omega[s] > 0.0) omega = a.omega[s];
+    }
+    const double eta = a.eta[s];
+    CS(CI::SC + CI::BNORM) = a.bnorm[s];
+    CS(CI::SC + CI::ETA) = eta;
+    double tau = eta / omega, sig = eta * omega;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
+
+    mv_ax(x, ax, axd);
+    mv_aty(y, yd, aty);
+
+    // KKT pieces of one iterate over the scenario (group): [0] ||pr||^2 scaled, [1] ||dres||^2
+    // scaled, [2] ||pr||^2 unscaled, [3] ||dres||^2 unscaled, [4] primal objective, [5] dual
+    // objective.  The iterate is given element-wise (xf, atf: column k; yf, axf: local row r;
+    // ydf: coupling row d; axdp: coupling row d's LOCAL partial of A x, reduced here together with
+    // the KKT sums, scaled by `scale`) so the average iterate is never materialised in registers.
+    // Row/column scalings are re-read from memory (cold path).
+    auto kkt = [&](auto xf, auto atf, auto yf, auto axf, auto ydf, auto axdp, double scale, double* o) {
+        double t[6 + DD];
+#pragma unroll
+        for (int u = 0; u < 6 + DD; ++u) t[u] = 0.0;
+        // element by element (seq() stops the scheduler from hoisting every element's loads and
+        // products at once, which would hold them all in registers beside the hot state)
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            seq();
+            const double axx = axf(r), yy = yf(r);
+            const double pr = axx - clampd(axx, rlo[r], rhi[r]);   // 0 on empty slots
+            t[0] += pr * pr;
+            const double pu = pr * CS(CI::IDR + r);
+            t[2] += pu * pu;
+            if (fin(rlo[r])) t[5] += rlo[r] * fmax(yy, 0.0);
+            if (fin(rhi[r])) t[5] += rhi[r] * fmin(yy, 0.0);
+        }
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            seq();
+            if (cj[k] >= 0) {
+                const double xx = xf(k);
+                const double qk = CS(CI::Q + k);
+                const double rc_ = c[k] + qk * xx - atf(k);
+                double dres = 0.0;
+                if (!fin(lo[k]) && rc_ > 0.0) dres += rc_;
+                if (!fin(hi[k]) && rc_ < 0.0) dres += rc_;
+                t[1] += dres * dres;
+                const double du = dres * CS(CI::IDC + k);
+                t[3] += du * du;
+                t[4] += c[k] * xx + 0.5 * qk * xx * xx;
+                if (fin(lo[k])) t[5] += lo[k] * fmax(rc_, 0.0);
+                if (fin(hi[k])) t[5] += hi[k] * fmin(rc_, 0.0);
+                t[5] -= 0.5 * qk * xx * xx;
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) t[6 + d] = axdp(d);
+        gsum_many<LPS, 6 + DD>(t);
+        // replicated coupling rows, added once after the group reduction
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            seq();
+            const double axx = t[6 + d] * scale, yy = ydf(d);
+            const double pr = axx - clampd(axx, dlo[d], dhi[d]);   // 0 on unused coupling slots
+            t[0] += pr * pr;
+            const double pu = pr * CS(CI::IDRD + d);
+            t[2] += pu * pu;
+            if (fin(dlo[d])) t[5] += dlo[d] * fmax(yy, 0.0);
+            if (fin(dhi[d])) t[5] += dhi[d] * fmin(yy, 0.0);
+        }
+#pragma unroll
+        for (int u = 0; u < 6; ++u) o[u] = t[u];
+    };
+    // the current iterate: coupling products are already reduced, so their "partial" is the
+    // value divided by the group size... instead pass the lane-0 share: value on gl == 0, else 0
+    auto kkt_cur = [&](double* o) {
+        kkt([&](int k) { return x[k]; }, [&](int k) { return aty[k]; }, [&](int r) { return y[r]; },
+            [&](int r) { return ax[r]; }, [&](int d) { return yd[d]; },
+            [&](int d) { return gl == 0 ? axd[d] : 0.0; }, 1.0, o);
+    };
+    auto kkt_avg = [&](double inv, double* o) {
+        kkt([&](int k) { return xsum[k] * inv; },
+            [&](int k) {
+                double acc = blk[0][k] * ysum[0];
+#pragma unroll
+                for (int r = 1; r < RPL; ++r) acc = fma(blk[r][k], ysum[r], acc);
+#pragma unroll
+                for (int d = 0; d < D; ++d) acc = fma(cf[d][k], ydsum[d], acc);
+                return acc * inv;
+            },
+            [&](int r) { return ysum[r] * inv; },
+            [&](int r) {
+                double acc = blk[r][0] * xsum[0];
+#pragma unroll
+                for (int k = 1; k < CPL; ++k) acc = fma(blk[r][k], xsum[k], acc);
+                return acc * inv;
+            },
+            [&](int d) { return ydsum[d] * inv; },
+            [&](int d) {
+                double acc = cf[d][0] * xsum[0];
+#pragma unroll
+                for (int k = 1; k < CPL; ++k) acc = fma(cf[d][k], xsum[k], acc);
+                return acc;
+            },
+            inv, o);
+    };
+    auto rel_of = [&](const double* o) {
+        const double p = sqrt(o[2]) / (1.0 + CS(CI::SC + CI::BNORM));
+        const double d = sqrt(o[3]) / (1.0 + CS(CI::SC + CI::CNORM));
+        const double g = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
+        return fmax(fmax(p, d), g);
+    };
+    auto wkkt_of = [&](const double* o, double w) {
+        const double g = o[4] - o[5];
+        return sqrt(w * w * o[0] + o[1] / (w * w) + g * g);
+    };
+
+    {
+        double o[6];
+        kkt_cur(o);
+        CS(CI::SC + CI::KRST) = wkkt_of(o, omega);
+        CS(CI::SC + CI::KPREV) = INFINITY;
+        CS(CI::SC + CI::OMEGA) = omega;
+    }
+    int it = 0, since = 0, cnt = 0;
+    bool live = true;
+    const int chk = a.check_every;
+
+    // epilogue for a group that has terminated (st 0 optimal, 1 iteration limit, 2 NaN)
+    auto finish = [&](bool use_avg, double inv, double rel, double pobj, double dobj, int st) {
+        if (!valid) return;
+        const int sl = launder(s);
+        const long sn = (long)sl * a.n, sm = (long)sl * a.m, sN = (long)sl * a.N;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            seq();
+            const int j = launder(cj[k]);
+            if (j >= 0) {
+                const long b = sn + j;
+                const double xv = use_avg ? xsum[k] * inv : x[k];
+                a.xs[b] = xv;
+                const double xu = xv * a.dc[b];
+                a.x_out[b] = xu;
+                const int kk = col_nonant[j];
+                if (kk >= 0) a.xN[sN + kk] = xu;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            seq();
+            const int i = L.row_of[gl * RPL + r];
+            if (i >= 0) {
+                const long b = sm + i;
+                const double yv = use_avg ? ysum[r] * inv : y[r];
+                a.ys[b] = yv;
+                a.y_out[b] = yv * a.dr[b];
+            }
+        }
+        if (gl == 0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int i = L.cpl_row[d];
+                if (i >= 0) {
+                    const long b = sm + i;
+                    const double yv = use_avg ? ydsum[d] * inv : yd[d];
+                    a.ys[b] = yv;
+                    a.y_out[b] = yv * a.dr[b];
+                }
+            }
+            const double offs = a.obj_off[sl] + (a.prox_on ? CS(CI::SC + CI::PROX) : 0.0);
+            a.omega[sl] = CS(CI::SC + CI::OMEGA);
+            a.obj[sl] = a.sense * (pobj + offs);
+            a.bound[sl] = a.sense * (dobj + offs);
+            a.kkt[sl] = rel;
+            a.iters[sl] = it;
+            a.status[sl] = st;
+        }
+    };
+
+    while (wave_any(live)) {
+#pragma unroll 1
+        for (int kk = 0; kk < chk; ++kk) {
+            // primal step: exact prox of the diagonal quadratic + box (1/(1+tau q) precomputed)
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const double xn = clamp_sel(fma(tau, aty[k] - c[k], x[k]) * ip[k], lo[k], hi[k]);
+                x[k] = xn;
+                xsum[k] += xn;
+            }
+            // dual step with extrapolation A(2x+ - x) = 2 A x+ - A x (empty row slots stay 0:
+            // zero block row and zero bounds)
+            double axn[RPL], axdn[DD];
+            mv_ax(x, axn, axdn);
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+                const double g = y[r] - sig * (2.0 * axn[r] - ax[r]);
+                y[r] = fmax(fma(sig, rlo[r], g), 0.0) + fmin(fma(sig, rhi[r], g), 0.0);
+                ax[r] = axn[r];
+                ysum[r] += y[r];
+            }
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const double g = yd[d] - sig * (2.0 * axdn[d] - axd[d]);
+                yd[d] = fmax(fma(sig, dlo[d], g), 0.0) + fmin(fma(sig, dhi[d], g), 0.0);
+                axd[d] = axdn[d];
+                ydsum[d] += yd[d];
+            }
+            mv_aty(y, yd, aty);
+        }
+        it += chk;
+        since += chk;
+        cnt += chk;
+
+        // ---------------------------------------------------------- restart / termination check
+        const double inv = 1.0 / (double)cnt;
+        double oc[6], oa[6];
+        kkt_cur(oc);
+        kkt_avg(inv, oa);
+        const double rel_cur = rel_of(oc), rel_avg = rel_of(oa);
+        const bool nan = !(rel_cur == rel_cur);
+        const bool term = live && (nan || rel_cur <= a.eps || rel_avg <= a.eps);
+        const bool cap = live && !term && it >= a.max_iter;
+        if (term || cap) {
+            const bool ua = !nan && rel_avg < rel_cur;
+            finish(ua, inv, ua ? rel_avg : rel_cur, ua ? oa[4] : oc[4], ua ? oa[5] : oc[5],
+                   nan ? 2 : (term ? 0 : 1));
+            live = false;
+        }
+        if (!wave_any(live)) break;
+
+        omega = CS(CI::SC + CI::OMEGA);
+        const double k_cur = wkkt_of(oc, omega), k_avg = wkkt_of(oa, omega);
+        const bool use_avg = k_avg < k_cur;
+        const double cand = use_avg ? k_avg : k_cur;
+        const double krst = CS(CI::SC + CI::KRST);
+        const bool restart = live && ((cand <= 0.2 * krst) ||
+                                      (cand <= 0.8 * krst && cand > CS(CI::SC + CI::KPREV)) ||
+                                      ((double)since >= 0.36 * (double)it));
+        CS(CI::SC + CI::KPREV) = cand;
+        if (wave_any(restart)) {
+            const bool ra = restart && use_avg;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) x[k] = ra ? xsum[k] * inv : x[k];
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) y[r] = ra ? ysum[r] * inv : y[r];
+#pragma unroll
+            for (int d = 0; d < D; ++d) yd[d] = ra ? ydsum[d] * inv : yd[d];
+            // primal weight update (theta = 0.5) from the movement since the last restart
+            double mv[2] = {0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) { const double t = x[k] - CS(CI::XR + k); mv[0] += t * t; }
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) { const double t = y[r] - CS(CI::YR + r); mv[1] += t * t; }
+            gsum_many<LPS, 2>(mv);
+#pragma unroll
+            for (int d = 0; d < D; ++d) { const double t = yd[d] - CS(CI::YDR + d); mv[1] += t * t; }
+            const double dx = sqrt(mv[0]), dy = sqrt(mv[1]);
+            if (restart && dx > 1e-10 && dy > 1e-10) omega = sqrt(dy / dx * omega);   // exp(.5 log(dy/dx) + .5 log w)
+            const double et = CS(CI::SC + CI::ETA);
+            tau = et / omega;
+            sig = et * omega;
+            // exact products at the (possibly new) point; unchanged groups recompute the same values
+            mv_ax(x, ax, axd);
+            mv_aty(y, yd, aty);
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
+            if (restart) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) { CS(CI::XR + k) = x[k]; xsum[k] = 0.0; }
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) { CS(CI::YR + r) = y[r]; ysum[r] = 0.0; }
+#pragma unroll
+                for (int d = 0; d < D; ++d) { CS(CI::YDR + d) = yd[d]; ydsum[d] = 0.0; }
+                CS(CI::SC + CI::OMEGA) = omega;
+                CS(CI::SC + CI::KRST) = cand;
+                CS(CI::SC + CI::KPREV) = INFINITY;
+                cnt = 0;
+                since = 0;
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- dispatch
+struct LocalVariant {
+    int LPS, CPL, RPL, D;
+    void (*fn)(PdhgArgs);
+};
+
+#define PHG_L(a_, b_, c_, d_) {a_, b_, c_, d_, pdhg_local_kernel<a_, b_, c_, d_>}
+// ordered by preference: fewest lanes per scenario first, then smallest register footprint
+static const LocalVariant kLocalVariants[] = {
+    PHG_L(16, 4, 3, 1),
+    PHG_L(16, 4, 4, 2),
+    PHG_L(32, 4, 3, 1),
+    PHG_L(32, 4, 4, 2),
+    PHG_L(64, 4, 3, 1),
+    PHG_L(64, 4, 4, 2),
+};
+#undef PHG_L
+
+int pdhg_local_num_variants() { return (int)(sizeof(kLocalVariants) / sizeof(kLocalVariants[0])); }
+
+void pdhg_local_variant_shape(int v, int* out4) {
+    const LocalVariant& V = kLocalVariants[v];
+    out4[0] = V.LPS; out4[1] = V.CPL; out4[2] = V.RPL; out4[3] = V.D;
+}
+
+size_t pdhg_local_lds_bytes(int v) {
+    const LocalVariant& V = kLocalVariants[v];
+    const int DD = V.D > 0 ? V.D : 1;
+    return (size_t)(3 * V.CPL + 2 * V.RPL + 2 * DD + 7) * 64 * sizeof(double);   // Cold<CPL,RPL,D>::N
+}
+
+hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream) {
+    const int G = 64 / kLocalVariants[v].LPS;
+    hipLaunchKernelGGL(kLocalVariants[v].fn, dim3((a.S + G - 1) / G), dim3(64), pdhg_local_lds_bytes(v),
+                       stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace phg

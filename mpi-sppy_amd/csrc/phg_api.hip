@@ -20,6 +20,9 @@ int pdhg_num_variants();
 void pdhg_variant_shape(int v, int* out6);
 hipError_t pdhg_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t prep_launch(const PrepArgs& a, hipStream_t stream);
+int pdhg_local_num_variants();
+void pdhg_local_variant_shape(int v, int* out4);
+hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
 hipError_t eval_obj_launch(int S, int n, int N, const double* x, const double* c, const double* obj_off,
@@ -51,8 +54,11 @@ struct phg_handle {
     bool loaded = false;
     int S = 0, n = 0, m = 0, nnz = 0, N = 0, L = 0, N_tot = 0, n_nodes = 0, P = 1, n_pad = 0;
     double sense = 1.0;
-    int variant = -1;
+    int variant = -1;          // gather kernel variant (pdhg.hip), or
+    int local_variant = -1;    // lane-local kernel variant (pdhg_local.hip); preferred when >= 0
+    int layout_policy = PHG_LAYOUT_AUTO;
     int vshape[6] = {0};
+    int lshape[4] = {0};
     std::vector<void*> allocs;
     // device arrays
     double *vals = nullptr, *c = nullptr, *cl = nullptr, *cu = nullptr, *rl = nullptr, *ru = nullptr;
@@ -64,6 +70,7 @@ struct phg_handle {
     int *iters = nullptr, *status = nullptr;
     int* nonant_col_d = nullptr;
     Layout lay{};
+    LocalLayout loc{};
     PhArgs ph{};
     double *nodesum = nullptr, *convpart = nullptr;
     std::vector<int> nonant_col_h;
@@ -134,6 +141,14 @@ int phg_set_stream(phg_handle* h, void* s) {
     return 0;
 }
 
+int phg_set_layout(phg_handle* h, int32_t policy) {
+    if (!h) return fail("null handle");
+    if (h->loaded) return fail("phg_set_layout: must be called before phg_load_batch");
+    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_LOCAL) return fail("phg_set_layout: bad policy");
+    h->layout_policy = policy;
+    return 0;
+}
+
 int phg_sync(phg_handle* h) {
     if (!h) return fail("null handle");
     CK(hipStreamSynchronize(h->stream));
@@ -167,7 +182,8 @@ static int build_layout(phg_handle* h, const phg_batch* b, const std::vector<int
         snprintf(msg, sizeof msg,
                  "phg_load_batch: no PDHG kernel variant fits n=%d m=%d max col nnz=%d "
                  "(wave-per-scenario variants cover n,m <= 256)", n, m, kcs_need);
-        return fail(msg);
+        g_err = msg;
+        return 1;
     }
     pdhg_variant_shape(chosen, sh);
     const int CPL = sh[0], KCS = sh[1], RPL = sh[2], KRS = sh[3], D = sh[4], KD = sh[5];
@@ -208,8 +224,6 @@ static int build_layout(phg_handle* h, const phg_batch* b, const std::vector<int
             }
         }
     }
-    std::vector<int> col_nonant(n, -1);
-    for (int k = 0; k < b->N; ++k) col_nonant[b->nonant_col[k]] = k;
     int* p;
     if (dput(h, &p, col_of.data(), col_of.size())) return -1; h->lay.col_of = p;
     if (dput(h, &p, cent_p.data(), cent_p.size())) return -1; h->lay.cent_p = p;
@@ -220,8 +234,168 @@ static int build_layout(phg_handle* h, const phg_batch* b, const std::vector<int
     if (dput(h, &p, rent_col.data(), rent_col.size())) return -1; h->lay.rent_col = p;
     if (dput(h, &p, dent_p.data(), dent_p.size())) return -1; h->lay.dent_p = p;
     if (dput(h, &p, dent_col.data(), dent_col.size())) return -1; h->lay.dent_col = p;
-    if (dput(h, &p, col_nonant.data(), col_nonant.size())) return -1; h->lay.col_nonant = p;
     return 0;
+}
+
+// Lane-local layout (pdhg_local.hip): pick coupling rows greedily (longest row of an oversized
+// block) until every connected block of the remaining row/column graph fits one lane (<= CPL
+// columns, <= RPL rows), then first-fit-decreasing pack the blocks into LPS lanes.
+// Returns 0 (built), 1 (this shape does not fit), -1 (error).
+struct LocalPlan {
+    std::vector<int> col_of, row_of, blk_p, cpl_row, cpl_p;
+};
+
+static int plan_local(const phg_batch* b, int LPS, int CPL, int RPL, int D, LocalPlan& P) {
+    const int n = b->n, m = b->m;
+    if (n > LPS * CPL || m > LPS * RPL + D) return 1;
+    std::vector<char> coupling(m, 0);
+    std::vector<int> cpl;
+    std::vector<int> par(n);
+    std::vector<int> comp_of_col(n), comp_of_row(m);
+    int ncomp = 0;
+    std::vector<int> ccols, crows;
+    // connected blocks of the graph without the coupling rows (and without row `skip`)
+    auto blocks = [&](int skip) {
+        for (int j = 0; j < n; ++j) par[j] = j;
+        auto find = [&](int j) { while (par[j] != j) { par[j] = par[par[j]]; j = par[j]; } return j; };
+        for (int i = 0; i < m; ++i) {
+            if (coupling[i] || i == skip) continue;
+            for (int p = b->rowptr[i] + 1; p < b->rowptr[i + 1]; ++p) {
+                const int u = find(b->colidx[b->rowptr[i]]), v = find(b->colidx[p]);
+                if (u != v) par[u] = v;
+            }
+        }
+        std::vector<int> id(n, -1);
+        ncomp = 0;
+        for (int j = 0; j < n; ++j) {
+            const int r = find(j);
+            if (id[r] < 0) id[r] = ncomp++;
+            comp_of_col[j] = id[r];
+        }
+        for (int i = 0; i < m; ++i) {
+            if (coupling[i] || i == skip) { comp_of_row[i] = -1; continue; }
+            if (b->rowptr[i + 1] == b->rowptr[i]) { comp_of_row[i] = ncomp++; continue; }   // empty row
+            comp_of_row[i] = comp_of_col[b->colidx[b->rowptr[i]]];
+        }
+        ccols.assign(ncomp, 0);
+        crows.assign(ncomp, 0);
+        for (int j = 0; j < n; ++j) ccols[comp_of_col[j]]++;
+        for (int i = 0; i < m; ++i)
+            if (comp_of_row[i] >= 0) crows[comp_of_row[i]]++;
+        // score: (oversized blocks, largest block) -- lower is better
+        long over = 0, big = 0;
+        for (int g = 0; g < ncomp; ++g) {
+            over += (ccols[g] > CPL || crows[g] > RPL);
+            big = std::max(big, (long)ccols[g] + crows[g]);
+        }
+        return over * 1000000L + big;
+    };
+    for (;;) {
+        const long sc = blocks(-1);
+        if (sc < 1000000L) break;                  // every block fits a lane
+        if ((int)cpl.size() >= D) return 1;
+        // next coupling row: the one whose removal leaves the fewest / smallest oversized blocks
+        // (ties: the longer row)
+        std::vector<int> cand;
+        {
+            std::vector<char> bad(ncomp, 0);
+            for (int g = 0; g < ncomp; ++g) bad[g] = ccols[g] > CPL || crows[g] > RPL;
+            for (int i = 0; i < m; ++i)
+                if (!coupling[i] && comp_of_row[i] >= 0 && bad[comp_of_row[i]]) cand.push_back(i);
+        }
+        int best = -1, blen = -1;
+        long bsc = 0;
+        for (int i : cand) {
+            const long s2 = blocks(i);
+            const int len = b->rowptr[i + 1] - b->rowptr[i];
+            if (best < 0 || s2 < bsc || (s2 == bsc && len > blen)) { best = i; bsc = s2; blen = len; }
+        }
+        if (best < 0) return 1;
+        coupling[best] = 1;
+        cpl.push_back(best);
+    }
+    // first-fit decreasing by (columns, rows)
+    std::vector<int> order(ncomp);
+    for (int g = 0; g < ncomp; ++g) order[g] = g;
+    std::stable_sort(order.begin(), order.end(), [&](int u, int v) {
+        return ccols[u] != ccols[v] ? ccols[u] > ccols[v] : crows[u] > crows[v];
+    });
+    std::vector<int> lane_c(LPS, 0), lane_r(LPS, 0), lane_of(ncomp, -1);
+    for (int g : order) {
+        int l = 0;
+        while (l < LPS && (lane_c[l] + ccols[g] > CPL || lane_r[l] + crows[g] > RPL)) ++l;
+        if (l == LPS) return 1;
+        lane_of[g] = l;
+        lane_c[l] += ccols[g];
+        lane_r[l] += crows[g];
+    }
+    P.col_of.assign(LPS * CPL, -1);
+    P.row_of.assign(LPS * RPL, -1);
+    P.blk_p.assign(LPS * RPL * CPL, -1);
+    P.cpl_row.assign(std::max(1, D), -1);
+    P.cpl_p.assign(std::max(1, D * LPS * CPL), -1);
+    std::vector<int> slot_of_col(n, -1), lane_of_col(n, -1);
+    std::fill(lane_c.begin(), lane_c.end(), 0);
+    std::fill(lane_r.begin(), lane_r.end(), 0);
+    for (int j = 0; j < n; ++j) {
+        const int l = lane_of[comp_of_col[j]];
+        const int k = lane_c[l]++;
+        P.col_of[l * CPL + k] = j;
+        slot_of_col[j] = k;
+        lane_of_col[j] = l;
+    }
+    for (int i = 0; i < m; ++i) {
+        if (comp_of_row[i] < 0) continue;
+        const int l = lane_of[comp_of_row[i]];
+        const int r = lane_r[l]++;
+        P.row_of[l * RPL + r] = i;
+        for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) {
+            const int j = b->colidx[p];
+            if (lane_of_col[j] != l) return fail("plan_local: internal error (row split across lanes)");
+            P.blk_p[(l * RPL + r) * CPL + slot_of_col[j]] = p;
+        }
+    }
+    for (int d = 0; d < (int)cpl.size(); ++d) {
+        const int i = cpl[d];
+        P.cpl_row[d] = i;
+        for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) {
+            const int j = b->colidx[p];
+            P.cpl_p[(d * LPS + lane_of_col[j]) * CPL + slot_of_col[j]] = p;
+        }
+    }
+    return 0;
+}
+
+static int pick_local_variant(const phg_batch* b, LocalPlan& plan, int* sh) {
+    for (int v = 0; v < pdhg_local_num_variants(); ++v) {
+        pdhg_local_variant_shape(v, sh);
+        const int r = plan_local(b, sh[0], sh[1], sh[2], sh[3], plan);
+        if (r < 0) return -2;
+        if (r == 0) return v;
+    }
+    return -1;
+}
+
+static int build_local_layout(phg_handle* h, const phg_batch* b) {
+    int sh[4];
+    LocalPlan plan;
+    for (int v = 0; v < pdhg_local_num_variants(); ++v) {
+        pdhg_local_variant_shape(v, sh);
+        const int r = plan_local(b, sh[0], sh[1], sh[2], sh[3], plan);
+        if (r < 0) return -1;
+        if (r > 0) continue;
+        h->local_variant = v;
+        std::memcpy(h->lshape, sh, sizeof sh);
+        int* p;
+        if (dput(h, &p, plan.col_of.data(), plan.col_of.size())) return -1; h->loc.col_of = p;
+        if (dput(h, &p, plan.row_of.data(), plan.row_of.size())) return -1; h->loc.row_of = p;
+        if (dput(h, &p, plan.blk_p.data(), plan.blk_p.size())) return -1; h->loc.blk_p = p;
+        if (dput(h, &p, plan.cpl_row.data(), plan.cpl_row.size())) return -1; h->loc.cpl_row = p;
+        if (dput(h, &p, plan.cpl_p.data(), plan.cpl_p.size())) return -1; h->loc.cpl_p = p;
+        return 0;
+    }
+    g_err = "phg_load_batch: the pattern has no lane-local layout (blocks too large or too many coupling rows)";
+    return 1;
 }
 
 static int build_ph_tables(phg_handle* h, const phg_batch* b) {
@@ -342,6 +516,30 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     return 0;
 }
 
+int phg_plan(const phg_batch* b, int32_t* out8) {
+    if (!b || !out8) return fail("phg_plan: null argument");
+    if (b->n <= 0 || b->m <= 0 || !b->rowptr || !b->colidx) return fail("phg_plan: empty pattern");
+    LocalPlan plan;
+    int sh[4] = {0, 0, 0, 0};
+    const int v = pick_local_variant(b, plan, sh);
+    if (v == -2) return -1;
+    for (int i = 0; i < 8; ++i) out8[i] = 0;
+    out8[0] = v;
+    if (v >= 0) {
+        int ncpl = 0;
+        for (int i : plan.cpl_row) ncpl += i >= 0;
+        out8[1] = sh[0]; out8[2] = sh[1]; out8[3] = sh[2]; out8[4] = sh[3]; out8[5] = ncpl;
+        int lanes = 0;
+        for (int l = 0; l < sh[0]; ++l) {
+            bool used = false;
+            for (int k = 0; k < sh[1]; ++k) used |= plan.col_of[l * sh[1] + k] >= 0;
+            lanes += used;
+        }
+        out8[6] = lanes;
+    }
+    return 0;
+}
+
 int phg_load_batch(phg_handle* h, const phg_batch* b) {
     if (!h || !b) return fail("phg_load_batch: null argument");
     if (h->loaded) return fail("phg_load_batch: handle already holds a batch");
@@ -378,7 +576,23 @@ int phg_load_batch(phg_handle* h, const phg_batch* b) {
                 row_of_p[p] = i;
             }
     }
-    if (build_layout(h, b, colptr, csc_row, csc_p)) return -1;
+    {
+        std::vector<int> col_nonant(n, -1);
+        for (int k = 0; k < b->N; ++k) col_nonant[b->nonant_col[k]] = k;
+        int* p;
+        if (dput(h, &p, col_nonant.data(), col_nonant.size())) return -1;
+        h->lay.col_nonant = p;
+    }
+    int lr = 1, gr = 1;
+    if (h->layout_policy != PHG_LAYOUT_GATHER) {
+        lr = build_local_layout(h, b);
+        if (lr < 0) return -1;
+        if (lr > 0 && h->layout_policy == PHG_LAYOUT_LOCAL) return -1;
+    }
+    if (lr != 0) {
+        gr = build_layout(h, b, colptr, csc_row, csc_p);
+        if (gr != 0) return -1;
+    }
     // min-form objective
     std::vector<double> cmin((size_t)S * n), off((size_t)S, 0.0);
     for (size_t e = 0; e < cmin.size(); ++e) cmin[e] = h->sense * b->c[e];
@@ -438,7 +652,8 @@ int phg_load_batch(phg_handle* h, const phg_batch* b) {
 int phg_info(phg_handle* h, int32_t* o) {
     if (!h || !h->loaded) return fail("phg_info: no batch loaded");
     o[0] = h->S; o[1] = h->n; o[2] = h->m; o[3] = h->nnz; o[4] = h->N; o[5] = h->N_tot;
-    o[6] = h->variant; o[7] = 64;
+    if (h->local_variant >= 0) { o[6] = 100 + h->local_variant; o[7] = h->lshape[0]; }
+    else { o[6] = h->variant; o[7] = 64; }
     return 0;
 }
 
@@ -512,7 +727,9 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.w_on = w_on; a.prox_on = prox_on; a.fix_nonants = o->fix_nonants; a.warm = o->warm_start;
     a.max_iter = o->max_iter; a.check_every = o->check_every; a.eps = o->eps_rel; a.sense = h->sense;
     CK(hipEventRecord(h->ev[0], h->stream));
-    CK(pdhg_launch(h->variant, a, h->stream));
+    a.loc = h->loc;
+    if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
+    else CK(pdhg_launch(h->variant, a, h->stream));
     CK(hipEventRecord(h->ev[1], h->stream));
     return 0;
 }

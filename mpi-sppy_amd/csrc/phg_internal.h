@@ -25,9 +25,24 @@ struct Layout {
     const int* col_nonant;  // [n] nonant index of column j or -1
 };
 
+// Lane-local layout of the register-resident PDHG kernel (pdhg_local.hip).  Built on the host by
+// partitioning the shared pattern's row/column graph (phg_api.hip: build_local_layout):
+//   * "coupling" rows (a few rows linking many blocks, e.g. farmer's total-acreage row) are
+//     replicated in every lane of the scenario's lane group and reduced with gsum<LPS>;
+//   * every other row lives in the same lane as ALL of its columns, so A x and A^T y for it are
+//     plain register FMAs over a dense RPL x CPL block (zero where the pattern has no entry).
+struct LocalLayout {
+    const int* col_of;      // [LPS*CPL]      column of lane slot, -1 = empty
+    const int* row_of;      // [LPS*RPL]      row of lane slot, -1 = empty
+    const int* blk_p;       // [LPS*RPL*CPL]  CSR position of entry (row slot, col slot) or -1
+    const int* cpl_row;     // [D]            coupling rows (-1 = unused)
+    const int* cpl_p;       // [D*LPS*CPL]    CSR position of coupling entry on (lane, col slot) or -1
+};
+
 struct PdhgArgs {
     int S, n, m, nnz, N, n_pad;
     Layout lay;
+    LocalLayout loc;
     // scenario data (scaled where noted)
     const double* vals;     // [S*nnz] scaled values
     const double* c;        // [S*n]   min-form objective, UNscaled

@@ -106,10 +106,27 @@ class BatchArrays:
         return b, keep
 
 
+def plan_layout(batch):
+    """Host-only dry run of the lane-local layout planner (``phg_plan``): dict or None."""
+    import ctypes
+    lib = _lib.load()
+    b, keep = batch.c_struct()
+    out = np.zeros(8, np.int32)
+    _lib.check(lib.phg_plan(ctypes.byref(b), ptr(out)))
+    del keep
+    if out[0] < 0:
+        return None
+    return {"variant": int(out[0]), "lanes_per_scenario": int(out[1]), "cols_per_lane": int(out[2]),
+            "rows_per_lane": int(out[3]), "coupling_slots": int(out[4]), "coupling_rows": int(out[5]),
+            "lanes_used": int(out[6])}
+
+
 class Engine:
     """One libphg handle on one GPU (no CPU fallback: raises if the library or device is missing)."""
 
-    def __init__(self, batch, device=0, stream=None, exchange=None):
+    LAYOUTS = {"auto": 0, "gather": 1, "local": 2}
+
+    def __init__(self, batch, device=0, stream=None, exchange=None, layout="auto"):
         self.lib = _lib.load()
         self.batch = batch
         import ctypes
@@ -118,6 +135,7 @@ class Engine:
         self.h = h
         if stream is not None:
             _lib.check(self.lib.phg_set_stream(self.h, ctypes.c_void_p(int(stream))))
+        _lib.check(self.lib.phg_set_layout(self.h, self.LAYOUTS[layout]))
         b, keep = batch.c_struct()
         _lib.check(self.lib.phg_load_batch(self.h, ctypes.byref(b)))
         del keep
@@ -126,6 +144,8 @@ class Engine:
         info = np.zeros(8, np.int32)
         _lib.check(self.lib.phg_info(self.h, ptr(info)))
         self.variant = int(info[6])
+        self.lanes_per_scenario = int(info[7])
+        self.layout = "local" if self.variant >= 100 else "gather"
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:

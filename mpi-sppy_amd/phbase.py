@@ -92,7 +92,8 @@ class PHBase(SPBase):
         batch = BatchArrays(models, self.all_nodenames, prob, self.scen_global0,
                             len(self.all_scenario_names), self._virt_nproc())
         device, stream, exchange = self._device_setup(batch)
-        self.engine = Engine(batch, device=device, stream=stream, exchange=exchange)
+        self.engine = Engine(batch, device=device, stream=stream, exchange=exchange,
+                             layout=self.options.get("pdhg_layout", "auto"))
         self.engine.set(_lib.F_RHO, float(self.options["defaultPHrho"]))
 
     def _device_setup(self, batch):

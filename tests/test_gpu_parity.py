@@ -34,8 +34,11 @@ def _opts(**kw):
     return o
 
 
-def _farmer_ph(S, cm=1, virtual_nproc=None, **kw):
-    o = _opts(**kw)
+LAYOUTS = ["gather", "local"]
+
+
+def _farmer_ph(S, cm=1, virtual_nproc=None, layout="auto", **kw):
+    o = _opts(pdhg_layout=layout, **kw)
     if virtual_nproc:
         o["virtual_nproc"] = virtual_nproc
     return PH(o, farmer.scenario_names_creator(S), farmer.scenario_creator,
@@ -97,8 +100,9 @@ def test_ph_update_kernels_vs_oracle_hydro():
 
 
 # ----------------------------------------------------------------------------- batched solves
-def test_iter0_lp_farmer3():
-    ph = _farmer_ph(3)
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_iter0_lp_farmer3(layout):
+    ph = _farmer_ph(3, layout=layout)
     ph.PH_Prep()
     tb = ph.Iter0()
     o = _farmer_oracle(3)
@@ -106,12 +110,14 @@ def test_iter0_lp_farmer3():
     assert abs(tb - otb) <= 1e-7 * abs(otb)
     np.testing.assert_allclose(ph.nonants(), np.array([o.nonants(k) for k in range(3)]), atol=1e-4)
     assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+    assert ph.engine.layout == layout
 
 
-@pytest.mark.parametrize("S,cm", [(30, 10), (12, 2)])
-def test_iter0_lp_objectives(S, cm):
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("S,cm", [(30, 10), (12, 2), (5, 20)])
+def test_iter0_lp_objectives(S, cm, layout):
     """LP optima may be non-unique (cm>1: identical crops), so compare objectives / bounds."""
-    ph = _farmer_ph(S, cm=cm)
+    ph = _farmer_ph(S, cm=cm, layout=layout)
     ph.PH_Prep()
     tb = ph.Iter0()
     o = _farmer_oracle(S, cm=cm)
@@ -121,10 +127,11 @@ def test_iter0_lp_objectives(S, cm):
     np.testing.assert_allclose(ph.engine.get(_lib.F_BOUND), o.outer, rtol=1e-6)
 
 
-@pytest.mark.parametrize("S,cm", [(3, 1), (30, 10)])
-def test_prox_qp_solves_vs_oracle(S, cm):
+@pytest.mark.parametrize("layout", LAYOUTS)
+@pytest.mark.parametrize("S,cm", [(3, 1), (30, 10), (7, 5)])
+def test_prox_qp_solves_vs_oracle(S, cm, layout):
     """Same W / xbar into both solvers: the prox QPs are strictly convex in x_N -> unique x_N."""
-    ph = _farmer_ph(S, cm=cm)
+    ph = _farmer_ph(S, cm=cm, layout=layout)
     ph.PH_Prep()
     ph.Iter0()
     o = _farmer_oracle(S, cm=cm, PHIterLimit=3)
@@ -164,8 +171,9 @@ def test_w_and_xbar_fixtures_farmer3():
         assert abs(xb[vn.index(vname)] - float(x)) <= 1e-6 * abs(float(x))
 
 
-def test_farmer3_ph_vs_oracle_trajectory():
-    ph = _farmer_ph(3, PHIterLimit=8)
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_farmer3_ph_vs_oracle_trajectory(layout):
+    ph = _farmer_ph(3, PHIterLimit=8, layout=layout)
     conv, eobj, tb = ph.ph_main()
     o = _farmer_oracle(3, PHIterLimit=8)
     oconv, oeobj, otb = o.ph_main()
