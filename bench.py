@@ -35,6 +35,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0: skip)")
     ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local"],
                     help="PDHG data layout (include/phg.h: phg_set_layout)")
+    ap.add_argument("--no-schedule", action="store_true", help="launch scenarios in index order")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
 
@@ -73,6 +74,7 @@ def main():
     names = farmer.scenario_names_creator(S)
     opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
             "convthresh": 1e-4, "verbose": False, "display_progress": False, "pdhg_layout": args.layout,
+            "pdhg_schedule": not args.no_schedule,
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps}}
     t_setup = time.perf_counter()
     ph = PH(dict(opts), names, farmer.scenario_creator, mpicomm=comm,
@@ -96,26 +98,32 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # timed region
-    pdhg_ms = 0.0
-    upd_ms = 0.0
-    pdhg_iters = 0
-    max_iters = 0
+    # timed region: per-launch HIP events and iteration counts are accumulated on the device and
+    # read once afterwards (no per-step host synchronisation beyond PH's own conv readback)
+    eng.timing_reset(solves=True)
     if comm is not None:
         comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         conv = step()
-        pdhg_ms += eng.last_ms(0)
-        upd_ms += eng.last_ms(1)
-        its = eng.get_i32(_lib.I_ITERS)
-        pdhg_iters += int(its.sum())
-        max_iters = max(max_iters, int(its.max()))
     torch.cuda.synchronize()
     if comm is not None:
         comm.barrier()
     el = time.perf_counter() - t0
+    pdhg_ms, n_solves, pdhg_iters = eng.timing(0)
+    assert n_solves == args.steps, n_solves
+    # the fused xbar/W/conv kernels, timed separately (HIP events only on them) over extra updates
+    W_saved = eng.get(_lib.F_W)
+    eng.timing_reset(solves=False, updates=True)
+    for _ in range(args.steps):
+        ph.Compute_Xbar()
+        ph.Update_W()
+        ph.convergence_diff()
+    upd_ms, n_upd, _ = eng.timing(1)
+    eng.timing_reset(solves=False, updates=False)
+    eng.set(_lib.F_W, W_saved)
+    max_iters = int(eng.get_i32(_lib.I_ITERS).max())
     if comm is not None:
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -76,6 +76,8 @@ typedef struct phg_opts {
     int32_t check_every;   /* iterations between restart/termination checks (e.g. 64)   */
     int32_t warm_start;    /* bit 0: start from the previous x, y; bit 1: keep its primal weight */
     int32_t fix_nonants;   /* 1: nonants fixed to the values set by phg_set_fixed (xhat) */
+    int32_t schedule;      /* 1: launch scenarios heaviest-first by the previous solve's PDHG
+                              iteration counts (device radix sort after each solve)          */
 } phg_opts;
 
 /* solve modes (mpisppy/phbase.py:670-760: W_on / prox_on toggles) */
@@ -96,7 +98,8 @@ enum {
     PHG_F_EVAL = 9,     /* [S] objective evaluated by phg_eval_objective                  */
     PHG_F_KKT = 10,     /* [S] final relative KKT error                                    */
     PHG_F_FIXED = 11,   /* [S*N] values nonants are fixed to when opts.fix_nonants         */
-    PHG_F_CONV_PART = 12,/* [2*virt_nproc] per-virtual-rank (sum |x-xbar|, count)           */
+    PHG_F_CONV_PART = 12,/* [2*virt_nproc+2] per-virtual-rank (sum |x-xbar|, count), then the
+                            status counts of phg_solve_summary                              */
     PHG_F_OMEGA = 13    /* [S] PDHG primal weight carried between solves                    */
 };
 enum {
@@ -135,23 +138,32 @@ int  phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* opt
 /* PH update, split for an external (RCCL / torch.distributed) all-reduce between steps:
  *   1. phg_node_sums   : dev_nodesum[2*N_tot] <- local sums of prob_coeff*x, prob_coeff*x^2
  *   2. (all-reduce SUM of dev_nodesum across GPUs)
- *   3. phg_apply_xbar  : xbar <- nodesum; W += rho (x - xbar); dev_convpart[2*virt_nproc]
- *   4. (all-reduce SUM of dev_convpart across GPUs)
+ *   3. phg_apply_xbar  : xbar <- nodesum; W += rho (x - xbar); dev_convpart[2*virt_nproc+2]
+ *   4. (all-reduce SUM of dev_convpart[2*virt_nproc + 2] across GPUs)
  *   5. phg_conv_finish : conv = (1/P) sum_v sum_v/count_v
  * phg_ph_update does 1-5 on one GPU (no exchange).                                          */
 int  phg_node_sums(phg_handle* h, double* dev_nodesum);
 int  phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpart);
 int  phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_conv);
+/* status summary of the solve preceding the last PH update, read back by phg_conv_finish with the
+ * convergence partials (dev_convpart[2P], [2P+1]; summed over GPUs by the same all-reduce):
+ * out2 = {scenarios not at the KKT tolerance, scenarios with a numerical failure}            */
+int  phg_solve_summary(phg_handle* h, int32_t* out2);
 int  phg_ph_update(phg_handle* h, double* host_conv);
 
 /* per-scenario objective with the CURRENT W/xbar/rho (pyo.value(objfct), spopt.py:365) */
 int  phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on);
 
-/* elapsed milliseconds (HIP events on the handle's stream) of the last phg_solve launch
- * (which = 0) or of the last node-sum + W-update launches (which = 1) */
-int  phg_last_ms(phg_handle* h, int32_t which, double* ms);
 
-/* device pointer of the handle's own exchange buffers (2*N_tot and 2*virt_nproc doubles) */
+/* launch timing without per-launch synchronisation: phg_timing_reset clears the counters and
+ * selects what gets HIP events (enable bit 0: solves, bit 1: PH updates; 0 = none, the
+ * production default);
+ * phg_timing sums the HIP-event durations of every solve (which = 0) or PH update (which = 1)
+ * launched since, and the PDHG iterations of all scenarios over those solves              */
+int  phg_timing_reset(phg_handle* h, int32_t enable);
+int  phg_timing(phg_handle* h, int32_t which, double* total_ms, int32_t* launches, int64_t* pdhg_iters);
+
+/* device pointer of the handle's own exchange buffers (2*N_tot and 2*virt_nproc+2 doubles) */
 int  phg_exchange_buffers(phg_handle* h, double** dev_nodesum, double** dev_convpart);
 
 #ifdef __cplusplus

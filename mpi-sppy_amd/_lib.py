@@ -31,7 +31,7 @@ class PhgBatch(C.Structure):
 
 class PhgOpts(C.Structure):
     _fields_ = [("eps_rel", C.c_double), ("max_iter", C.c_int32), ("check_every", C.c_int32),
-                ("warm_start", C.c_int32), ("fix_nonants", C.c_int32)]
+                ("warm_start", C.c_int32), ("fix_nonants", C.c_int32), ("schedule", C.c_int32)]
 
 
 F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART, F_OMEGA = range(14)
@@ -56,9 +56,11 @@ SIGNATURES = {
     "phg_apply_xbar": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "phg_conv_finish": (C.c_int, [C.c_void_p, C.c_void_p, f64p]),
     "phg_ph_update": (C.c_int, [C.c_void_p, f64p]),
+    "phg_solve_summary": (C.c_int, [C.c_void_p, i32p]),
     "phg_eval_objective": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "phg_exchange_buffers": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
-    "phg_last_ms": (C.c_int, [C.c_void_p, C.c_int32, f64p]),
+    "phg_timing_reset": (C.c_int, [C.c_void_p, C.c_int32]),
+    "phg_timing": (C.c_int, [C.c_void_p, C.c_int32, f64p, i32p, C.POINTER(C.c_int64)]),
 }
 
 _lib = None

@@ -27,7 +27,7 @@ __device__ __forceinline__ void wsum_many(double (&v)[K]) { gsum_many<64, K>(v);
 template <int CPL, int KCS, int RPL, int KRS, int D, int KD>
 __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int s = blockIdx.x;
+    const int s = a.order ? a.order[blockIdx.x] : blockIdx.x;
     const int l = threadIdx.x;
     double* xl = smem;               // [n_pad]  x staged for the row gathers
     double* yl = smem + a.n_pad;     // [m]      y staged for the column gathers
@@ -427,6 +427,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
         a.bound[s] = a.sense * (o[5] + offs);
         a.kkt[s] = rel_final;
         a.iters[s] = it;
+        a.iters_acc[s] += it;
         a.status[s] = st;
     }
 }

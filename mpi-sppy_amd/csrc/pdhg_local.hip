@@ -41,9 +41,10 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
     const int lane = threadIdx.x;
     auto CS = [&](int item) -> double& { return cold[item * 64 + lane]; };
     const int gl = lane % LPS;                     // lane inside the scenario's group
-    const int s_raw = blockIdx.x * G + lane / LPS;
-    const bool valid = s_raw < a.S;
-    const int s = valid ? s_raw : a.S - 1;         // a tail group mirrors the last scenario, writes nothing
+    const int w_raw = blockIdx.x * G + lane / LPS;  // work item
+    const bool valid = w_raw < a.S;
+    const int w = valid ? w_raw : a.S - 1;         // a tail group mirrors the last item, writes nothing
+    const int s = a.order ? a.order[w] : w;        // scenario of this work item
     const LocalLayout& L = a.loc;
     const int* col_nonant = a.lay.col_nonant;
 
@@ -206,6 +207,28 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
     CS(CI::SC + CI::BNORM) = a.bnorm[s];
     CS(CI::SC + CI::ETA) = eta;
     double tau = eta / omega, sig = eta * omega;
+    // row bounds are held pre-multiplied by -sig (the dual step; re-derived from memory at
+    // restarts), so the dual projection is one v_max_f64 + one v_min_f64 without modifiers
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) { rlo[r] *= -sig; rhi[r] *= -sig; }
+#pragma unroll
+    for (int d = 0; d < D; ++d) { dlo[d] *= -sig; dhi[d] *= -sig; }
+    auto rescale_bounds = [&]() {
+        const int sl = launder(s);
+        const long sm = (long)sl * a.m;
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            seq();
+            const int i = L.row_of[gl * RPL + r];
+            if (i >= 0) { rlo[r] = -sig * a.rl[sm + i]; rhi[r] = -sig * a.ru[sm + i]; }
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            seq();
+            const int i = L.cpl_row[d];
+            if (i >= 0) { dlo[d] = -sig * a.rl[sm + i]; dhi[d] = -sig * a.ru[sm + i]; }
+        }
+    };
 #pragma unroll
     for (int k = 0; k < CPL; ++k) ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
 
@@ -222,18 +245,20 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         double t[6 + DD];
 #pragma unroll
         for (int u = 0; u < 6 + DD; ++u) t[u] = 0.0;
+        const double isg = -1.0 / sig;   // registers hold -sig * (row bounds)
         // element by element (seq() stops the scheduler from hoisting every element's loads and
         // products at once, which would hold them all in registers beside the hot state)
 #pragma unroll
         for (int r = 0; r < RPL; ++r) {
             seq();
             const double axx = axf(r), yy = yf(r);
-            const double pr = axx - clampd(axx, rlo[r], rhi[r]);   // 0 on empty slots
+            const double bl = rlo[r] * isg, bu = rhi[r] * isg;
+            const double pr = axx - clampd(axx, bl, bu);   // 0 on empty slots
             t[0] += pr * pr;
             const double pu = pr * CS(CI::IDR + r);
             t[2] += pu * pu;
-            if (fin(rlo[r])) t[5] += rlo[r] * fmax(yy, 0.0);
-            if (fin(rhi[r])) t[5] += rhi[r] * fmin(yy, 0.0);
+            if (fin(bl)) t[5] += bl * fmax(yy, 0.0);
+            if (fin(bu)) t[5] += bu * fmin(yy, 0.0);
         }
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
@@ -262,12 +287,13 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         for (int d = 0; d < D; ++d) {
             seq();
             const double axx = t[6 + d] * scale, yy = ydf(d);
-            const double pr = axx - clampd(axx, dlo[d], dhi[d]);   // 0 on unused coupling slots
+            const double bl = dlo[d] * isg, bu = dhi[d] * isg;
+            const double pr = axx - clampd(axx, bl, bu);   // 0 on unused coupling slots
             t[0] += pr * pr;
             const double pu = pr * CS(CI::IDRD + d);
             t[2] += pu * pu;
-            if (fin(dlo[d])) t[5] += dlo[d] * fmax(yy, 0.0);
-            if (fin(dhi[d])) t[5] += dhi[d] * fmin(yy, 0.0);
+            if (fin(bl)) t[5] += bl * fmax(yy, 0.0);
+            if (fin(bu)) t[5] += bu * fmin(yy, 0.0);
         }
 #pragma unroll
         for (int u = 0; u < 6; ++u) o[u] = t[u];
@@ -374,17 +400,19 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             a.bound[sl] = a.sense * (dobj + offs);
             a.kkt[sl] = rel;
             a.iters[sl] = it;
+            a.iters_acc[sl] += it;
             a.status[sl] = st;
         }
     };
 
     while (wave_any(live)) {
-#pragma unroll 1
-        for (int kk = 0; kk < chk; ++kk) {
+        // two PDHG iterations per trip (check_every is even): the A x / A x+ hand-over is a
+        // register rename instead of copies
+        auto step = [&]() {
             // primal step: exact prox of the diagonal quadratic + box (1/(1+tau q) precomputed)
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
-                const double xn = clamp_sel(fma(tau, aty[k] - c[k], x[k]) * ip[k], lo[k], hi[k]);
+                const double xn = vmin(vmax(fma(tau, aty[k] - c[k], x[k]) * ip[k], lo[k]), hi[k]);
                 x[k] = xn;
                 xsum[k] += xn;
             }
@@ -394,19 +422,25 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             mv_ax(x, axn, axdn);
 #pragma unroll
             for (int r = 0; r < RPL; ++r) {
+                // y+ = max(g + sig lo, 0) + min(g + sig hi, 0) = g - clamp(g, -sig hi, -sig lo)
                 const double g = y[r] - sig * (2.0 * axn[r] - ax[r]);
-                y[r] = fmax(fma(sig, rlo[r], g), 0.0) + fmin(fma(sig, rhi[r], g), 0.0);
+                y[r] = g - vmin(vmax(g, rhi[r]), rlo[r]);
                 ax[r] = axn[r];
                 ysum[r] += y[r];
             }
 #pragma unroll
             for (int d = 0; d < D; ++d) {
                 const double g = yd[d] - sig * (2.0 * axdn[d] - axd[d]);
-                yd[d] = fmax(fma(sig, dlo[d], g), 0.0) + fmin(fma(sig, dhi[d], g), 0.0);
+                yd[d] = g - vmin(vmax(g, dhi[d]), dlo[d]);
                 axd[d] = axdn[d];
                 ydsum[d] += yd[d];
             }
             mv_aty(y, yd, aty);
+        };
+#pragma unroll 1
+        for (int kk = 0; kk < chk; kk += 2) {
+            step();
+            step();
         }
         it += chk;
         since += chk;
@@ -460,6 +494,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             const double et = CS(CI::SC + CI::ETA);
             tau = et / omega;
             sig = et * omega;
+            rescale_bounds();
             // exact products at the (possibly new) point; unchanged groups recompute the same values
             mv_ax(x, ax, axd);
             mv_aty(y, yd, aty);

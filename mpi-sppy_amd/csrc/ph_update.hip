@@ -5,16 +5,44 @@
 //   _Compute_Xbar     mpisppy/phbase.py:32-112   node sums of prob_coeff*x and prob_coeff*x^2
 //   Update_W          mpisppy/phbase.py:301-326  W += rho (x - xbar)
 //   convergence_diff  mpisppy/phbase.py:349-371  (1/P) sum_v  sum_{s in v,k} |x - xbar| / count_v
-// Node sums are reduced per "segment" (a contiguous scenario range inside one node) and then
-// per node in segment order; the cross-GPU all-reduce (RCCL) of the 2*N_tot node sums and of the
-// 2*P convergence partials happens between the kernels (see include/phg.h).
+// Two launches per PH iteration.  Node sums are reduced per "segment" (a contiguous scenario range
+// inside one node) and then, by the last workgroup, per node in segment order; the cross-GPU
+// all-reduce (RCCL) of the 2*N_tot node sums and of the 2*P+2 convergence partials happens
+// between / after the kernels (see include/phg.h).
 #include "phg_internal.h"
 
 namespace phg {
 
-// one workgroup per node segment; thread t handles nonant k = t % klen of scenarios
-// s0 + t / klen + q*i  (q = 256 / klen lanes per nonant) -> coalesced rows of xN
-__global__ __launch_bounds__(256) void node_partial_kernel(PhArgs a) {
+// "Last workgroup done" hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): every storing
+// wave drains its stores, lane 0 releases at agent scope and takes a ticket; the workgroup whose
+// ticket is last acquires at agent scope and finishes the reduction in a FIXED order, so the result
+// does not depend on which workgroup arrived last.  That workgroup also re-zeroes the counter for
+// the next (stream-ordered) launch.
+__device__ __forceinline__ bool last_workgroup(unsigned* counter) {
+    __shared__ unsigned s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = prev == gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_last = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return s_last != 0u;
+}
+
+// Node sums (first half of _Compute_Xbar).  One workgroup per node segment; thread t handles
+// nonant k = t % klen of scenarios s0 + t / klen + q*i (q = 256 / klen lanes per nonant) ->
+// coalesced rows of xN.  The last workgroup adds every node's segment partials in segment order:
+// nodesum[e] = sum p x, nodesum[N_tot + e] = sum p x^2 (the buffer the cross-GPU all-reduce sums).
+__global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
     __shared__ double sh[2 * 256];
     const NodeSeg sg = a.seg[blockIdx.x];
     const int tid = threadIdx.x;
@@ -45,65 +73,125 @@ __global__ __launch_bounds__(256) void node_partial_kernel(PhArgs a) {
         }
         __syncthreads();
     }
+    if (!last_workgroup(a.ticket)) return;
+    // T lanes per node element (power of two <= 64), each summing every T-th segment of the node,
+    // then a fixed xor-butterfly over the T lanes: wide enough to hide the L2 latency when N_tot is
+    // small, one lane per element when it is large
+    int T = 1;
+    while (T < 64 && T * 2 * a.N_tot <= 256) T *= 2;
+    const int E = 256 / T;
+    const int sub = tid % T;
+    for (int e0 = 0; e0 < a.N_tot; e0 += E) {
+        const int e = e0 + tid / T;
+        double t1 = 0.0, t2 = 0.0;
+        if (e < a.N_tot) {
+            // node g with node_off[g] <= e < node_off[g] + level_len[level[g]]
+            int lo = 0, hi = a.n_nodes - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (a.node_off[mid] <= e) lo = mid; else hi = mid - 1;
+            }
+            const int i = e - a.node_off[lo];
+#pragma unroll 4
+            for (int g = a.node_first_seg[lo] + sub; g < a.node_first_seg[lo + 1]; g += T) {
+                t1 += a.segpart[(long)g * 2 * a.maxk + i];
+                t2 += a.segpart[(long)g * 2 * a.maxk + a.maxk + i];
+            }
+        }
+        for (int o = 1; o < T; o <<= 1) {
+            t1 += __shfl_xor(t1, o, 64);
+            t2 += __shfl_xor(t2, o, 64);
+        }
+        if (e < a.N_tot && sub == 0) {
+            nodesum[e] = t1;
+            nodesum[a.N_tot + e] = t2;
+        }
+    }
 }
 
-// one thread per (node, i): add that node's segment partials in segment order
-__global__ void node_final_kernel(PhArgs a, double* nodesum) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= a.N_tot) return;
-    // find the node g with node_off[g] <= e < node_off[g] + level_len[level[g]]
-    int lo = 0, hi = a.n_nodes - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (a.node_off[mid] <= e) lo = mid; else hi = mid - 1;
-    }
-    const int g = lo;
-    const int i = e - a.node_off[g];
-    double t1 = 0.0, t2 = 0.0;
-    for (int sg = a.node_first_seg[g]; sg < a.node_first_seg[g + 1]; ++sg) {
-        t1 += a.segpart[(long)sg * 2 * a.maxk + i];
-        t2 += a.segpart[(long)sg * 2 * a.maxk + a.maxk + i];
-    }
-    nodesum[e] = t1;
-    nodesum[a.N_tot + e] = t2;
+// fixed-order sum of v[first..last) by all 256 threads of the workgroup (same result in every thread)
+__device__ __forceinline__ double block_sum_range(const double* v, int first, int last, double* red) {
+    const int tid = threadIdx.x;
+    double t = 0.0;
+    for (int g = first + tid; g < last; g += 256) t += v[g];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = t;
+    __syncthreads();
+    return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// one workgroup per convergence segment (scenario range inside one virtual rank):
-// xbar from the (all-reduced) node sums, W update, sum |x - xbar|
-__global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* nodesum) {
+// Update_W + convergence_diff (local half) + the solve-status summary.  One workgroup per
+// convergence segment (scenario range inside one virtual rank): xbar from the (all-reduced) node
+// sums, W += rho (x - xbar), sum |x - xbar|, and the number of scenarios whose last solve did not
+// reach the KKT tolerance / failed numerically.  The last workgroup reduces the segment partials
+// per virtual rank (fixed order) into convpart[2v], convpart[2v+1] = (sum, count) and
+// convpart[2P], convpart[2P+1] = the two status counts; workgroup 0 publishes xbar / xsqbar.
+__global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* nodesum, double* convpart) {
     __shared__ double red[4];
+    __shared__ int bad[8];
     const int b = blockIdx.x;
-    const long e0 = (long)a.cseg_s0[b] * a.N, e1 = (long)a.cseg_s1[b] * a.N;
+    const int tid = threadIdx.x;
+    const int s0 = a.cseg_s0[b], s1 = a.cseg_s1[b];
+    const long e0 = (long)s0 * a.N, e1 = (long)s1 * a.N;
     double acc = 0.0;
-    for (long e = e0 + threadIdx.x; e < e1; e += 256) {
+    for (long e = e0 + tid; e < e1; e += 256) {
         const double xb = nodesum[a.xidx[e]];
         const double d = a.xN[e] - xb;
         a.W[e] += a.rho[e] * d;
         acc += fabs(d);
     }
+    int nb = 0, nn = 0;
+    if (a.status)
+        for (int s = s0 + tid; s < s1; s += 256) {
+            const int st = a.status[s];
+            nb += st != 0;
+            nn += st == 2;
+        }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    for (int o = 32; o > 0; o >>= 1) {
+        acc += __shfl_xor(acc, o, 64);
+        nb += __shfl_xor(nb, o, 64);
+        nn += __shfl_xor(nn, o, 64);
+    }
+    if ((tid & 63) == 0) { red[tid >> 6] = acc; bad[tid >> 6] = nb; bad[4 + (tid >> 6)] = nn; }
     __syncthreads();
-    if (threadIdx.x == 0) a.csegpart[b] = ((red[0] + red[1]) + red[2]) + red[3];
-    // the first workgroup also publishes xbar / xsqbar
+    if (tid == 0) {
+        a.csegpart[b] = ((red[0] + red[1]) + red[2]) + red[3];
+        a.csegbad[2 * b] = bad[0] + bad[1] + bad[2] + bad[3];
+        a.csegbad[2 * b + 1] = bad[4] + bad[5] + bad[6] + bad[7];
+    }
     if (b == 0)
-        for (int j = threadIdx.x; j < a.N_tot; j += 256) {
+        for (int j = tid; j < a.N_tot; j += 256) {
             a.xbar[j] = nodesum[j];
             a.xsqbar[j] = nodesum[a.N_tot + j];
         }
-}
-
-__global__ void conv_final_kernel(PhArgs a, double* convpart) {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= a.P) return;
-    double t = 0.0, cnt = 0.0;
-    for (int b = a.vr_first[v]; b < a.vr_first[v + 1]; ++b) {
-        t += a.csegpart[b];
-        cnt += (double)(a.cseg_s1[b] - a.cseg_s0[b]) * (double)a.N;
+    if (!last_workgroup(a.ticket + 1)) return;
+    for (int v = 0; v < a.P; ++v) {
+        const int g0 = a.vr_first[v], g1 = a.vr_first[v + 1];
+        const double t = block_sum_range(a.csegpart, g0, g1, red);
+        if (tid == 0) {
+            convpart[2 * v] = t;
+            convpart[2 * v + 1] = g1 > g0 ? (double)(a.cseg_s1[g1 - 1] - a.cseg_s0[g0]) * (double)a.N : 0.0;
+        }
     }
-    convpart[2 * v] = t;
-    convpart[2 * v + 1] = cnt;
+    {
+        int tb = 0, tn = 0;
+        for (int g = tid; g < (int)gridDim.x; g += 256) { tb += a.csegbad[2 * g]; tn += a.csegbad[2 * g + 1]; }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            tb += __shfl_xor(tb, o, 64);
+            tn += __shfl_xor(tn, o, 64);
+        }
+        __syncthreads();
+        if ((tid & 63) == 0) { bad[tid >> 6] = tb; bad[4 + (tid >> 6)] = tn; }
+        __syncthreads();
+        if (tid == 0) {
+            convpart[2 * a.P] = (double)(bad[0] + bad[1] + bad[2] + bad[3]);
+            convpart[2 * a.P + 1] = (double)(bad[4] + bad[5] + bad[6] + bad[7]);
+        }
+    }
 }
 
 // per-scenario objective value with the current W / xbar / rho (pyo.value(objfct))
@@ -131,14 +219,12 @@ __global__ void eval_obj_kernel(int S, int n, int N, const double* x, const doub
 }
 
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
-    hipLaunchKernelGGL(node_partial_kernel, dim3(a.n_seg), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(node_final_kernel, dim3((a.N_tot + 255) / 256), dim3(256), 0, st, a, nodesum);
+    hipLaunchKernelGGL(node_sums_kernel, dim3(a.n_seg), dim3(256), 0, st, a, nodesum);
     return hipGetLastError();
 }
 
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st) {
-    hipLaunchKernelGGL(w_update_kernel, dim3(a.n_cseg), dim3(256), 0, st, a, nodesum);
-    hipLaunchKernelGGL(conv_final_kernel, dim3((a.P + 255) / 256), dim3(256), 0, st, a, convpart);
+    hipLaunchKernelGGL(w_update_kernel, dim3(a.n_cseg), dim3(256), 0, st, a, nodesum, convpart);
     return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@ int pdhg_num_variants();
 void pdhg_variant_shape(int v, int* out6);
 hipError_t pdhg_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t prep_launch(const PrepArgs& a, hipStream_t stream);
+hipError_t schedule_launch(const int* iters, int S, int unit, int* order, hipStream_t st);
 int pdhg_local_num_variants();
 void pdhg_local_variant_shape(int v, int* out4);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
@@ -68,6 +69,10 @@ struct phg_handle {
     double *xs = nullptr, *ys = nullptr, *omega = nullptr, *x_out = nullptr, *y_out = nullptr;
     double *xN = nullptr, *obj = nullptr, *bound = nullptr, *kkt = nullptr, *eval = nullptr;
     int *iters = nullptr, *status = nullptr;
+    int* order = nullptr;      // launch schedule (schedule.hip)
+    bool have_order = false;
+    double* pinned = nullptr;  // page-locked readback buffer (convergence partials)
+    int summary[2] = {0, 0};   // scenarios not optimal / NaN, as of the last phg_conv_finish
     int* nonant_col_d = nullptr;
     Layout lay{};
     LocalLayout loc{};
@@ -75,7 +80,12 @@ struct phg_handle {
     double *nodesum = nullptr, *convpart = nullptr;
     std::vector<int> nonant_col_h;
     // timing of the last launches (HIP events on the handle's stream)
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // per-launch timing since the last phg_timing_reset: event pairs of every solve (0) and every
+    // PH update (1), read only when phg_timing is called -- no per-launch host synchronisation
+    std::vector<hipEvent_t> tev[2];
+    int tcount[2] = {0, 0};
+    int timing_mask = 0;       // bit 0: time solves, bit 1: time PH updates
+    long long* iters_acc = nullptr;
 };
 
 template <class T>
@@ -96,6 +106,20 @@ static int dput(phg_handle* h, T** p, const T* src, size_t count) {
     return 0;
 }
 
+static int timing_event(phg_handle* h, int which, int half) {
+    if (!(h->timing_mask & (1 << which))) return 0;
+    std::vector<hipEvent_t>& v = h->tev[which];
+    const size_t idx = 2 * (size_t)h->tcount[which] + half;
+    while (v.size() <= idx) {
+        hipEvent_t e;
+        CK(hipEventCreate(&e));
+        v.push_back(e);
+    }
+    CK(hipEventRecord(v[idx], h->stream));
+    if (half == 1) h->tcount[which]++;
+    return 0;
+}
+
 extern "C" {
 
 const char* phg_last_error(void) { return g_err.c_str(); }
@@ -113,7 +137,6 @@ int phg_create(int device, phg_handle** out) {
         return fail("phg_create: hipStreamCreate failed");
     }
     h->own_stream = true;
-    for (auto& e : h->ev) CK(hipEventCreate(&e));
     *out = h;
     return 0;
 }
@@ -123,8 +146,9 @@ void phg_destroy(phg_handle* h) {
     (void)hipSetDevice(h->device);
     (void)hipStreamSynchronize(h->stream);
     for (void* p : h->allocs) (void)hipFree(p);
-    for (auto& e : h->ev)
-        if (e) (void)hipEventDestroy(e);
+    if (h->pinned) (void)hipHostFree(h->pinned);
+    for (auto& v : h->tev)
+        for (auto& e : v) (void)hipEventDestroy(e);
     if (h->own_stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -425,7 +449,9 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     std::vector<std::vector<NodeSeg>> per_node(b->n_nodes);
     for (int lv = 0; lv < L; ++lv) {
         const int klen = b->level_len[lv];
-        const int chunk = std::max(1, 8192 / std::max(1, klen));
+        // ~8 scenarios per thread of a 256-thread workgroup: enough workgroups to hide the load
+        // latency at small S, whole-row coalesced streaming at large S
+        const int chunk = klen >= 256 ? 8 : 8 * (256 / std::max(1, klen));
         int s = 0;
         while (s < S) {
             const int g = b->scen_node[s * L + lv];
@@ -458,7 +484,7 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
         }
     }
     std::vector<int> cv, cs0, cs1, vfirst(P + 1, 0);
-    const int cchunk = std::max(1, 8192 / std::max(1, N));
+    const int cchunk = std::max(1, 2048 / std::max(1, N));   // ~8 elements per thread
     {
         int s = 0;
         std::vector<std::vector<int>> tmp0(P), tmp1(P);
@@ -508,11 +534,17 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     if (dput(h, &ip, cs0.data(), cs0.size())) return -1; a.cseg_s0 = ip;
     if (dput(h, &ip, cs1.data(), cs1.size())) return -1; a.cseg_s1 = ip;
     if (dalloc(h, &dp, cv.size())) return -1; a.csegpart = dp;
+    if (dalloc(h, &ip, 2 * cv.size())) return -1; a.csegbad = ip;
+    {
+        unsigned* t;
+        if (dalloc(h, &t, 2)) return -1;
+        a.ticket = t;
+    }
     if (dput(h, &ip, vfirst.data(), vfirst.size())) return -1; a.vr_first = ip;
     if (dput(h, &ip, xidx.data(), xidx.size())) return -1; h->xidx = ip;
     a.xidx = h->xidx;
     if (dalloc(h, &h->nodesum, 2 * (size_t)b->N_tot)) return -1;
-    if (dalloc(h, &h->convpart, 2 * (size_t)P)) return -1;
+    if (dalloc(h, &h->convpart, 2 * (size_t)P + 2)) return -1;
     return 0;
 }
 
@@ -626,9 +658,12 @@ int phg_load_batch(phg_handle* h, const phg_batch* b) {
     if (dalloc(h, &h->eval, S)) return -1;
     if (dalloc(h, &h->iters, S)) return -1;
     if (dalloc(h, &h->status, S)) return -1;
+    if (dalloc(h, &h->iters_acc, S)) return -1;
+    if (dalloc(h, &h->order, S)) return -1;
     h->nonant_col_h.assign(b->nonant_col, b->nonant_col + N);
     if (dput(h, &h->nonant_col_d, b->nonant_col, N)) return -1;
     if (build_ph_tables(h, b)) return -1;
+    h->ph.status = h->status;
     h->ph.xN = h->xN; h->ph.W = h->W; h->ph.rho = h->rho; h->ph.xbar = h->xbar; h->ph.xsqbar = h->xsqbar;
     // preconditioning
     PrepArgs pa{};
@@ -672,7 +707,7 @@ static double* field_ptr(phg_handle* h, int f, size_t* count) {
         case PHG_F_EVAL: *count = S; return h->eval;
         case PHG_F_KKT: *count = S; return h->kkt;
         case PHG_F_FIXED: *count = S * N; return h->fixed;
-        case PHG_F_CONV_PART: *count = 2 * (size_t)h->P; return h->convpart;
+        case PHG_F_CONV_PART: *count = 2 * (size_t)h->P + 2; return h->convpart;
         case PHG_F_OMEGA: *count = S; return h->omega;
         default: return nullptr;
     }
@@ -724,20 +759,27 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.xs = h->xs; a.ys = h->ys; a.omega = h->omega;
     a.x_out = h->x_out; a.y_out = h->y_out; a.xN = h->xN; a.obj = h->obj; a.bound = h->bound;
     a.kkt = h->kkt; a.iters = h->iters; a.status = h->status;
+    a.order = (o->schedule && h->have_order) ? h->order : nullptr;
+    a.iters_acc = h->iters_acc;
     a.w_on = w_on; a.prox_on = prox_on; a.fix_nonants = o->fix_nonants; a.warm = o->warm_start;
     a.max_iter = o->max_iter; a.check_every = o->check_every; a.eps = o->eps_rel; a.sense = h->sense;
-    CK(hipEventRecord(h->ev[0], h->stream));
+    if (h->local_variant >= 0) a.check_every = (a.check_every + 1) & ~1;   // 2 iterations per trip
+    if (timing_event(h, 0, 0)) return -1;
     a.loc = h->loc;
     if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
-    CK(hipEventRecord(h->ev[1], h->stream));
+    if (timing_event(h, 0, 1)) return -1;
+    if (o->schedule) {
+        CK(schedule_launch(h->iters, h->S, a.check_every, h->order, h->stream));
+        h->have_order = true;
+    }
     return 0;
 }
 
 int phg_node_sums(phg_handle* h, double* dev_nodesum) {
     if (!h || !h->loaded) return fail("phg_node_sums: no batch loaded");
     CK(hipSetDevice(h->device));
-    CK(hipEventRecord(h->ev[2], h->stream));
+    if (timing_event(h, 1, 0)) return -1;
     CK(node_sums_launch(h->ph, dev_nodesum ? dev_nodesum : h->nodesum, h->stream));
     return 0;
 }
@@ -747,20 +789,31 @@ int phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpar
     CK(hipSetDevice(h->device));
     CK(w_update_launch(h->ph, dev_nodesum ? dev_nodesum : h->nodesum,
                        dev_convpart ? dev_convpart : h->convpart, h->stream));
-    CK(hipEventRecord(h->ev[3], h->stream));
+    if (timing_event(h, 1, 1)) return -1;
     return 0;
 }
 
 int phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_conv) {
     if (!h || !h->loaded) return fail("phg_conv_finish: no batch loaded");
-    std::vector<double> cp(2 * (size_t)h->P);
-    CK(hipMemcpyAsync(cp.data(), dev_convpart ? dev_convpart : h->convpart, cp.size() * sizeof(double),
+    const size_t ncp = 2 * (size_t)h->P + 2;
+    if (!h->pinned) CK(hipHostMalloc((void**)&h->pinned, ncp * sizeof(double), hipHostMallocDefault));
+    double* cp = h->pinned;
+    CK(hipMemcpyAsync(cp, dev_convpart ? dev_convpart : h->convpart, ncp * sizeof(double),
                       hipMemcpyDeviceToHost, h->stream));
     CK(hipStreamSynchronize(h->stream));
     double tot = 0.0;
     for (int v = 0; v < h->P; ++v)
         if (cp[2 * v + 1] > 0.0) tot += cp[2 * v] / cp[2 * v + 1];
     *host_conv = tot / (double)h->P;
+    h->summary[0] = (int)cp[2 * (size_t)h->P];
+    h->summary[1] = (int)cp[2 * (size_t)h->P + 1];
+    return 0;
+}
+
+int phg_solve_summary(phg_handle* h, int32_t* out2) {
+    if (!h || !h->loaded) return fail("phg_solve_summary: no batch loaded");
+    out2[0] = h->summary[0];
+    out2[1] = h->summary[1];
     return 0;
 }
 
@@ -786,14 +839,37 @@ int phg_exchange_buffers(phg_handle* h, double** ns, double** cp) {
     return 0;
 }
 
-// elapsed ms between the events of the last phg_solve (which=0) / PH update (which=1)
-int phg_last_ms(phg_handle* h, int32_t which, double* ms) {
-    if (!h) return fail("null handle");
-    float f = 0.f;
-    CK(hipEventSynchronize(h->ev[which == 0 ? 1 : 3]));
-    CK(hipEventElapsedTime(&f, h->ev[which == 0 ? 0 : 2], h->ev[which == 0 ? 1 : 3]));
-    *ms = f;
+int phg_timing_reset(phg_handle* h, int32_t enable) {
+    if (!h || !h->loaded) return fail("phg_timing_reset: no batch loaded");
+    CK(hipStreamSynchronize(h->stream));
+    h->tcount[0] = h->tcount[1] = 0;
+    h->timing_mask = enable & 3;
+    CK(hipMemsetAsync(h->iters_acc, 0, (size_t)h->S * sizeof(long long), h->stream));
+    CK(hipStreamSynchronize(h->stream));
     return 0;
 }
+
+int phg_timing(phg_handle* h, int32_t which, double* total_ms, int32_t* launches, int64_t* pdhg_iters) {
+    if (!h || !h->loaded) return fail("phg_timing: no batch loaded");
+    if (which < 0 || which > 1) return fail("phg_timing: which must be 0 (solves) or 1 (PH updates)");
+    CK(hipStreamSynchronize(h->stream));
+    double tot = 0.0;
+    for (int k = 0; k < h->tcount[which]; ++k) {
+        float f = 0.f;
+        CK(hipEventElapsedTime(&f, h->tev[which][2 * k], h->tev[which][2 * k + 1]));
+        tot += f;
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = h->tcount[which];
+    if (pdhg_iters) {
+        std::vector<long long> acc(h->S);
+        CK(hipMemcpy(acc.data(), h->iters_acc, acc.size() * sizeof(long long), hipMemcpyDeviceToHost));
+        long long t = 0;
+        for (long long v : acc) t += v;
+        *pdhg_iters = t;
+    }
+    return 0;
+}
+
 
 }  // extern "C"

@@ -74,6 +74,8 @@ struct PdhgArgs {
     double* kkt;            // [S]
     int*    iters;          // [S]
     int*    status;         // [S]
+    const int* order;       // [S] launch order (scenario of work item i), or nullptr = identity
+    long long* iters_acc;   // [S] PDHG iterations accumulated over solves (phg_timing_reset zeroes)
     int w_on, prox_on, fix_nonants, warm, max_iter, check_every;
     double eps, sense;
 };
@@ -124,8 +126,10 @@ struct PhArgs {
     const int* cseg_s0;     // [n_cseg]
     const int* cseg_s1;
     double* csegpart;       // [n_cseg]
+    int* csegbad;           // [2*n_cseg] scenarios not optimal / NaN in the last solve
     const int* vr_first;    // [P+1] conv segments of vrank v
-    double* convpart;       // [2*P]
+    const int* status;      // [S] status of the last solve (may be null)
+    unsigned* ticket;       // [2] last-workgroup counters of the two kernels (zeroed)
 };
 
 }  // namespace phg

@@ -75,6 +75,21 @@ __device__ __forceinline__ double clamp_sel(double v, double lo, double hi) {
     return v > hi ? hi : v;
 }
 
+// raw v_max_f64 / v_min_f64: IEEE-mode fmax/fmin must quiet signalling NaNs, so the compiler
+// re-canonicalises every operand it cannot prove canonical (loop-carried bounds included: one
+// extra v_max_f64 per operand per use).  Our operands come from arithmetic or are finite/inf
+// bounds, never sNaN, so the bare instructions are exact here.
+__device__ __forceinline__ double vmax(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmin(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // opaque to the optimiser: stops loop-invariant code motion from hoisting address arithmetic /
 // loads used only by the rarely-run check and epilogue code into registers held across the
 // hot loop

@@ -165,7 +165,7 @@ class Engine:
         S, n, m, N = self.batch.S, self.batch.n, self.batch.m, self.N
         return {_lib.F_X: S * n, _lib.F_Y: S * m, _lib.F_XN: S * N, _lib.F_W: S * N, _lib.F_RHO: S * N,
                 _lib.F_XBAR: self.N_tot, _lib.F_XSQBAR: self.N_tot, _lib.F_OBJ: S, _lib.F_BOUND: S,
-                _lib.F_EVAL: S, _lib.F_KKT: S, _lib.F_FIXED: S * N, _lib.F_CONV_PART: 2 * self.P,
+                _lib.F_EVAL: S, _lib.F_KKT: S, _lib.F_FIXED: S * N, _lib.F_CONV_PART: 2 * self.P + 2,
                 _lib.F_OMEGA: S}[field]
 
     def get(self, field):
@@ -184,9 +184,9 @@ class Engine:
 
     # ------------------------------------------------------------------ hot path
     def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=64, warm_start=3,
-              fix_nonants=False):
+              fix_nonants=False, schedule=True):
         o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(warm_start),
-                         int(bool(fix_nonants)))
+                         int(bool(fix_nonants)), int(bool(schedule)))
         import ctypes
         _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))
 
@@ -209,12 +209,23 @@ class Engine:
         _lib.check(self.lib.phg_conv_finish(self.h, cp, ctypes.byref(v)))
         return v.value
 
+    def solve_summary(self):
+        """(scenarios not at the KKT tolerance, numerical failures) of the solve preceding the last
+        PH update, as read back by :meth:`conv_finish` (summed over GPUs)."""
+        out = np.zeros(2, np.int32)
+        _lib.check(self.lib.phg_solve_summary(self.h, ptr(out)))
+        return int(out[0]), int(out[1])
+
     def eval_objective(self, w_on, prox_on):
         _lib.check(self.lib.phg_eval_objective(self.h, int(w_on), int(prox_on)))
         return self.get(_lib.F_EVAL)
 
-    def last_ms(self, which):
+    def timing_reset(self, solves=True, updates=False):
+        _lib.check(self.lib.phg_timing_reset(self.h, int(bool(solves)) | (2 if updates else 0)))
+
+    def timing(self, which):
+        """(total ms, launches, PDHG iterations summed over scenarios) since timing_reset."""
         import ctypes
-        v = ctypes.c_double()
-        _lib.check(self.lib.phg_last_ms(self.h, int(which), ctypes.byref(v)))
-        return v.value
+        ms, n, it = ctypes.c_double(), ctypes.c_int32(), ctypes.c_int64()
+        _lib.check(self.lib.phg_timing(self.h, int(which), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(it)))
+        return ms.value, n.value, it.value

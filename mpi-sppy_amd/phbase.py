@@ -28,7 +28,8 @@ from .spbase import SPBase
 
 # PDHG controls read from iter0_solver_options / iterk_solver_options (other solver options,
 # e.g. "mipgap" or "threads", belong to CPU solvers and are ignored)
-_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": 64, "pdhg_keep_omega": False}
+_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": 64, "pdhg_keep_omega": False,
+                    "pdhg_schedule": True}
 
 
 class PHBase(SPBase):
@@ -107,7 +108,7 @@ class PHBase(SPBase):
                 stream = torch.cuda.current_stream(device).cuda_stream
                 if self.n_proc > 1:
                     exchange = (torch.zeros(2 * batch.N_tot, dtype=torch.float64, device=f"cuda:{device}"),
-                                torch.zeros(2 * batch.virt_nproc, dtype=torch.float64, device=f"cuda:{device}"))
+                                torch.zeros(2 * batch.virt_nproc + 2, dtype=torch.float64, device=f"cuda:{device}"))
         except ImportError:
             pass
         return device, stream, exchange
@@ -181,11 +182,26 @@ class PHBase(SPBase):
         t0 = time.perf_counter()
         self.engine.solve(w_on, prox_on, eps=o["pdhg_eps"], max_iter=o["pdhg_max_iter"],
                           check_every=o["pdhg_check_every"],
-                          warm_start=(1 | (2 if o["pdhg_keep_omega"] else 0)) if warm_start else 0)
-        self.engine.sync()
+                          warm_start=(1 | (2 if o["pdhg_keep_omega"] else 0)) if warm_start else 0,
+                          schedule=o["pdhg_schedule"])
         self.solve_count += self.engine.S
+        # The launch is asynchronous: the statuses reach the host with the next convergence
+        # readback (phg_solve_summary, checked in convergence_diff), so a PH iteration costs one
+        # host synchronisation; feas_prob / infeas_prob (Iter0) and dtiming fetch them at once.
+        self._status_pending = (gripe, need_solution)
+        if dtiming:
+            self._check_status_now(gripe, need_solution)
+        if dtiming and self.cylinder_rank == 0:
+            print(f"batched solve of {self.engine.S} subproblems: {time.perf_counter() - t0:.4f} s")
+        if self.extobject is not None:
+            self.extobject.post_solve_loop()
+        self.W_on, self.prox_on = saved if (dis_W or dis_prox) else (self.W_on, self.prox_on)
+
+    def _check_status_now(self, gripe, need_solution):
+        """Per-scenario statuses of the last solve (synchronous; spopt.py:194-231 semantics)."""
         status = self.engine.get_i32(_lib.I_STATUS)
         self._feasible = status != 2
+        self._status_pending = None
         if gripe and (status != 0).any():
             bad = [self.local_scenario_names[i] for i in np.nonzero(status != 0)[0][:5]]
             print(f"[{self.__class__.__name__}] {int((status != 0).sum())} subproblem(s) did not reach "
@@ -193,11 +209,19 @@ class PHBase(SPBase):
         if need_solution and (status == 2).any():
             raise RuntimeError("PDHG numerical failure (NaN) in scenario(s) "
                                f"{[self.local_scenario_names[i] for i in np.nonzero(status == 2)[0][:5]]}")
-        if dtiming and self.cylinder_rank == 0:
-            print(f"batched solve of {self.engine.S} subproblems: {time.perf_counter() - t0:.4f} s")
-        if self.extobject is not None:
-            self.extobject.post_solve_loop()
-        self.W_on, self.prox_on = saved if (dis_W or dis_prox) else (self.W_on, self.prox_on)
+
+    def _check_status_summary(self):
+        """Deferred status check of the solve before this PH update (counts summed over ranks)."""
+        pend = getattr(self, "_status_pending", None)
+        if pend is None:
+            return
+        gripe, need_solution = pend
+        self._status_pending = None
+        n_bad, n_nan = self.engine.solve_summary()
+        if gripe and n_bad and self.cylinder_rank == 0:
+            print(f"[{self.__class__.__name__}] {n_bad} subproblem(s) did not reach the KKT tolerance")
+        if need_solution and n_nan:
+            raise RuntimeError(f"PDHG numerical failure (NaN) in {n_nan} subproblem(s)")
 
     # ------------------------------------------------------------------------------- PH update
     def Compute_Xbar(self, verbose=False):
@@ -216,7 +240,9 @@ class PHBase(SPBase):
         """``phbase.py:349-371``: mean over (virtual) ranks of the per-rank mean |x - xbar|."""
         if self.engine.exchange is not None:
             self.mpicomm.allreduce_sum_(self.engine.exchange[1])
-        return self.engine.conv_finish()
+        conv = self.engine.conv_finish()
+        self._check_status_summary()
+        return conv
 
     # ------------------------------------------------------------------------------- expectations
     def _rank_fsum(self, vals):
@@ -246,11 +272,18 @@ class PHBase(SPBase):
     def _update_E1(self):
         self.E1 = self._rank_fsum(list(self.engine.batch.prob))
 
+    def _statuses(self):
+        if getattr(self, "_status_pending", None) is not None:
+            self._check_status_now(*self._status_pending)
+        return self._feasible
+
     def feas_prob(self):
+        self._statuses()
         p = self.engine.batch.prob
         return self._rank_fsum([p[k] for k in range(len(p)) if self._feasible[k]])
 
     def infeas_prob(self):
+        self._statuses()
         p = self.engine.batch.prob
         return self._rank_fsum([p[k] for k in range(len(p)) if not self._feasible[k]])
 
@@ -390,6 +423,7 @@ class PHBase(SPBase):
 
     def post_loops(self, extensions=None):
         """``phbase.py:1064-1119``."""
+        self._statuses()          # the last solve's statuses (deferred inside iterk_loop)
         self.mpicomm.Barrier()
         if self.scenario_denouement is not None:
             self._load_solutions()

@@ -95,7 +95,7 @@ class NumpyEngine:
         b = self.batch
         ns = self.exchange[0].numpy()
         self.xbar = ns[:self.N_tot].copy()
-        cp = np.zeros(2 * self.P)
+        cp = np.zeros(2 * self.P + 2)
         avg = b.S_global / self.P
         for s in range(self.S):
             gs = b.scen_global0 + s
@@ -112,6 +112,10 @@ class NumpyEngine:
 
     def eval_objective(self, w_on, prox_on):
         return self.obj.copy()
+
+    def solve_summary(self):
+        cp = self.exchange[1].numpy()
+        return int(cp[2 * self.P]), int(cp[2 * self.P + 1])
 
 
 def _worker(rank, world, port, case, q):
@@ -137,7 +141,7 @@ def _worker(rank, world, port, case, q):
                 batch = BatchArrays(models, self.all_nodenames, [m._mpisppy_probability for m in models],
                                     self.scen_global0, len(self.all_scenario_names), self._virt_nproc())
                 ex = (torch.zeros(2 * batch.N_tot, dtype=torch.float64),
-                      torch.zeros(2 * batch.virt_nproc, dtype=torch.float64))
+                      torch.zeros(2 * batch.virt_nproc + 2, dtype=torch.float64))
                 self.engine = NumpyEngine(batch, ex)
                 self.engine.set(0 + 4, float(self.options["defaultPHrho"]))
 

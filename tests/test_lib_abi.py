@@ -30,8 +30,30 @@ def test_library_exports():
     _lib.load()
 
 
-def test_struct_layout():
-    # phg_batch field order/size must match include/phg.h (64-bit ABI)
-    assert ctypes.sizeof(_lib.PhgOpts) == 24
-    names = [f[0] for f in _lib.PhgBatch._fields_]
-    assert names[:4] == ["S", "n", "m", "nnz"] and names[-3:] == ["scen_global0", "S_global", "virt_nproc"]
+def _c_layout(struct, fields):
+    """sizeof / offsetof of a header struct as gcc lays it out (the C ABI the library is built to)."""
+    import shutil
+    import subprocess
+    import tempfile
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    body = "\n".join(f'printf("%zu\\n", offsetof({struct}, {f}));' for f in fields)
+    src = (f'#include <stdio.h>\n#include <stddef.h>\n#include "phg.h"\nint main(void) {{\n'
+           f'printf("%zu\\n", sizeof({struct}));\n{body}\nreturn 0; }}\n')
+    with tempfile.TemporaryDirectory() as d:
+        c, exe = os.path.join(d, "t.c"), os.path.join(d, "t")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split()
+    return [int(v) for v in out]
+
+
+@pytest.mark.parametrize("struct,cls", [("phg_batch", "PhgBatch"), ("phg_opts", "PhgOpts")])
+def test_struct_layout(struct, cls):
+    """ctypes mirrors of the header structs have gcc's size and field offsets."""
+    ct = getattr(_lib, cls)
+    fields = [f[0] for f in ct._fields_]
+    want = _c_layout(struct, fields)
+    assert ctypes.sizeof(ct) == want[0]
+    for f, off in zip(fields, want[1:]):
+        assert getattr(ct, f).offset == off, f
