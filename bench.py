@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local"],
                     help="PDHG data layout (include/phg.h: phg_set_layout)")
     ap.add_argument("--no-schedule", action="store_true", help="launch scenarios in index order")
+    ap.add_argument("--check-every", type=int, default=32, help="PDHG restart/termination check interval")
+    ap.add_argument("--beta-art", type=float, default=0.0, help="artificial restart fraction (0: default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
 
@@ -74,7 +76,8 @@ def main():
     names = farmer.scenario_names_creator(S)
     opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
             "convthresh": 1e-4, "verbose": False, "display_progress": False, "pdhg_layout": args.layout,
-            "pdhg_schedule": not args.no_schedule,
+            "pdhg_schedule": not args.no_schedule, "pdhg_check_every": args.check_every,
+            "pdhg_beta_artificial": args.beta_art,
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps}}
     t_setup = time.perf_counter()
     ph = PH(dict(opts), names, farmer.scenario_creator, mpicomm=comm,

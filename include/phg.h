@@ -77,7 +77,13 @@ typedef struct phg_opts {
     int32_t warm_start;    /* bit 0: start from the previous x, y; bit 1: keep its primal weight */
     int32_t fix_nonants;   /* 1: nonants fixed to the values set by phg_set_fixed (xhat) */
     int32_t schedule;      /* 1: launch scenarios heaviest-first by the previous solve's PDHG
-                              iteration counts (device radix sort after each solve)          */
+                              iteration counts (device counting sort after each solve)       */
+    /* restart rule (PDLP-style; <= 0 selects the default): restart when the KKT error of the
+     * candidate drops below beta_sufficient x the last restart's, or below beta_necessary x it
+     * while rising, or after beta_artificial x (iterations so far) without a restart          */
+    double  beta_sufficient;   /* default 0.2  */
+    double  beta_necessary;    /* default 0.8  */
+    double  beta_artificial;   /* default 0.25 (tuned on PH prox-QPs; PDLP uses 0.36) */
 } phg_opts;
 
 /* solve modes (mpisppy/phbase.py:670-760: W_on / prox_on toggles) */

@@ -14,7 +14,7 @@
 //   s.t. rl <= A x <= ru, cl <= x <= cu
 // Algorithm: PDHG (Chambolle-Pock) on the Ruiz + Pock-Chambolle scaled problem with the
 // diagonal Hessian treated exactly in the primal prox, constant step eta/||A||, PDLP-style
-// adaptive restarts to the average/current iterate (beta 0.2 / 0.8 / 0.36) with primal-weight
+// adaptive restarts to the average/current iterate (beta 0.2 / 0.8 / 0.25) with primal-weight
 // updates, and a relative KKT termination test on the UNscaled problem.
 #include "phg_internal.h"
 #include "wave_ops.h"
@@ -332,9 +332,9 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
         const double k_cur = wkkt_of(o, omega), k_avg = wkkt_of(o + 6, omega);
         const bool use_avg = k_avg < k_cur;
         const double cand = use_avg ? k_avg : k_cur;
-        const bool restart = (cand <= 0.2 * kkt_restart) ||
-                             (cand <= 0.8 * kkt_restart && cand > kkt_prev) ||
-                             ((double)since >= 0.36 * (double)it);
+        const bool restart = (cand <= a.beta_suf * kkt_restart) ||
+                             (cand <= a.beta_nec * kkt_restart && cand > kkt_prev) ||
+                             ((double)since >= a.beta_art * (double)it);
         kkt_prev = cand;
         if (restart) {
             if (use_avg) {

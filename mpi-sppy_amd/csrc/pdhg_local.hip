@@ -468,9 +468,9 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         const bool use_avg = k_avg < k_cur;
         const double cand = use_avg ? k_avg : k_cur;
         const double krst = CS(CI::SC + CI::KRST);
-        const bool restart = live && ((cand <= 0.2 * krst) ||
-                                      (cand <= 0.8 * krst && cand > CS(CI::SC + CI::KPREV)) ||
-                                      ((double)since >= 0.36 * (double)it));
+        const bool restart = live && ((cand <= a.beta_suf * krst) ||
+                                      (cand <= a.beta_nec * krst && cand > CS(CI::SC + CI::KPREV)) ||
+                                      ((double)since >= a.beta_art * (double)it));
         CS(CI::SC + CI::KPREV) = cand;
         if (wave_any(restart)) {
             const bool ra = restart && use_avg;

@@ -763,6 +763,9 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.iters_acc = h->iters_acc;
     a.w_on = w_on; a.prox_on = prox_on; a.fix_nonants = o->fix_nonants; a.warm = o->warm_start;
     a.max_iter = o->max_iter; a.check_every = o->check_every; a.eps = o->eps_rel; a.sense = h->sense;
+    a.beta_suf = o->beta_sufficient > 0 ? o->beta_sufficient : 0.2;
+    a.beta_nec = o->beta_necessary > 0 ? o->beta_necessary : 0.8;
+    a.beta_art = o->beta_artificial > 0 ? o->beta_artificial : 0.25;
     if (h->local_variant >= 0) a.check_every = (a.check_every + 1) & ~1;   // 2 iterations per trip
     if (timing_event(h, 0, 0)) return -1;
     a.loc = h->loc;

@@ -78,6 +78,7 @@ struct PdhgArgs {
     long long* iters_acc;   // [S] PDHG iterations accumulated over solves (phg_timing_reset zeroes)
     int w_on, prox_on, fix_nonants, warm, max_iter, check_every;
     double eps, sense;
+    double beta_suf, beta_nec, beta_art;   // restart rule
 };
 
 struct PrepArgs {

@@ -183,10 +183,10 @@ class Engine:
         return out
 
     # ------------------------------------------------------------------ hot path
-    def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=64, warm_start=3,
-              fix_nonants=False, schedule=True):
+    def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=32, warm_start=3,
+              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0)):
         o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(warm_start),
-                         int(bool(fix_nonants)), int(bool(schedule)))
+                         int(bool(fix_nonants)), int(bool(schedule)), *[float(v) for v in beta])
         import ctypes
         _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))
 
