@@ -121,9 +121,11 @@ int  phg_sync(phg_handle* h);
 
 /* PDHG data layout, chosen at phg_load_batch (call before it):
  *   AUTO   : the lane-local register layout (pdhg_local.hip) when the pattern splits into blocks
- *            that fit a lane plus <= a few coupling rows, else the LDS-gather layout (pdhg.hip)
- *   GATHER : always the LDS-gather layout;  LOCAL : lane-local or fail                          */
-enum { PHG_LAYOUT_AUTO = 0, PHG_LAYOUT_GATHER = 1, PHG_LAYOUT_LOCAL = 2 };
+ *            that fit a lane plus <= a few coupling rows, else the wave LDS-gather layout
+ *            (pdhg.hip, n, m <= 256), else the workgroup-per-scenario streaming layout
+ *            (pdhg_block.hip, n, m up to 4096)
+ *   GATHER / LOCAL / BLOCK : that layout or fail                                                */
+enum { PHG_LAYOUT_AUTO = 0, PHG_LAYOUT_GATHER = 1, PHG_LAYOUT_LOCAL = 2, PHG_LAYOUT_BLOCK = 3 };
 int  phg_set_layout(phg_handle* h, int32_t policy);
 /* host-only dry run of the lane-local planner (no device needed): out8 = {local variant or -1,
  * lanes per scenario, columns per lane, rows per lane, coupling-row slots, coupling rows used,
@@ -135,7 +137,8 @@ int  phg_set(phg_handle* h, int32_t field, const double* host_in);
 int  phg_get(phg_handle* h, int32_t field, double* host_out);
 int  phg_get_i32(phg_handle* h, int32_t field, int32_t* host_out);
 int  phg_info(phg_handle* h, int32_t* out8);   /* S, n, m, nnz, N, N_tot, kernel variant
-                                                  (>= 100: lane-local), lanes per scenario */
+                                                  (>= 100: lane-local, >= 200: workgroup),
+                                                  lanes (threads) per scenario             */
 
 /* Solve every scenario's subproblem (solve_loop):
  *   min-form  c^T x + w_on * sum_k W_k x_k + prox_on * sum_k rho_k/2 (x_k - xbar_k)^2      */

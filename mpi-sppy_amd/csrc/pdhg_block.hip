@@ -1,0 +1,475 @@
+// pdhg_block.hip -- batched PDHG for scenario LPs/QPs too large for one wavefront (gfx950).
+//
+// Same algorithm, restart rule and outputs as pdhg.hip / pdhg_local.hip (replaces
+// SPOpt.solve_one, mpisppy/spopt.py:184-231, for every local scenario), mapped for n, m in the
+// hundreds to thousands (sslp: 705 x 60, netdes: 2940 x 1520):
+//
+//   * one workgroup of NT = 256 / 512 / 1024 threads per scenario; the iterates x, y and the
+//     SpMV partial sums live in LDS, per-column / per-row state in registers (CPL / RPL slots);
+//   * A x and A^T y are CSR / CSC SpMVs over "pieces" of <= 8 consecutive entries of a row /
+//     column.  Piece p belongs to thread p % NT (slot p / NT); its values are STREAMED from memory
+//     every iteration in a piece-major layout [slot][entry][thread], so a wave's loads are
+//     coalesced 512-byte rows (the HBM-bound streaming path of SURVEY 8(d)1); when every scenario
+//     has the same matrix the layout is stored once and served from L2 / MALL;
+//   * a row's pieces are consecutive, so the row owner adds its pieces' partials from LDS in a
+//     fixed order (deterministic, no atomics); four workgroup barriers per PDHG iteration.
+#include "phg_internal.h"
+#include "wave_ops.h"
+
+namespace phg {
+
+// workgroup all-reduce of K <= 16 values: DPP wave sums, wave partials to LDS, thread k adds value
+// k's NT/64 partials in wave order, every thread reads the K totals back (same bits everywhere)
+template <int NT, int K>
+__device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
+    constexpr int NW = NT / 64;
+    static_assert(K <= 16, "block_sum scratch holds 16 values");
+    gsum_many<64, K>(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[k * NW + w] = v[k];
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        double t = red[k * NW];
+#pragma unroll 1
+        for (int u = 1; u < NW; ++u) t += red[k * NW + u];
+        red[16 * NW + k] = t;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = red[16 * NW + k];
+}
+
+template <int NT, int CPL, int RPL, int PPT, int QPT>
+__global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const BlockLayout& B = a.blk;
+    const int t = threadIdx.x;
+    const int s = a.order ? a.order[blockIdx.x] : blockIdx.x;
+    double* xl = smem;                   // [n_pad]
+    double* yl = xl + B.n_pad;           // [m_pad]
+    double* rp = yl + B.m_pad;           // [PPT*NT] row-piece partials
+    double* cp = rp + PPT * NT;          // [QPT*NT] column-piece partials
+    double* red = cp + QPT * NT;         // [16 * (NT/64 + 1)] reduction scratch
+    const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
+    const double* rv = B.rvals + (long)s * B.vstride_r;
+    const double* cv = B.cvals + (long)s * B.vstride_c;
+
+    // ------------------------------------------------------------------ columns owned
+    int cj[CPL], cf[CPL], cn[CPL];
+    // restart reference points live in the xs / ys state arrays (each thread reads back only the
+    // elements it wrote), not in registers
+    double x[CPL], aty[CPL], c[CPL], q[CPL], lo[CPL], hi[CPL], ip[CPL], xsum[CPL];
+    double prox_const = 0.0, c2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int j = B.col_of[k * NT + t];
+        cj[k] = j;
+        cf[k] = B.col_pfirst[k * NT + t];
+        cn[k] = B.col_pcnt[k * NT + t];
+        x[k] = aty[k] = c[k] = q[k] = lo[k] = hi[k] = xsum[k] = 0.0;
+        if (j >= 0) {
+            const long b = sn + j;
+            const double d = a.dc[b];
+            double cc = a.c[b], qq = 0.0;
+            double lo_ = a.cl[b], hi_ = a.cu[b];
+            const int kk = a.lay.col_nonant[j];
+            if (kk >= 0) {
+                const long tt = sN + kk;
+                if (a.w_on) cc += a.W[tt];
+                if (a.prox_on) {
+                    const double r = a.rho[tt];
+                    const double xb = a.xbar[a.xidx[tt]];
+                    cc -= r * xb;
+                    qq = r;
+                    prox_const += 0.5 * r * xb * xb;
+                }
+                if (a.fix_nonants) { lo_ = hi_ = a.fixed[tt] / d; }
+            }
+            c2 += cc * cc;
+            c[k] = cc * d;
+            q[k] = qq * d * d;
+            lo[k] = lo_;
+            hi[k] = hi_;
+            x[k] = clampd((a.warm & 1) ? a.xs[b] : 0.0, lo_, hi_);
+            a.xs[b] = x[k];
+        }
+    }
+    // ------------------------------------------------------------------ rows owned
+    int ri[RPL], rf[RPL], rn[RPL];
+    double y[RPL], ax[RPL], rlo[RPL], rhi[RPL], ysum[RPL];
+    double b2 = 0.0;
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+        const int i = B.row_of[r * NT + t];
+        ri[r] = i;
+        rf[r] = B.row_pfirst[r * NT + t];
+        rn[r] = B.row_pcnt[r * NT + t];
+        y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
+        if (i >= 0) {
+            const long b = sm + i;
+            rlo[r] = a.rl[b];
+            rhi[r] = a.ru[b];
+            double yy = (a.warm & 1) ? a.ys[b] : 0.0;
+            if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
+            if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];
+            y[r] = yy;
+            a.ys[b] = yy;
+        }
+    }
+
+    // ------------------------------------------------------------------ SpMVs through LDS
+    // A x for the x currently in xl: pieces -> rp, barrier, row owners add their pieces
+    auto spmv_ax = [&](double (&out)[RPL]) {
+        int off = 0;
+#pragma unroll
+        for (int ps = 0; ps < PPT; ++ps) {
+            const int kk = B.rk[ps];
+            double acc = 0.0;
+#pragma unroll 2
+            for (int k = 0; k < kk; ++k) {
+                const int e = off + k * NT + t;
+                acc = fma(rv[e], xl[B.ridx[e]], acc);
+            }
+            rp[ps * NT + t] = acc;
+            off += kk * NT;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            double acc = 0.0;
+#pragma unroll 1
+            for (int u = 0; u < rn[r]; ++u) acc += rp[rf[r] + u];
+            out[r] = acc;
+        }
+    };
+    // A^T y for the y currently in yl
+    auto spmv_aty = [&](double (&out)[CPL]) {
+        int off = 0;
+#pragma unroll
+        for (int ps = 0; ps < QPT; ++ps) {
+            const int kk = B.ck[ps];
+            double acc = 0.0;
+#pragma unroll 2
+            for (int k = 0; k < kk; ++k) {
+                const int e = off + k * NT + t;
+                acc = fma(cv[e], yl[B.cidx[e]], acc);
+            }
+            cp[ps * NT + t] = acc;
+            off += kk * NT;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            double acc = 0.0;
+#pragma unroll 1
+            for (int u = 0; u < cn[k]; ++u) acc += cp[cf[k] + u];
+            out[k] = acc;
+        }
+    };
+    auto put_x = [&](const double (&v)[CPL]) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if (cj[k] >= 0) xl[cj[k]] = v[k];
+    };
+    auto put_y = [&](const double (&v)[RPL]) {
+#pragma unroll
+        for (int r = 0; r < RPL; ++r)
+            if (ri[r] >= 0) yl[ri[r]] = v[r];
+    };
+    // products at the current point (x, y): ends with every partial consumed
+    auto products = [&]() {
+        __syncthreads();
+        put_x(x);
+        put_y(y);
+        __syncthreads();
+        spmv_ax(ax);
+        spmv_aty(aty);
+        __syncthreads();
+    };
+
+    // ------------------------------------------------------------------ scalars
+    double omega, cnorm;
+    {
+        double rr[4] = {c2, prox_const, 0.0, b2};
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
+        block_sum<NT, 4>(rr, red);
+        cnorm = sqrt(rr[0]);
+        prox_const = rr[1];
+        const double cn_ = sqrt(rr[2]), bn = sqrt(rr[3]);
+        omega = (cn_ > 1e-10 && bn > 1e-10) ? cn_ / bn : 1.0;
+        if ((a.warm & 2) && a.omega[s] > 0.0) omega = a.omega[s];
+    }
+    const double bnorm = a.bnorm[s];
+    const double eta = a.eta[s];
+    double tau = eta / omega, sig = eta * omega;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) ip[k] = 1.0 / (1.0 + tau * q[k]);
+    products();
+
+    // KKT pieces of one iterate (see pdhg.hip), reduced over the workgroup
+    auto kkt = [&](const double (&xx)[CPL], const double (&at)[CPL], const double (&yy)[RPL],
+                   const double (&axx)[RPL], double* o) {
+        double v[6] = {0, 0, 0, 0, 0, 0};
+        const int sl = launder(s);
+        const long sn_ = (long)sl * a.n, sm_ = (long)sl * a.m;
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            seq();
+            if (ri[r] >= 0) {
+                const double pr = axx[r] - clampd(axx[r], rlo[r], rhi[r]);
+                v[0] += pr * pr;
+                const double pu = pr / a.dr[sm_ + ri[r]];
+                v[2] += pu * pu;
+                if (fin(rlo[r])) v[5] += rlo[r] * fmax(yy[r], 0.0);
+                if (fin(rhi[r])) v[5] += rhi[r] * fmin(yy[r], 0.0);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            seq();
+            if (cj[k] >= 0) {
+                const double rc_ = c[k] + q[k] * xx[k] - at[k];
+                double dres = 0.0;
+                if (!fin(lo[k]) && rc_ > 0.0) dres += rc_;
+                if (!fin(hi[k]) && rc_ < 0.0) dres += rc_;
+                v[1] += dres * dres;
+                const double du = dres / a.dc[sn_ + cj[k]];
+                v[3] += du * du;
+                v[4] += c[k] * xx[k] + 0.5 * q[k] * xx[k] * xx[k];
+                if (fin(lo[k])) v[5] += lo[k] * fmax(rc_, 0.0);
+                if (fin(hi[k])) v[5] += hi[k] * fmin(rc_, 0.0);
+                v[5] -= 0.5 * q[k] * xx[k] * xx[k];
+            }
+        }
+        block_sum<NT, 6>(v, red);
+#pragma unroll
+        for (int u = 0; u < 6; ++u) o[u] = v[u];
+    };
+    auto rel_of = [&](const double* o) {
+        const double p = sqrt(o[2]) / (1.0 + bnorm);
+        const double d = sqrt(o[3]) / (1.0 + cnorm);
+        const double g = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
+        return fmax(fmax(p, d), g);
+    };
+    auto wkkt_of = [&](const double* o, double w) {
+        const double g = o[4] - o[5];
+        return sqrt(w * w * o[0] + o[1] / (w * w) + g * g);
+    };
+
+    double kkt_restart, kkt_prev = INFINITY;
+    {
+        double o[6];
+        kkt(x, aty, y, ax, o);
+        kkt_restart = wkkt_of(o, omega);
+    }
+    int it = 0, since = 0, cnt = 0, st = 1;
+    double rel_final = INFINITY, pobj = 0.0, dobj = 0.0;
+    bool use_avg_final = false;
+    const int chk = a.check_every;
+
+    while (true) {
+        for (int kk = 0; kk < chk; ++kk) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const double xn = clampd(fma(tau, aty[k] - c[k], x[k]) * ip[k], lo[k], hi[k]);
+                x[k] = xn;
+                xsum[k] += xn;
+            }
+            put_x(x);
+            __syncthreads();
+            double axn[RPL];
+            spmv_ax(axn);
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+                const double g = y[r] - sig * (2.0 * axn[r] - ax[r]);
+                y[r] = fmax(fma(sig, rlo[r], g), 0.0) + fmin(fma(sig, rhi[r], g), 0.0);   // 0 on empty slots
+                ax[r] = axn[r];
+                ysum[r] += y[r];
+            }
+            put_y(y);
+            __syncthreads();
+            spmv_aty(aty);
+        }
+        it += chk;
+        since += chk;
+        cnt += chk;
+
+        // ---------------------------------------------------------- restart / termination check
+        const double inv = 1.0 / (double)cnt;
+        double oc[6], oa[6];
+        kkt(x, aty, y, ax, oc);
+        {
+            double xa[CPL], ya[RPL], ata[CPL], axa[RPL];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) xa[k] = xsum[k] * inv;
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) ya[r] = ysum[r] * inv;
+            __syncthreads();
+            put_x(xa);
+            put_y(ya);
+            __syncthreads();
+            spmv_ax(axa);
+            spmv_aty(ata);
+            kkt(xa, ata, ya, axa, oa);
+        }
+        const double rel_cur = rel_of(oc), rel_avg = rel_of(oa);
+        const bool nan = !(rel_cur == rel_cur);
+        if (nan || rel_cur <= a.eps || rel_avg <= a.eps || it >= a.max_iter) {
+            use_avg_final = !nan && rel_avg < rel_cur;
+            rel_final = use_avg_final ? rel_avg : rel_cur;
+            pobj = use_avg_final ? oa[4] : oc[4];
+            dobj = use_avg_final ? oa[5] : oc[5];
+            st = nan ? 2 : ((rel_cur <= a.eps || rel_avg <= a.eps) ? 0 : 1);
+            break;
+        }
+        const double k_cur = wkkt_of(oc, omega), k_avg = wkkt_of(oa, omega);
+        const bool use_avg = k_avg < k_cur;
+        const double cand = use_avg ? k_avg : k_cur;
+        const bool restart = (cand <= a.beta_suf * kkt_restart) ||
+                             (cand <= a.beta_nec * kkt_restart && cand > kkt_prev) ||
+                             ((double)since >= a.beta_art * (double)it);
+        kkt_prev = cand;
+        if (restart) {
+            if (use_avg) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) x[k] = xsum[k] * inv;
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) y[r] = ysum[r] * inv;
+            }
+            double mv[2] = {0.0, 0.0};
+            {
+                const int sl = launder(s);
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    seq();
+                    if (cj[k] >= 0) {
+                        const long b = (long)sl * a.n + cj[k];
+                        const double d = x[k] - a.xs[b];
+                        mv[0] += d * d;
+                        a.xs[b] = x[k];
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) {
+                    seq();
+                    if (ri[r] >= 0) {
+                        const long b = (long)sl * a.m + ri[r];
+                        const double d = y[r] - a.ys[b];
+                        mv[1] += d * d;
+                        a.ys[b] = y[r];
+                    }
+                }
+            }
+            block_sum<NT, 2>(mv, red);
+            const double dx = sqrt(mv[0]), dy = sqrt(mv[1]);
+            if (dx > 1e-10 && dy > 1e-10) omega = sqrt(dy / dx * omega);
+            tau = eta / omega;
+            sig = eta * omega;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) { ip[k] = 1.0 / (1.0 + tau * q[k]); xsum[k] = 0.0; }
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) ysum[r] = 0.0;
+            cnt = 0;
+            since = 0;
+            kkt_restart = cand;
+            kkt_prev = INFINITY;
+        }
+        products();   // exact A x, A^T y at the current point (xl/yl held the average)
+    }
+
+    // ------------------------------------------------------------------ outputs
+    const double inv = cnt > 0 ? 1.0 / (double)cnt : 0.0;
+    const double offs = a.obj_off[s] + (a.prox_on ? prox_const : 0.0);
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        if (cj[k] >= 0) {
+            const long b = sn + cj[k];
+            const double xv = use_avg_final ? xsum[k] * inv : x[k];
+            a.xs[b] = xv;
+            const double xu = xv * a.dc[b];
+            a.x_out[b] = xu;
+            const int kk = a.lay.col_nonant[cj[k]];
+            if (kk >= 0) a.xN[sN + kk] = xu;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+        if (ri[r] >= 0) {
+            const long b = sm + ri[r];
+            const double yv = use_avg_final ? ysum[r] * inv : y[r];
+            a.ys[b] = yv;
+            a.y_out[b] = yv * a.dr[b];
+        }
+    }
+    if (t == 0) {
+        a.omega[s] = omega;
+        a.obj[s] = a.sense * (pobj + offs);
+        a.bound[s] = a.sense * (dobj + offs);
+        a.kkt[s] = rel_final;
+        a.iters[s] = it;
+        a.iters_acc[s] += it;
+        a.status[s] = st;
+    }
+}
+
+// ----------------------------------------------------------------------------- dispatch
+struct BlockVariant {
+    int NT, CPL, RPL, PPT, QPT;
+    void (*fn)(PdhgArgs);
+};
+
+#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, pdhg_block_kernel<a_, b_, c_, d_, e_>}
+// preference order: smallest workgroup that holds the problem
+static const BlockVariant kBlockVariants[] = {
+    PHG_B(256, 3, 1, 2, 3),      // sslp-like: n <= 768, m <= 256
+    PHG_B(256, 4, 4, 4, 4),      // n, m, pieces <= 1024
+    PHG_B(512, 4, 4, 4, 4),      // <= 2048
+    PHG_B(1024, 3, 2, 3, 3),     // netdes-like: n <= 3072, m <= 2048
+    PHG_B(1024, 4, 4, 4, 4),     // <= 4096
+};
+#undef PHG_B
+
+int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
+
+void pdhg_block_variant_shape(int v, int* out5) {
+    const BlockVariant& V = kBlockVariants[v];
+    out5[0] = V.NT; out5[1] = V.CPL; out5[2] = V.RPL; out5[3] = V.PPT; out5[4] = V.QPT;
+}
+
+size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad) {
+    const BlockVariant& V = kBlockVariants[v];
+    return (size_t)(n_pad + m_pad + V.PPT * V.NT + V.QPT * V.NT + 16 * (V.NT / 64 + 1)) * sizeof(double);
+}
+
+hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream) {
+    const BlockVariant& V = kBlockVariants[v];
+    const size_t lds = pdhg_block_lds_bytes(v, a.blk.n_pad, a.blk.m_pad);
+    hipLaunchKernelGGL(V.fn, dim3(a.S), dim3(V.NT), lds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace phg
+
+namespace phg {
+
+// piece-major value copies: out[s][e] = vals[s][perm[e]] (0 where perm < 0); grid (ceil(E/256), S')
+__global__ void piece_gather_kernel(const double* vals, int nnz, const int* perm, int E, double* out) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const long s = blockIdx.y;
+    if (e >= E) return;
+    const int p = perm[e];
+    out[s * E + e] = p >= 0 ? vals[s * nnz + p] : 0.0;
+}
+
+hipError_t piece_gather_launch(const double* vals, int nnz, const int* perm, int E, int S, double* out,
+                               hipStream_t st) {
+    hipLaunchKernelGGL(piece_gather_kernel, dim3((E + 255) / 256, S), dim3(256), 0, st, vals, nnz, perm, E, out);
+    return hipGetLastError();
+}
+
+}  // namespace phg

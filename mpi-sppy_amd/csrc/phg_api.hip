@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -24,6 +25,12 @@ hipError_t schedule_launch(const int* iters, int S, int unit, int* order, hipStr
 int pdhg_local_num_variants();
 void pdhg_local_variant_shape(int v, int* out4);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
+int pdhg_block_num_variants();
+void pdhg_block_variant_shape(int v, int* out5);
+size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad);
+hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
+hipError_t piece_gather_launch(const double* vals, int nnz, const int* perm, int E, int S, double* out,
+                               hipStream_t st);
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
 hipError_t eval_obj_launch(int S, int n, int N, const double* x, const double* c, const double* obj_off,
@@ -57,6 +64,10 @@ struct phg_handle {
     double sense = 1.0;
     int variant = -1;          // gather kernel variant (pdhg.hip), or
     int local_variant = -1;    // lane-local kernel variant (pdhg_local.hip); preferred when >= 0
+    int block_variant = -1;    // workgroup-per-scenario kernel variant (pdhg_block.hip)
+    int bshape[5] = {0};
+    std::vector<int> block_rperm, block_cperm;   // piece layout -> CSR position (host copies)
+    bool vals_shared = false;
     int layout_policy = PHG_LAYOUT_AUTO;
     int vshape[6] = {0};
     int lshape[4] = {0};
@@ -76,6 +87,7 @@ struct phg_handle {
     int* nonant_col_d = nullptr;
     Layout lay{};
     LocalLayout loc{};
+    BlockLayout blk{};
     PhArgs ph{};
     double *nodesum = nullptr, *convpart = nullptr;
     std::vector<int> nonant_col_h;
@@ -168,7 +180,7 @@ int phg_set_stream(phg_handle* h, void* s) {
 int phg_set_layout(phg_handle* h, int32_t policy) {
     if (!h) return fail("null handle");
     if (h->loaded) return fail("phg_set_layout: must be called before phg_load_batch");
-    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_LOCAL) return fail("phg_set_layout: bad policy");
+    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_BLOCK) return fail("phg_set_layout: bad policy");
     h->layout_policy = policy;
     return 0;
 }
@@ -548,6 +560,128 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     return 0;
 }
 
+// Workgroup-per-scenario layout (pdhg_block.hip): owner slots and <= kPiece-entry pieces.
+// Returns 0 (built), 1 (no variant fits), -1 (error).  Values are gathered into the piece layout
+// after preconditioning (build_block_values).
+static constexpr int kPiece = 8;
+
+static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vector<int>& colptr,
+                              const std::vector<int>& csc_row, const std::vector<int>& csc_p) {
+    const int n = b->n, m = b->m;
+    // pieces in row (column) order
+    std::vector<int> rpf(m), rpc(m), cpf(n), cpc(n);
+    std::vector<int> rps, rpl, cps, cpl;   // start position, length
+    for (int i = 0; i < m; ++i) {
+        rpf[i] = (int)rps.size();
+        for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; p += kPiece) {
+            rps.push_back(p);
+            rpl.push_back(std::min(kPiece, b->rowptr[i + 1] - p));
+        }
+        rpc[i] = (int)rps.size() - rpf[i];
+    }
+    for (int j = 0; j < n; ++j) {
+        cpf[j] = (int)cps.size();
+        for (int e = colptr[j]; e < colptr[j + 1]; e += kPiece) {
+            cps.push_back(e);
+            cpl.push_back(std::min(kPiece, colptr[j + 1] - e));
+        }
+        cpc[j] = (int)cps.size() - cpf[j];
+    }
+    const int n_pad = (n + 1) & ~1, m_pad = (m + 1) & ~1;
+    int sh[5], chosen = -1;
+    for (int v = 0; v < pdhg_block_num_variants(); ++v) {
+        pdhg_block_variant_shape(v, sh);
+        const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4];
+        if (n > CPL * NT || m > RPL * NT || (int)rps.size() > PPT * NT || (int)cps.size() > QPT * NT) continue;
+        if (pdhg_block_lds_bytes(v, n_pad, m_pad) > 160 * 1024) continue;
+        chosen = v;
+        break;
+    }
+    if (chosen < 0) {
+        char msg[256];
+        snprintf(msg, sizeof msg, "phg_load_batch: no workgroup PDHG variant fits n=%d m=%d (%zu/%zu pieces)", n, m,
+                 rps.size(), cps.size());
+        g_err = msg;
+        return 1;
+    }
+    pdhg_block_variant_shape(chosen, sh);
+    const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4];
+    h->block_variant = chosen;
+    std::memcpy(h->bshape, sh, sizeof sh);
+    BlockLayout& L = h->blk;
+    L.n_pad = n_pad;
+    L.m_pad = m_pad;
+    std::vector<int> col_of(CPL * NT, -1), colf(CPL * NT, 0), colc(CPL * NT, 0);
+    for (int j = 0; j < n; ++j) {
+        const int idx = (j / NT) * NT + j % NT;
+        col_of[idx] = j; colf[idx] = cpf[j]; colc[idx] = cpc[j];
+    }
+    std::vector<int> row_of(RPL * NT, -1), rowf(RPL * NT, 0), rowc(RPL * NT, 0);
+    for (int i = 0; i < m; ++i) {
+        const int idx = (i / NT) * NT + i % NT;
+        row_of[idx] = i; rowf[idx] = rpf[i]; rowc[idx] = rpc[i];
+    }
+    // piece-major entry layout
+    auto lay = [&](const std::vector<int>& ps, const std::vector<int>& pl, int SLOTS, int* kk,
+                   const std::function<int(int)>& idx_of, const std::function<int(int)>& pos_of,
+                   std::vector<int>& idx, std::vector<int>& perm) {
+        for (int sl = 0; sl < 8; ++sl) kk[sl] = 0;
+        for (size_t p = 0; p < ps.size(); ++p) kk[p / NT] = std::max(kk[p / NT], pl[p]);
+        int tot = 0;
+        std::vector<int> off(SLOTS + 1, 0);
+        for (int sl = 0; sl < SLOTS; ++sl) { off[sl] = tot; tot += kk[sl] * NT; }
+        idx.assign(std::max(1, tot), 0);
+        perm.assign(std::max(1, tot), -1);
+        for (size_t p = 0; p < ps.size(); ++p) {
+            const int sl = (int)p / NT, t = (int)p % NT;
+            for (int k = 0; k < pl[p]; ++k) {
+                const int e = off[sl] + k * NT + t;
+                idx[e] = idx_of(ps[p] + k);
+                perm[e] = pos_of(ps[p] + k);
+            }
+        }
+        return tot;
+    };
+    std::vector<int> ridx, cidx;
+    const int rtot = lay(rps, rpl, PPT, L.rk, [&](int p) { return b->colidx[p]; }, [&](int p) { return p; }, ridx,
+                         h->block_rperm);
+    const int ctot = lay(cps, cpl, QPT, L.ck, [&](int e) { return csc_row[e]; }, [&](int e) { return csc_p[e]; }, cidx,
+                         h->block_cperm);
+    (void)rtot; (void)ctot;
+    int* p;
+    if (dput(h, &p, col_of.data(), col_of.size())) return -1; L.col_of = p;
+    if (dput(h, &p, colf.data(), colf.size())) return -1; L.col_pfirst = p;
+    if (dput(h, &p, colc.data(), colc.size())) return -1; L.col_pcnt = p;
+    if (dput(h, &p, row_of.data(), row_of.size())) return -1; L.row_of = p;
+    if (dput(h, &p, rowf.data(), rowf.size())) return -1; L.row_pfirst = p;
+    if (dput(h, &p, rowc.data(), rowc.size())) return -1; L.row_pcnt = p;
+    if (dput(h, &p, ridx.data(), ridx.size())) return -1; L.ridx = p;
+    if (dput(h, &p, cidx.data(), cidx.size())) return -1; L.cidx = p;
+    return 0;
+}
+
+// piece-major copies of the (preconditioned) values; one copy when every scenario has the same A
+static int build_block_values(phg_handle* h) {
+    BlockLayout& L = h->blk;
+    const int Er = (int)h->block_rperm.size(), Ec = (int)h->block_cperm.size();
+    const int Sv = h->vals_shared ? 1 : h->S;
+    int* rperm;
+    int* cperm;
+    double* rv;
+    double* cv;
+    if (dput(h, &rperm, h->block_rperm.data(), Er)) return -1;
+    if (dput(h, &cperm, h->block_cperm.data(), Ec)) return -1;
+    if (dalloc(h, &rv, (size_t)Sv * Er)) return -1;
+    if (dalloc(h, &cv, (size_t)Sv * Ec)) return -1;
+    CK(piece_gather_launch(h->vals, h->nnz, rperm, Er, Sv, rv, h->stream));
+    CK(piece_gather_launch(h->vals, h->nnz, cperm, Ec, Sv, cv, h->stream));
+    L.rvals = rv;
+    L.cvals = cv;
+    L.vstride_r = h->vals_shared ? 0 : Er;
+    L.vstride_c = h->vals_shared ? 0 : Ec;
+    return 0;
+}
+
 int phg_plan(const phg_batch* b, int32_t* out8) {
     if (!b || !out8) return fail("phg_plan: null argument");
     if (b->n <= 0 || b->m <= 0 || !b->rowptr || !b->colidx) return fail("phg_plan: empty pattern");
@@ -615,15 +749,30 @@ int phg_load_batch(phg_handle* h, const phg_batch* b) {
         if (dput(h, &p, col_nonant.data(), col_nonant.size())) return -1;
         h->lay.col_nonant = p;
     }
-    int lr = 1, gr = 1;
-    if (h->layout_policy != PHG_LAYOUT_GATHER) {
+    // layout: lane-local (block-structured patterns) > wave gather (n, m <= 256) > workgroup block
+    int lr = 1, gr = 1, br = 1;
+    const int pol = h->layout_policy;
+    if (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_LOCAL) {
         lr = build_local_layout(h, b);
         if (lr < 0) return -1;
-        if (lr > 0 && h->layout_policy == PHG_LAYOUT_LOCAL) return -1;
+        if (lr > 0 && pol == PHG_LAYOUT_LOCAL) return -1;
     }
-    if (lr != 0) {
+    if (lr != 0 && (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_GATHER)) {
         gr = build_layout(h, b, colptr, csc_row, csc_p);
-        if (gr != 0) return -1;
+        if (gr < 0 || (gr > 0 && pol == PHG_LAYOUT_GATHER)) return -1;
+    }
+    if (lr != 0 && gr != 0) {
+        br = build_block_layout(h, b, colptr, csc_row, csc_p);
+        if (br != 0) return -1;
+        h->variant = -1;
+    }
+    // one matrix for all scenarios? (then the block kernel streams a single copy)
+    {
+        bool same = true;
+        const size_t nz = (size_t)b->nnz;
+        for (int s2 = 1; s2 < b->S && same; ++s2)
+            same = std::memcmp(b->vals, b->vals + s2 * nz, nz * sizeof(double)) == 0;
+        h->vals_shared = same;
     }
     // min-form objective
     std::vector<double> cmin((size_t)S * n), off((size_t)S, 0.0);
@@ -679,6 +828,7 @@ int phg_load_batch(phg_handle* h, const phg_batch* b) {
     pa.vals = h->vals; pa.dc = h->dc; pa.dr = h->dr; pa.cl = h->cl; pa.cu = h->cu; pa.rl = h->rl;
     pa.ru = h->ru; pa.eta = h->eta; pa.bnorm = h->bnorm; pa.scratch = scratch;
     CK(prep_launch(pa, h->stream));
+    if (h->block_variant >= 0 && build_block_values(h)) return -1;
     CK(hipStreamSynchronize(h->stream));
     h->loaded = true;
     return 0;
@@ -688,6 +838,7 @@ int phg_info(phg_handle* h, int32_t* o) {
     if (!h || !h->loaded) return fail("phg_info: no batch loaded");
     o[0] = h->S; o[1] = h->n; o[2] = h->m; o[3] = h->nnz; o[4] = h->N; o[5] = h->N_tot;
     if (h->local_variant >= 0) { o[6] = 100 + h->local_variant; o[7] = h->lshape[0]; }
+    else if (h->block_variant >= 0) { o[6] = 200 + h->block_variant; o[7] = h->bshape[0]; }
     else { o[6] = h->variant; o[7] = 64; }
     return 0;
 }
@@ -769,7 +920,9 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     if (h->local_variant >= 0) a.check_every = (a.check_every + 1) & ~1;   // 2 iterations per trip
     if (timing_event(h, 0, 0)) return -1;
     a.loc = h->loc;
+    a.blk = h->blk;
     if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
+    else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
     if (timing_event(h, 0, 1)) return -1;
     if (o->schedule) {

@@ -39,10 +39,31 @@ struct LocalLayout {
     const int* cpl_p;       // [D*LPS*CPL]    CSR position of coupling entry on (lane, col slot) or -1
 };
 
+// Workgroup-per-scenario layout (pdhg_block.hip).  Owner slots: column j -> (slot j / NT,
+// thread j % NT), row i likewise.  Row (column) pieces: <= 8 consecutive CSR (CSC) entries; piece p
+// -> (slot p / NT, thread p % NT); entry k of a slot-ps piece of thread t sits at
+// e = sum_{s < ps} rk[s] NT + k NT + t in the piece-major value / index arrays (coalesced).
+struct BlockLayout {
+    int n_pad, m_pad;
+    const int* col_of;      // [CPL*NT]
+    const int* col_pfirst;  // [CPL*NT] first column piece (= LDS partial index) of the column
+    const int* col_pcnt;    // [CPL*NT]
+    const int* row_of;      // [RPL*NT]
+    const int* row_pfirst;  // [RPL*NT]
+    const int* row_pcnt;    // [RPL*NT]
+    int rk[8], ck[8];       // entries per piece slot (max over the slot's pieces)
+    const int* ridx;        // [sum rk NT] column of a row-piece entry (0 on padding)
+    const int* cidx;        // [sum ck NT] row of a column-piece entry
+    const double* rvals;    // [S or 1][sum rk NT] scaled values, row pieces (0 on padding)
+    const double* cvals;    // [S or 1][sum ck NT] scaled values, column pieces
+    long vstride_r, vstride_c;   // per-scenario strides (0: one matrix shared by all scenarios)
+};
+
 struct PdhgArgs {
     int S, n, m, nnz, N, n_pad;
     Layout lay;
     LocalLayout loc;
+    BlockLayout blk;
     // scenario data (scaled where noted)
     const double* vals;     // [S*nnz] scaled values
     const double* c;        // [S*n]   min-form objective, UNscaled

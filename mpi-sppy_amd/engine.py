@@ -124,7 +124,7 @@ def plan_layout(batch):
 class Engine:
     """One libphg handle on one GPU (no CPU fallback: raises if the library or device is missing)."""
 
-    LAYOUTS = {"auto": 0, "gather": 1, "local": 2}
+    LAYOUTS = {"auto": 0, "gather": 1, "local": 2, "block": 3}
 
     def __init__(self, batch, device=0, stream=None, exchange=None, layout="auto"):
         self.lib = _lib.load()
@@ -145,7 +145,7 @@ class Engine:
         _lib.check(self.lib.phg_info(self.h, ptr(info)))
         self.variant = int(info[6])
         self.lanes_per_scenario = int(info[7])
-        self.layout = "local" if self.variant >= 100 else "gather"
+        self.layout = "block" if self.variant >= 200 else ("local" if self.variant >= 100 else "gather")
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:

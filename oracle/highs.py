@@ -41,6 +41,13 @@ def solve(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=None, o
     c = np.asarray(c, dtype=np.float64)
     n = c.shape[0]
     m = len(rowptr) - 1
+    if qdiag is not None and np.any(np.asarray(qdiag) != 0) and n > 1000 and do_polish:
+        # large prox-QPs (netdes: 2940 columns, 1470 quadratic terms): HiGHS 1.8's active-set QP
+        # solver can take minutes; the interior-point oracle certifies them in seconds
+        from . import ipm
+        r = ipm.solve_qp(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=qdiag, offset=offset)
+        if r.ok:
+            return SolveResult("Optimal", r.x, r.obj)
     h = _hc._Highs()
     h.setOptionValue("output_flag", False)
     h.setOptionValue("threads", int(threads))
@@ -89,13 +96,58 @@ def solve(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=None, o
     rd = np.array(sol.row_dual, dtype=np.float64) if sol.dual_valid else None
     cd = np.array(sol.col_dual, dtype=np.float64) if sol.dual_valid else None
     if qdiag is not None and st == "Optimal" and do_polish:
-        xp, ok = polish(c, qdiag, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, x)
+        # 1. HiGHS's own point, when its duals certify it (relative KKT <= 1e-9);
+        # 2. else the exact active-set polish (small subproblems: dense KKT solves);
+        # 3. else the interior-point oracle (LP-dominated, degenerate prox-QPs such as sslp defeat
+        #    the single-swap polish)
+        ok = rd is not None and cd is not None and \
+            kkt_certify(c, qdiag, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, x, rd, cd) <= 1e-9
+        xp = x
+        if not ok and n <= 400:
+            xp, ok = polish(c, qdiag, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, x)
         if not ok:
-            raise RuntimeError("oracle QP polish failed to certify optimality")
+            from . import ipm
+            r = ipm.solve_qp(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=qdiag,
+                             offset=offset)
+            if not r.ok:
+                raise RuntimeError("oracle QP: HiGHS, the active-set polish and the IPM all failed to "
+                                   "certify optimality")
+            xp = r.x
         x = xp
         qd = np.asarray(qdiag, dtype=np.float64)
         obj = float(c @ x + 0.5 * np.sum(qd * x * x) + offset)
     return SolveResult(st, x, obj, rd, cd)
+
+
+def kkt_certify(c, qdiag, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, x, row_dual, col_dual):
+    """Relative KKT error of (x, duals) for the min-form QP (HiGHS sign convention: col_dual =
+    c + Q x - A^T row_dual; a positive dual means the lower bound is active)."""
+    c = np.asarray(c, float)
+    n = c.shape[0]
+    m = len(rowptr) - 1
+    A = np.zeros((m, n)) if m == 0 else None
+    ax = np.zeros(m)
+    aty = np.zeros(n)
+    for i in range(m):
+        for p in range(rowptr[i], rowptr[i + 1]):
+            ax[i] += vals[p] * x[colidx[p]]
+            aty[colidx[p]] += vals[p] * row_dual[i]
+    q = np.zeros(n) if qdiag is None else np.asarray(qdiag, float)
+    sc = 1.0 + np.abs(c).max(initial=0.0)
+    stat = np.abs(c + q * x - aty - col_dual).max(initial=0.0) / sc
+    xs = 1.0 + np.abs(x).max(initial=0.0)
+    axs = 1.0 + np.abs(ax).max(initial=0.0)
+    pr = max(np.maximum(np.asarray(col_lo) - x, x - np.asarray(col_hi)).max(initial=0.0) / xs,
+             np.maximum(np.asarray(row_lo) - ax, ax - np.asarray(row_hi)).max(initial=0.0) / axs, 0.0)
+    # complementarity: dual sign must match an active bound; measure |dual| * distance
+    dl = np.where(col_dual > 0, col_dual * (x - np.where(np.isfinite(col_lo), col_lo, -np.inf)), 0.0)
+    du = np.where(col_dual < 0, -col_dual * (np.where(np.isfinite(col_hi), col_hi, np.inf) - x), 0.0)
+    rl_ = np.where(row_dual > 0, row_dual * (ax - np.where(np.isfinite(row_lo), row_lo, -np.inf)), 0.0)
+    ru_ = np.where(row_dual < 0, -row_dual * (np.where(np.isfinite(row_hi), row_hi, np.inf) - ax), 0.0)
+    comp = max(np.abs(dl).max(initial=0), np.abs(du).max(initial=0), np.abs(rl_).max(initial=0),
+               np.abs(ru_).max(initial=0)) / (sc * max(xs, axs))
+    val = max(stat, pr, comp)
+    return val if np.isfinite(val) else np.inf
 
 
 def _dense(rowptr, colidx, vals, m, n):

@@ -11,6 +11,7 @@ the reference's nonant order) and the probability (None -> SPBase default 1/S,
 This module is written independently of the product's generators in ``mpi-sppy_amd/examples``;
 ``tests/test_models.py`` checks the two bit-for-bit.
 """
+import os
 import re
 
 import numpy as np
@@ -203,3 +204,87 @@ def hydro(scenario_name, branching_factors=(3, 3), inflow=None):
 
 def hydro_names(num_scens=9):
     return [f"Scen{i}" for i in range(1, num_scens + 1)]
+
+
+# ------------------------------------------------------------------------------------------------
+# sslp LP relaxation: examples/sslp/model/ReferenceModel.py + examples/sslp/sslp.py:26-46, data
+# sslp_15_45_10 (npz extract of the reference .dat files, tools/make_example_data.py)
+# ------------------------------------------------------------------------------------------------
+_EXDATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-sppy_amd",
+                       "examples", "data")
+
+
+def _npz(name):
+    z = np.load(os.path.join(_EXDATA, name))
+    return {k: z[k] for k in z.files}
+
+
+def sslp(scenario_name, penalty=1000.0):
+    k = extract_num(scenario_name)
+    d = _npz("sslp_15_45_10.npz")
+    P = d["client_present"]
+    if 1 <= k <= P.shape[0]:
+        present = P[k - 1].astype(float)
+    else:   # synthetic scale-up: Bernoulli(mean presence), default_rng([1134, k])
+        present = (np.random.default_rng([1134, k]).random(P.shape[1]) < P.mean(axis=0)).astype(float)
+    ns, nc = d["fixed_cost"].shape[0], d["revenue"].shape[0]
+    s = OScen(scenario_name)
+    # columns in the reference's component order: FacilityOpen, Allocation, Dummy
+    fo = {j: s.var(f"FacilityOpen[{j}]", 0.0, 1.0, float(d["fixed_cost"][j - 1])) for j in range(1, ns + 1)}
+    al = {}
+    for i in range(1, nc + 1):
+        for j in range(1, ns + 1):
+            al[i, j] = s.var(f"Allocation[({i}, {j})]", 0.0, 1.0, -float(d["revenue"][i - 1, j - 1]))
+    du = {j: s.var(f"Dummy[{j}]", 0.0, INF, penalty) for j in range(1, ns + 1)}
+    cap = float(d["capacity"])
+    for j in range(1, ns + 1):   # Demand . Allocation - Dummy <= Capacity FacilityOpen
+        co = {al[i, j]: float(d["demand"][i - 1, j - 1]) for i in range(1, nc + 1)
+              if d["demand"][i - 1, j - 1] != 0.0}
+        co[du[j]] = -1.0
+        co[fo[j]] = -cap
+        s.row(co, -INF, 0.0, f"DemandConstraint[{j}]")
+    for i in range(1, nc + 1):
+        s.row({al[i, j]: 1.0 for j in range(1, ns + 1)}, present[i - 1], present[i - 1], f"ClientConstraint[{i}]")
+    s.nodes = [dict(name="ROOT", cond_prob=1.0, stage=1, cols=[fo[j] for j in range(1, ns + 1)])]
+    s.prob = None
+    return s
+
+
+def sslp_names(num_scens, start=1):
+    return [f"Scenario{i}" for i in range(start, start + num_scens)]
+
+
+# ------------------------------------------------------------------------------------------------
+# netdes LP relaxation: examples/netdes/netdes.py:39-80 + parse.py, instance network-50-30-H-01
+# ------------------------------------------------------------------------------------------------
+def netdes(scenario_name, num_scens=None):
+    k = extract_num(scenario_name)
+    d = _npz("network-50-30-H-01.npz")
+    K = d["p"].shape[0]
+    base = k % K
+    dk, uk, bk = d["d"][base].copy(), d["u"][base].copy(), d["b"][base]
+    if k >= K:   # synthetic scale-up (documented in mpi-sppy_amd/examples/netdes.py)
+        rng = np.random.default_rng([1134, k])
+        dk = dk * rng.uniform(0.9, 1.1, dk.shape[0])
+        uk = uk * rng.uniform(1.0, 1.1, uk.shape[0])
+    E = [tuple(int(v) for v in e) for e in d["edges"]]
+    s = OScen(scenario_name)
+    x = [s.var(f"x[{e}]", 0.0, 1.0, float(d["c"][t])) for t, e in enumerate(E)]
+    y = [s.var(f"y[{e}]", 0.0, INF, float(dk[t])) for t, e in enumerate(E)]
+    for t in range(len(E)):
+        s.row({y[t]: 1.0, x[t]: -float(uk[t])}, -INF, 0.0, f"vubs[{t + 1}]")
+    for i in range(int(d["N"])):
+        co = {}
+        for t, (a, b) in enumerate(E):
+            if a == i:
+                co[y[t]] = co.get(y[t], 0.0) + 1.0
+            if b == i:
+                co[y[t]] = co.get(y[t], 0.0) - 1.0
+        s.row(co, float(bk[i]), float(bk[i]), f"bals[{i + 1}]")
+    s.nodes = [dict(name="ROOT", cond_prob=1.0, stage=1, cols=list(x))]
+    s.prob = float(d["p"][base]) if (num_scens is None or num_scens == K) and k < K else 1.0 / num_scens
+    return s
+
+
+def netdes_names(num_scens, start=0):
+    return [f"Scenario{i}" for i in range(start, start + num_scens)]

@@ -75,3 +75,35 @@ def test_batch_arrays_farmer_prob_default():
     assert all(m._mpisppy_probability == 0.2 for m in models)
     b = BatchArrays(models, sp.all_nodenames, [m._mpisppy_probability for m in models], 0, 5, 1)
     assert b.N == 6 and b.n == 24 and b.m == 19 and b.nnz == 54
+
+
+@pytest.mark.parametrize("sn", ["Scenario1", "Scenario7", "Scenario10", "Scenario11", "Scenario2048"])
+def test_sslp_bit_exact(sn):
+    from mpisppy_amd.examples import sslp
+    _same(sslp.scenario_creator(sn), om.sslp(sn))
+
+
+def test_sslp_sizes_and_synthetic_presence():
+    from mpisppy_amd.examples import sslp
+    m = sslp.scenario_creator("Scenario3")
+    assert (m.n, m.m, len(m.pattern()[1])) == (705, 60, 1364)
+    # synthetic scenarios are reproducible per scenario and differ from each other
+    a, b = sslp.client_present(11), sslp.client_present(12)
+    assert np.array_equal(a, sslp.client_present(11)) and not np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("sn,S", [("Scenario0", None), ("Scenario29", None), ("Scenario31", 64), ("Scenario1000", 1024)])
+def test_netdes_bit_exact(sn, S):
+    from mpisppy_amd.examples import netdes
+    mp = netdes.scenario_creator(sn, num_scens=S)
+    o = om.netdes(sn, num_scens=S)
+    _same(mp, o)
+    assert mp._mpisppy_probability == o.prob
+
+
+def test_netdes_sizes_and_balance():
+    from mpisppy_amd.examples import netdes
+    m = netdes.scenario_creator("Scenario5")
+    assert (m.n, m.m, len(m.pattern()[1]), len(m._mpisppy_node_list[0].nonant_vardata_list)) == (2940, 1520, 5880, 1470)
+    a = m.arrays()
+    assert abs(a["row_lo"][1470:].sum()) < 1e-9       # flow balance: sum of node demands is zero
