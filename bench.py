@@ -26,7 +26,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--scen", type=int, default=10000, help="scenarios PER GPU (weak scaling)")
+    ap.add_argument("--case", default="farmer", choices=["farmer", "sslp", "netdes"],
+                    help="workload: farmer (the BASELINE.json headline, configs[1]), sslp_15_45_10 or "
+                         "netdes network-50-30-H-01 LP relaxations (configs[2], configs[4])")
+    ap.add_argument("--scen", type=int, default=None,
+                    help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes")
     ap.add_argument("--cm", type=int, default=10)
     ap.add_argument("--rho", type=float, default=1.0)
     ap.add_argument("--eps", type=float, default=1e-9)
@@ -67,21 +71,31 @@ def main():
     _pkg.load()
     from mpisppy_amd import _lib
     from mpisppy_amd.comm import TorchComm
-    from mpisppy_amd.examples import farmer
+    from mpisppy_amd.examples import farmer, netdes, sslp
     from mpisppy_amd.ph import PH
     if world > 1:
         comm = TorchComm()
 
+    if args.scen is None:
+        args.scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024}[args.case]
     S = args.scen * world
-    names = farmer.scenario_names_creator(S)
+    if args.case == "farmer":
+        names, creator = farmer.scenario_names_creator(S), farmer.scenario_creator
+        ckw = {"crops_multiplier": args.cm, "num_scens": S}
+        desc = f"farmer crops_multiplier={args.cm}"
+    elif args.case == "sslp":
+        names, creator, ckw = sslp.scenario_names_creator(S), sslp.scenario_creator, {}
+        desc = "sslp_15_45_10 LP relaxation"
+    else:
+        names, creator, ckw = netdes.scenario_names_creator(S), netdes.scenario_creator, {"num_scens": S}
+        desc = "netdes network-50-30-H-01 LP relaxation"
     opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
             "convthresh": 1e-4, "verbose": False, "display_progress": False, "pdhg_layout": args.layout,
             "pdhg_schedule": not args.no_schedule, "pdhg_check_every": args.check_every,
             "pdhg_beta_artificial": args.beta_art,
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps}}
     t_setup = time.perf_counter()
-    ph = PH(dict(opts), names, farmer.scenario_creator, mpicomm=comm,
-            scenario_creator_kwargs={"crops_multiplier": args.cm, "num_scens": S})
+    ph = PH(dict(opts), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw)
     ph.PH_Prep()
     t_iter0 = time.perf_counter()
     ph.Iter0()
@@ -145,6 +159,13 @@ def main():
     flops_per_launch = f_it * pdhg_iters / args.steps
     avg_launch_s = pdhg_ms / args.steps / 1e3
     achieved_tf = flops_per_launch / avg_launch_s / 1e12
+    # SURVEY 8(d)1 streaming bytes per PDHG iteration per scenario: 16 nnz_distinct + 16 n + 16 m
+    # + 8 (n [c varies] + m [b varies]); distinct = CSR positions whose value differs across scenarios
+    nnz_distinct = int((b.vals != b.vals[0]).any(axis=0).sum()) if b.S > 1 else 0
+    c_var = bool((b.c != b.c[0]).any()) or True     # PH terms make every scenario's cost differ
+    b_var = bool((b.rl != b.rl[0]).any() or (b.ru != b.ru[0]).any())
+    bytes_it = 16 * nnz_distinct + 16 * b.n + 16 * b.m + 8 * (b.n * c_var + b.m * b_var)
+    achieved_gbs = bytes_it * pdhg_iters / args.steps / avg_launch_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -168,16 +189,25 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (farmer generator of examples/farmer/farmer.py, seeded per scenario)",
-        "config": {"workload": f"farmer crops_multiplier={args.cm}, {S} scenarios ({args.scen} per GPU), PH rho={args.rho}, "
+        "data": {"farmer": "synthetic (farmer generator of examples/farmer/farmer.py, seeded per scenario)",
+                 "sslp": "sslp_15_45_10 data (Scenario1-10) + seeded synthetic ClientPresent beyond 10",
+                 "netdes": "network-50-30-H-01 data (30 scenarios) + seeded synthetic cost/capacity noise beyond 30",
+                 }[args.case],
+        "config": {"workload": f"{desc}, {S} scenarios ({args.scen} per GPU), PH rho={args.rho}, "
                                f"PDHG eps_rel={args.eps}",
                    "scenarios": S, "n": b.n, "m": b.m, "nnz": b.nnz, "nonants": b.N,
                    "parallelism": f"scenario shards over {world} GPU(s)",
                    "pdhg_layout": eng.layout, "lanes_per_scenario": eng.lanes_per_scenario},
-        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 4), "peak": FP64_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 5),
-                     "traffic": traffic,
-                     "kernel": "pdhg_kernel (fp64 VALU; fp64 vector peak == fp64 matrix peak on MI355X)",
+        "roofline": ({"bound": "mfma", "achieved": round(achieved_tf, 4), "peak": FP64_PEAK_TFLOPS,
+                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 5)}
+                     if eng.layout != "block" else
+                     {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "bytes_per_pdhg_iter_per_scen": bytes_it,
+                      "nnz_distinct": nnz_distinct, "tflops_fp64": round(achieved_tf, 4)}) | {
+                     "traffic": traffic if args.case == "farmer" else None,
+                     "kernel": {"local": "pdhg_local_kernel (lane-local, fp64 VALU; fp64 vector peak == matrix peak)",
+                                "gather": "pdhg_kernel (wave LDS-gather, fp64 VALU)",
+                                "block": "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)"}[eng.layout],
                      "flops_per_pdhg_iter_per_scen": f_it,
                      "pdhg_iters_per_scen_per_step": round(pdhg_iters / args.steps / S_loc, 2),
                      "max_pdhg_iters": max_iters,
@@ -195,8 +225,7 @@ def main():
     # wall time to PH convergence < 1e-4 (fresh run, same instance)
     if args.conv_iters > 0:
         ph2 = PH(dict(opts, PHIterLimit=args.conv_iters, convthresh=1e-4,
-                      time_limit=args.conv_time), names, farmer.scenario_creator, mpicomm=comm,
-                 scenario_creator_kwargs={"crops_multiplier": args.cm, "num_scens": S})
+                      time_limit=args.conv_time), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw)
         ph2.PH_Prep()
         torch.cuda.synchronize()
         if comm is not None:
@@ -221,25 +250,27 @@ def main():
 
 
 def _cpu_worker(payload):
-    """Solve scenario prox-QPs with HiGHS (oracle restatement, threads=1) until the time budget."""
+    """Solve scenario prox-QPs with the oracle (HiGHS 1.8, threads=1; the oracle's interior-point
+    QP above 1000 columns, where HiGHS's active-set QP takes minutes) until the time budget."""
     import time as _t
     sys.path.insert(0, ROOT)
     from oracle import highs
     from oracle import models as om
-    names, cm, S, W, xbar, rho, budget = payload
+    case, names, kw, W, xbar, rho, budget = payload
+    build = {"farmer": om.farmer, "sslp": om.sslp, "netdes": om.netdes}[case]
     cnt = 0
     t0 = _t.perf_counter()
     for k, nm in enumerate(names):
-        sc = om.farmer(nm, crops_multiplier=cm, num_scens=S)
+        sc = build(nm, **kw)
         a = sc.arrays()
         cols = np.array(sc.nonant_cols())
         c = a["c"].copy()
         c[cols] += W[k] - rho * xbar
         q = np.zeros_like(c)
         q[cols] = rho
-        t1 = _t.perf_counter()
         highs.solve(c, a["rowptr"], a["colidx"], a["vals"], a["row_lo"], a["row_hi"], a["col_lo"],
-                    a["col_hi"], qdiag=q, offset=float(np.sum(rho / 2 * xbar * xbar)), do_polish=False)
+                    a["col_hi"], qdiag=q, offset=float(np.sum(rho / 2 * xbar * xbar)),
+                    do_polish=len(c) > 1000)
         cnt += 1
         if _t.perf_counter() - t0 > budget:
             break
@@ -247,8 +278,8 @@ def _cpu_worker(payload):
 
 
 def cpu_baseline(ph, args):
-    """The reference's CPU path restated (oracle): one HiGHS QP solve per scenario, P processes,
-    on the same W / xbar the GPU just used; bounded sample."""
+    """The reference's CPU path restated (oracle): one QP solve per scenario, P processes, on the
+    same W / xbar the GPU just used; bounded sample."""
     import multiprocessing as mp
     from mpisppy_amd import _lib
     try:
@@ -258,17 +289,21 @@ def cpu_baseline(ph, args):
         xbar = eng.get(_lib.F_XBAR)
         names = ph.local_scenario_names
         per = max(1, len(names) // P)
-        payloads = [(names[i * per:(i + 1) * per], args.cm, len(ph.all_scenario_names), W[i * per:(i + 1) * per], xbar,
-                     args.rho, args.cpu_seconds) for i in range(P)]
+        S = len(ph.all_scenario_names)
+        kw = {"farmer": {"crops_multiplier": args.cm, "num_scens": S}, "sslp": {}, "netdes": {"num_scens": S}}[args.case]
+        payloads = [(args.case, names[i * per:(i + 1) * per], kw, W[i * per:(i + 1) * per], xbar, args.rho,
+                     args.cpu_seconds) for i in range(P)]
         ctx = mp.get_context("spawn")
         with ctx.Pool(P) as pool:
             res = pool.map(_cpu_worker, payloads)
         n = sum(r[0] for r in res)
         t = max(r[1] for r in res)
+        solver = "HiGHS 1.8 via scipy, threads=1 each" if eng.batch.n <= 1000 else \
+            "oracle interior-point QP (numpy), one process each"
         return {"value": round(n / t, 2), "unit": "scenario-QP solves/s", "cores": P, "kind": "port",
-                "sample": f"{n} farmer cm={args.cm} prox-QPs (HiGHS 1.8 via scipy, threads=1 each) "
-                          f"on {P} processes for ~{args.cpu_seconds:.0f} s, same W/xbar as the GPU step; "
-                          "excludes Pyomo model/objective overhead (lower bound on mpi-sppy CPU time)"}
+                "sample": f"{n} {args.case} prox-QPs ({solver}) on {P} processes for "
+                          f"~{args.cpu_seconds:.0f} s, same W/xbar as the GPU step; excludes Pyomo "
+                          "model/objective overhead (lower bound on mpi-sppy CPU time)"}
     except Exception as e:  # the baseline must never sink the GPU measurement
         return {"value": None, "error": repr(e)}
 
