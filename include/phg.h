@@ -106,7 +106,10 @@ enum {
     PHG_F_FIXED = 11,   /* [S*N] values nonants are fixed to when opts.fix_nonants         */
     PHG_F_CONV_PART = 12,/* [2*virt_nproc+2] per-virtual-rank (sum |x-xbar|, count), then the
                             status counts of phg_solve_summary                              */
-    PHG_F_OMEGA = 13    /* [S] PDHG primal weight carried between solves                    */
+    PHG_F_OMEGA = 13,   /* [S] PDHG primal weight carried between solves                    */
+    PHG_F_Z = 14,       /* [S*N] smoothing centre z (smoothed PH)                          */
+    PHG_F_SMOOTH_P = 15,/* [S*N] smoothing weight p                                        */
+    PHG_F_SMOOTH_BETA = 16 /* [S*N] smoothing step beta                                    */
 };
 enum {
     PHG_I_ITERS = 0,    /* [S] PDHG iterations of the last solve                           */
@@ -159,6 +162,10 @@ int  phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_con
  * out2 = {scenarios not at the KKT tolerance, scenarios with a numerical failure}            */
 int  phg_solve_summary(phg_handle* h, int32_t* out2);
 int  phg_ph_update(phg_handle* h, double* host_conv);
+
+/* smoothed PH (phbase.py:329-346, 641-760): while on, every prox-on solve adds
+ * p/2 (x_k - z_k)^2 per nonant and phg_apply_xbar also does Update_z: z += beta (x - z)        */
+int  phg_set_smoothing(phg_handle* h, int32_t on);
 
 /* per-scenario objective with the CURRENT W/xbar/rho (pyo.value(objfct), spopt.py:365) */
 int  phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on);

@@ -36,7 +36,8 @@ class PhgOpts(C.Structure):
                 ("beta_artificial", C.c_double)]
 
 
-F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART, F_OMEGA = range(14)
+(F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART, F_OMEGA,
+ F_Z, F_SMOOTH_P, F_SMOOTH_BETA) = range(17)
 I_ITERS, I_STATUS = 0, 1
 
 # every symbol include/phg.h declares, with its ctypes signature
@@ -59,6 +60,7 @@ SIGNATURES = {
     "phg_conv_finish": (C.c_int, [C.c_void_p, C.c_void_p, f64p]),
     "phg_ph_update": (C.c_int, [C.c_void_p, f64p]),
     "phg_solve_summary": (C.c_int, [C.c_void_p, i32p]),
+    "phg_set_smoothing": (C.c_int, [C.c_void_p, C.c_int32]),
     "phg_eval_objective": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "phg_exchange_buffers": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "phg_timing_reset": (C.c_int, [C.c_void_p, C.c_int32]),

@@ -79,14 +79,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             const int kk = a.lay.col_nonant[j];
             if (kk >= 0) {
                 const long tt = sN + kk;
-                if (a.w_on) cc += a.W[tt];
-                if (a.prox_on) {
-                    const double r = a.rho[tt];
-                    const double xb = a.xbar[a.xidx[tt]];
-                    cc -= r * xb;
-                    qq = r;
-                    prox_const += 0.5 * r * xb * xb;
-                }
+                ph_terms(a, tt, cc, qq, prox_const);
                 if (a.fix_nonants) { lo_ = hi_ = a.fixed[tt] / d; }
             }
             c2 += cc * cc;

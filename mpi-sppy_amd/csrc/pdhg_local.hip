@@ -70,14 +70,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 const int kk = col_nonant[j];
                 if (kk >= 0) {
                     const long t = sN + kk;
-                    if (a.w_on) cc += a.W[t];
-                    if (a.prox_on) {
-                        const double r = a.rho[t];
-                        const double xb = a.xbar[a.xidx[t]];
-                        cc -= r * xb;
-                        qq = r;
-                        prox_const += 0.5 * r * xb * xb;
-                    }
+                    ph_terms(a, t, cc, qq, prox_const);
                     if (a.fix_nonants) { lo_ = hi_ = a.fixed[t] / d; }
                 }
                 c2 += cc * cc;

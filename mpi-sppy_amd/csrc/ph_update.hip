@@ -122,7 +122,7 @@ __device__ __forceinline__ double block_sum_range(const double* v, int first, in
     return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// Update_W + convergence_diff (local half) + the solve-status summary.  One workgroup per
+// Update_W + Update_z (smoothed PH only) + convergence_diff (local half) + the solve-status summary.  One workgroup per
 // convergence segment (scenario range inside one virtual rank): xbar from the (all-reduced) node
 // sums, W += rho (x - xbar), sum |x - xbar|, and the number of scenarios whose last solve did not
 // reach the KKT tolerance / failed numerically.  The last workgroup reduces the segment partials
@@ -137,10 +137,12 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
     const long e0 = (long)s0 * a.N, e1 = (long)s1 * a.N;
     double acc = 0.0;
     for (long e = e0 + tid; e < e1; e += 256) {
+        const double xv = a.xN[e];
         const double xb = nodesum[a.xidx[e]];
-        const double d = a.xN[e] - xb;
+        const double d = xv - xb;
         a.W[e] += a.rho[e] * d;
         acc += fabs(d);
+        if (a.smooth_on) a.Z[e] += a.beta[e] * (xv - a.Z[e]);   // Update_z (smoothed PH)
     }
     int nb = 0, nn = 0;
     if (a.status)
@@ -199,7 +201,7 @@ __global__ void eval_obj_kernel(int S, int n, int N, const double* x, const doub
                                 const double* obj_off, const int* nonant_col, const double* xN,
                                 const double* W, const double* rho, const double* xbar,
                                 const int* xidx, int w_on, int prox_on, double sense,
-                                double* out) {
+                                const double* Z, const double* Psm, int smooth_on, double* out) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
     double f = 0.0;
@@ -212,6 +214,10 @@ __global__ void eval_obj_kernel(int S, int n, int N, const double* x, const doub
         if (prox_on) {
             const double xb = xbar[xidx[e]];
             t += 0.5 * rho[e] * (xv * xv - 2.0 * xb * xv + xb * xb);
+            if (smooth_on) {
+                const double z = Z[e];
+                t += 0.5 * Psm[e] * (xv * xv - 2.0 * z * xv + z * z);
+            }
         }
     }
     // c is min-form: model objective = sense * (c.x + off) ; PH terms enter with the model sense
@@ -231,9 +237,9 @@ hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convp
 hipError_t eval_obj_launch(int S, int n, int N, const double* x, const double* c, const double* obj_off,
                            const int* nonant_col, const double* xN, const double* W, const double* rho,
                            const double* xbar, const int* xidx, int w_on, int prox_on, double sense,
-                           double* out, hipStream_t st) {
+                           const double* Z, const double* Psm, int smooth_on, double* out, hipStream_t st) {
     hipLaunchKernelGGL(eval_obj_kernel, dim3((S + 127) / 128), dim3(128), 0, st, S, n, N, x, c, obj_off,
-                       nonant_col, xN, W, rho, xbar, xidx, w_on, prox_on, sense, out);
+                       nonant_col, xN, W, rho, xbar, xidx, w_on, prox_on, sense, Z, Psm, smooth_on, out);
     return hipGetLastError();
 }
 

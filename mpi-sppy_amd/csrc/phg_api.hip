@@ -36,7 +36,7 @@ hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convp
 hipError_t eval_obj_launch(int S, int n, int N, const double* x, const double* c, const double* obj_off,
                            const int* nonant_col, const double* xN, const double* W, const double* rho,
                            const double* xbar, const int* xidx, int w_on, int prox_on, double sense,
-                           double* out, hipStream_t st);
+                           const double* Z, const double* Psm, int smooth_on, double* out, hipStream_t st);
 }  // namespace phg
 
 using namespace phg;
@@ -76,6 +76,8 @@ struct phg_handle {
     double *vals = nullptr, *c = nullptr, *cl = nullptr, *cu = nullptr, *rl = nullptr, *ru = nullptr;
     double *dc = nullptr, *dr = nullptr, *eta = nullptr, *bnorm = nullptr, *obj_off = nullptr;
     double *W = nullptr, *rho = nullptr, *xbar = nullptr, *xsqbar = nullptr, *fixed = nullptr;
+    double *Z = nullptr, *Psm = nullptr, *beta = nullptr;   // smoothed PH
+    int smooth_on = 0;
     int* xidx = nullptr;
     double *xs = nullptr, *ys = nullptr, *omega = nullptr, *x_out = nullptr, *y_out = nullptr;
     double *xN = nullptr, *obj = nullptr, *bound = nullptr, *kkt = nullptr, *eval = nullptr;
@@ -174,6 +176,13 @@ int phg_set_stream(phg_handle* h, void* s) {
         h->own_stream = false;
     }
     h->stream = (hipStream_t)s;
+    return 0;
+}
+
+int phg_set_smoothing(phg_handle* h, int32_t on) {
+    if (!h || !h->loaded) return fail("phg_set_smoothing: no batch loaded");
+    h->smooth_on = on ? 1 : 0;
+    h->ph.smooth_on = h->smooth_on;
     return 0;
 }
 
@@ -793,6 +802,9 @@ int phg_load_batch(phg_handle* h, const phg_batch* b) {
     if (dalloc(h, &h->W, (size_t)S * N)) return -1;
     if (dalloc(h, &h->rho, (size_t)S * N)) return -1;
     if (dalloc(h, &h->fixed, (size_t)S * N)) return -1;
+    if (dalloc(h, &h->Z, (size_t)S * N)) return -1;
+    if (dalloc(h, &h->Psm, (size_t)S * N)) return -1;
+    if (dalloc(h, &h->beta, (size_t)S * N)) return -1;
     if (dalloc(h, &h->xbar, std::max(1, b->N_tot))) return -1;
     if (dalloc(h, &h->xsqbar, std::max(1, b->N_tot))) return -1;
     if (dalloc(h, &h->xs, (size_t)S * n)) return -1;
@@ -813,6 +825,8 @@ int phg_load_batch(phg_handle* h, const phg_batch* b) {
     if (dput(h, &h->nonant_col_d, b->nonant_col, N)) return -1;
     if (build_ph_tables(h, b)) return -1;
     h->ph.status = h->status;
+    h->ph.Z = h->Z;
+    h->ph.beta = h->beta;
     h->ph.xN = h->xN; h->ph.W = h->W; h->ph.rho = h->rho; h->ph.xbar = h->xbar; h->ph.xsqbar = h->xsqbar;
     // preconditioning
     PrepArgs pa{};
@@ -860,6 +874,9 @@ static double* field_ptr(phg_handle* h, int f, size_t* count) {
         case PHG_F_FIXED: *count = S * N; return h->fixed;
         case PHG_F_CONV_PART: *count = 2 * (size_t)h->P + 2; return h->convpart;
         case PHG_F_OMEGA: *count = S; return h->omega;
+        case PHG_F_Z: *count = S * N; return h->Z;
+        case PHG_F_SMOOTH_P: *count = S * N; return h->Psm;
+        case PHG_F_SMOOTH_BETA: *count = S * N; return h->beta;
         default: return nullptr;
     }
 }
@@ -907,6 +924,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.vals = h->vals; a.c = h->c; a.cl = h->cl; a.cu = h->cu; a.rl = h->rl; a.ru = h->ru;
     a.dc = h->dc; a.dr = h->dr; a.eta = h->eta; a.obj_off = h->obj_off; a.bnorm = h->bnorm;
     a.W = h->W; a.rho = h->rho; a.xbar = h->xbar; a.xidx = h->xidx; a.fixed = h->fixed;
+    a.Z = h->Z; a.Psm = h->Psm; a.smooth_on = h->smooth_on;
     a.xs = h->xs; a.ys = h->ys; a.omega = h->omega;
     a.x_out = h->x_out; a.y_out = h->y_out; a.xN = h->xN; a.obj = h->obj; a.bound = h->bound;
     a.kkt = h->kkt; a.iters = h->iters; a.status = h->status;
@@ -983,7 +1001,8 @@ int phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on) {
     if (!h || !h->loaded) return fail("phg_eval_objective: no batch loaded");
     CK(hipSetDevice(h->device));
     CK(eval_obj_launch(h->S, h->n, h->N, h->x_out, h->c, h->obj_off, h->nonant_col_d, h->xN, h->W,
-                       h->rho, h->xbar, h->xidx, w_on, prox_on, h->sense, h->eval, h->stream));
+                       h->rho, h->xbar, h->xidx, w_on, prox_on, h->sense, h->Z, h->Psm, h->smooth_on, h->eval,
+                       h->stream));
     CK(hipStreamSynchronize(h->stream));
     return 0;
 }

@@ -82,6 +82,9 @@ struct PdhgArgs {
     const double* xbar;     // [N_tot]
     const int*    xidx;     // [S*N]   xbar slot of (s,k)
     const double* fixed;    // [S*N]
+    const double* Z;        // [S*N]   smoothing centre z (smoothed PH, phbase.py:641-760)
+    const double* Psm;      // [S*N]   smoothing weight p
+    int smooth_on;
     // state (scaled), persists across solves for warm starts
     double* xs;             // [S*n]
     double* ys;             // [S*m]
@@ -151,7 +154,29 @@ struct PhArgs {
     int* csegbad;           // [2*n_cseg] scenarios not optimal / NaN in the last solve
     const int* vr_first;    // [P+1] conv segments of vrank v
     const int* status;      // [S] status of the last solve (may be null)
+    double* Z;              // [S*N] smoothing centre (Update_z, phbase.py:329-346), when smooth_on
+    const double* beta;     // [S*N]
+    int smooth_on;
     unsigned* ticket;       // [2] last-workgroup counters of the two kernels (zeroed)
 };
+
+// PH terms of nonant t = s*N + k in the min-form subproblem objective (phbase.py:670-760):
+//   c += w_on W;  prox_on: c -= rho xbar (+ p z), q = rho (+ p), const += rho/2 xbar^2 (+ p/2 z^2)
+__device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, double& cc, double& qq, double& pc) {
+    if (a.w_on) cc += a.W[t];
+    if (a.prox_on) {
+        const double r = a.rho[t];
+        const double xb = a.xbar[a.xidx[t]];
+        cc -= r * xb;
+        qq = r;
+        pc += 0.5 * r * xb * xb;
+        if (a.smooth_on) {
+            const double p = a.Psm[t], z = a.Z[t];
+            cc -= p * z;
+            qq += p;
+            pc += 0.5 * p * z * z;
+        }
+    }
+}
 
 }  // namespace phg

@@ -166,7 +166,7 @@ class Engine:
         return {_lib.F_X: S * n, _lib.F_Y: S * m, _lib.F_XN: S * N, _lib.F_W: S * N, _lib.F_RHO: S * N,
                 _lib.F_XBAR: self.N_tot, _lib.F_XSQBAR: self.N_tot, _lib.F_OBJ: S, _lib.F_BOUND: S,
                 _lib.F_EVAL: S, _lib.F_KKT: S, _lib.F_FIXED: S * N, _lib.F_CONV_PART: 2 * self.P + 2,
-                _lib.F_OMEGA: S}[field]
+                _lib.F_OMEGA: S, _lib.F_Z: S * N, _lib.F_SMOOTH_P: S * N, _lib.F_SMOOTH_BETA: S * N}[field]
 
     def get(self, field):
         out = np.empty(self._count(field))
@@ -208,6 +208,9 @@ class Engine:
         cp = None if self.exchange is None else self.exchange[1].data_ptr()
         _lib.check(self.lib.phg_conv_finish(self.h, cp, ctypes.byref(v)))
         return v.value
+
+    def set_smoothing(self, on):
+        _lib.check(self.lib.phg_set_smoothing(self.h, int(bool(on))))
 
     def solve_summary(self):
         """(scenarios not at the KKT tolerance, numerical failures) of the solve preceding the last

@@ -14,7 +14,7 @@ go through the communicator (RCCL).  Nothing of size S x n crosses PCIe inside t
 iteration reads back one convergence scalar (2 x virtual-rank doubles).
 
 Documented deviations: per-subproblem extension hooks ``pre_solve``/``post_solve`` cannot run
-inside a batched launch (``pre_solve_loop``/``post_solve_loop`` do); ``smoothed``,
+inside a batched launch (``pre_solve_loop``/``post_solve_loop`` do);
 ``linearize_proximal_terms``, bundles and ``variable_probability`` are not supported yet.
 """
 import math
@@ -75,7 +75,9 @@ class PHBase(SPBase):
         self.options.setdefault("smoothed", 0)
         self.options.setdefault("time_limit", None)
         if self.options["smoothed"]:
-            raise NotImplementedError("smoothed PH is not supported by the GPU engine yet")
+            for k in ("defaultPHp", "defaultPHbeta"):
+                if k not in self.options:
+                    raise ValueError(f"smoothed PH needs option {k}")
         if self.options.get("linearize_proximal_terms"):
             raise NotImplementedError("linearize_proximal_terms: the engine solves the exact prox QP")
         if self.options.get("bundles_per_rank", 0):
@@ -129,11 +131,18 @@ class PHBase(SPBase):
         self.prox_on = 0
 
     def PH_Prep(self, attach_duals=True, attach_prox=True, attach_smooth=0):
-        """``phbase.py:763-788``: W, rho, xbar live on the device; W_on = prox_on = 0."""
+        """``phbase.py:763-788``: W, rho, xbar (and the smoothing z, p, beta of
+        ``attach_smoothing``, ``phbase.py:641-655``) live on the device; W_on = prox_on = 0."""
         self.attach_Ws_and_prox()
         self._attach_duals = attach_duals
         self._attach_prox = attach_prox
+        self._attach_smooth = attach_smooth
         self._create_solvers()
+        if attach_smooth:
+            self.engine.set(_lib.F_Z, 0.0)
+            self.engine.set(_lib.F_SMOOTH_P, float(self.options["defaultPHp"]))
+            self.engine.set(_lib.F_SMOOTH_BETA, float(self.options["defaultPHbeta"]))
+            self.engine.set_smoothing(True)
 
     def _disable_prox(self):
         self.prox_on = 0
@@ -237,6 +246,11 @@ class PHBase(SPBase):
         """``phbase.py:301-326``: W += rho (x - xbar) (fused with the conv partials)."""
         self.engine.apply_xbar()
         self._xbar_pending = False
+
+    def Update_z(self, verbose=False):
+        """``phbase.py:329-346`` z += beta (x - z): fused into the Update_W kernel (same x, same
+        iteration) whenever smoothing is attached, so there is nothing left to launch here."""
+        return None
 
     def convergence_diff(self):
         """``phbase.py:349-371``: mean over (virtual) ranks of the per-rank mean |x - xbar|."""
@@ -350,6 +364,9 @@ class PHBase(SPBase):
             self.extobject.post_iter0_after_sync()
         if self.rho_setter is not None:
             self._use_rho_setter(verbose and self.cylinder_rank == 0)
+        if self.options["smoothed"] == 2 and getattr(self, "_attach_smooth", 0):
+            # "ratio" smoothing: p *= rho (phbase.py:918-922)
+            self.engine.set(_lib.F_SMOOTH_P, self.engine.get(_lib.F_SMOOTH_P) * self.engine.get(_lib.F_RHO))
         if self.ph_converger is not None:
             self.convobject = self.ph_converger(self)
         self.conv = None

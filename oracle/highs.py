@@ -125,7 +125,6 @@ def kkt_certify(c, qdiag, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, 
     c = np.asarray(c, float)
     n = c.shape[0]
     m = len(rowptr) - 1
-    A = np.zeros((m, n)) if m == 0 else None
     ax = np.zeros(m)
     aty = np.zeros(n)
     for i in range(m):
@@ -140,10 +139,11 @@ def kkt_certify(c, qdiag, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, 
     pr = max(np.maximum(np.asarray(col_lo) - x, x - np.asarray(col_hi)).max(initial=0.0) / xs,
              np.maximum(np.asarray(row_lo) - ax, ax - np.asarray(row_hi)).max(initial=0.0) / axs, 0.0)
     # complementarity: dual sign must match an active bound; measure |dual| * distance
-    dl = np.where(col_dual > 0, col_dual * (x - np.where(np.isfinite(col_lo), col_lo, -np.inf)), 0.0)
-    du = np.where(col_dual < 0, -col_dual * (np.where(np.isfinite(col_hi), col_hi, np.inf) - x), 0.0)
-    rl_ = np.where(row_dual > 0, row_dual * (ax - np.where(np.isfinite(row_lo), row_lo, -np.inf)), 0.0)
-    ru_ = np.where(row_dual < 0, -row_dual * (np.where(np.isfinite(row_hi), row_hi, np.inf) - ax), 0.0)
+    with np.errstate(invalid="ignore"):   # 0 * inf in the unselected branch of np.where
+        dl = np.where(col_dual > 0, col_dual * (x - np.where(np.isfinite(col_lo), col_lo, -np.inf)), 0.0)
+        du = np.where(col_dual < 0, -col_dual * (np.where(np.isfinite(col_hi), col_hi, np.inf) - x), 0.0)
+        rl_ = np.where(row_dual > 0, row_dual * (ax - np.where(np.isfinite(row_lo), row_lo, -np.inf)), 0.0)
+        ru_ = np.where(row_dual < 0, -row_dual * (np.where(np.isfinite(row_hi), row_hi, np.inf) - ax), 0.0)
     comp = max(np.abs(dl).max(initial=0), np.abs(du).max(initial=0), np.abs(rl_).max(initial=0),
                np.abs(ru_).max(initial=0)) / (sc * max(xs, axs))
     val = max(stat, pr, comp)

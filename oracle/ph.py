@@ -72,6 +72,11 @@ class OraclePH:
         rho0 = float(self.options["defaultPHrho"])
         self.rho = np.full((self.S, self.N), rho0)
         self.W = np.zeros((self.S, self.N))
+        # smoothed PH (phbase.py:641-655): z = 0, p = defaultPHp, beta = defaultPHbeta
+        self.smoothed = int(self.options.get("smoothed", 0))
+        self.z = np.zeros((self.S, self.N))
+        self.p = np.full((self.S, self.N), float(self.options.get("defaultPHp", 0.0)))
+        self.beta = np.full((self.S, self.N), float(self.options.get("defaultPHbeta", 0.0)))
         self.xbar = np.zeros((self.S, self.N))
         self.xsqbar = np.zeros((self.S, self.N))
         self.x = [None] * self.S
@@ -106,6 +111,11 @@ class OraclePH:
             q = np.zeros_like(c)
             np.add.at(q, cols, rho)
             off = float(np.sum(rho / 2.0 * xb * xb))
+            if self.smoothed:   # phbase.py:743-755: + p/2 (x^2 - 2 z x + z^2)
+                p_, z = self.p[k], self.z[k]
+                np.add.at(c, cols, -p_ * z)
+                np.add.at(q, cols, p_)
+                off += float(np.sum(p_ / 2.0 * z * z))
         t0 = time.perf_counter()
         r = highs.solve(c, a["rowptr"], a["colidx"], a["vals"], a["row_lo"], a["row_hi"],
                         a["col_lo"], a["col_hi"], qdiag=q, offset=off, threads=self.threads)
@@ -166,6 +176,12 @@ class OraclePH:
             xs = self.nonants(k)
             self.W[k] += self.rho[k] * (xs - self.xbar[k])
 
+    def Update_z(self):
+        """``phbase.py:329-346``: z += beta (x - z)."""
+        for k in range(self.S):
+            xs = self.nonants(k)
+            self.z[k] += self.beta[k] * (xs - self.z[k])
+
     def convergence_diff(self):
         """``phbase.py:349-371``."""
         tot = 0.0
@@ -205,6 +221,8 @@ class OraclePH:
             term += float(np.sum(self.W[k] * xs))
         if prox_on:
             term += float(np.sum(self.rho[k] / 2.0 * (xs * xs - 2.0 * self.xbar[k] * xs + self.xbar[k] ** 2)))
+            if self.smoothed:
+                term += float(np.sum(self.p[k] / 2.0 * (xs * xs - 2.0 * self.z[k] * xs + self.z[k] ** 2)))
         return f + sg * term
 
     def Eobjective(self, W_on=None, prox_on=None):
@@ -234,6 +252,8 @@ class OraclePH:
         feasP = self.feas_prob()
         if feasP != self.E1:
             raise RuntimeError(f"Infeasibility detected; E_feas={feasP}, E1={self.E1}")
+        if self.smoothed == 2:   # phbase.py:918-922
+            self.p = self.p * self.rho
         self.conv = None
         self.trivial_bound = self.Ebound()
         self.W_on = 1
@@ -248,6 +268,8 @@ class OraclePH:
         for self._PHIter in range(1, max_iterations + 1):
             self.Compute_Xbar()
             self.Update_W()
+            if self.smoothed:
+                self.Update_z()
             self.conv = self.convergence_diff()
             self.history.append(self.conv)
             if callback is not None:

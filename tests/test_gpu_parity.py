@@ -202,3 +202,19 @@ def test_hydro_ph_reference_answers():
     # inside the optimal face, simplex a vertex, so the PH trajectories legitimately differ (as they
     # do between CPLEX and Gurobi in the reference); only the reference's 2 s.f. answers are pinned
     assert abs(e0 - o.Eobjective(W_on=0, prox_on=0)) <= 1e-2 * abs(e0)
+
+
+@pytest.mark.parametrize("smoothed", [1, 2])
+def test_smoothed_ph_vs_oracle(smoothed):
+    """Smoothed PH (phbase.py:329-346, 641-760, 918-922): p/2 (x - z)^2 prox term, z += beta (x - z)."""
+    kw = dict(PHIterLimit=6, smoothed=smoothed, defaultPHp=0.5, defaultPHbeta=0.3)
+    ph = _farmer_ph(3, **kw)
+    conv, eobj, tb = ph.ph_main()
+    o = _farmer_oracle(3, **kw)
+    oconv, oeobj, otb = o.ph_main()
+    assert abs(tb - otb) <= 1e-6 * abs(otb)
+    np.testing.assert_allclose(ph.xbars(), o.xbar[0], rtol=1e-6)
+    np.testing.assert_allclose(ph.Ws(), o.W, atol=1e-5)
+    np.testing.assert_allclose(ph.engine.get(_lib.F_Z).reshape(3, -1), o.z, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(ph.conv_history, o.history, rtol=1e-5, atol=1e-8)
+    assert abs(eobj - oeobj) <= 1e-6 * abs(oeobj)
