@@ -68,6 +68,10 @@ typedef struct phg_batch {
     int32_t scen_global0;
     int32_t S_global;
     int32_t virt_nproc;
+    /* variable_probability (spbase.py:398-438): [S*N] per-nonant prob coefficients replacing
+     * prob_coeff in the node sums; W of a zero-probability nonant is kept at 0 (phbase.py:323-326).
+     * NULL when unused.                                                                      */
+    const double*  prob_coeff_var;
 } phg_batch;
 
 typedef struct phg_opts {

@@ -26,6 +26,7 @@ class PhgBatch(C.Structure):
         ("nonant_pos", i32p), ("level_len", i32p), ("scen_node", i32p), ("n_nodes", C.c_int32),
         ("node_off", i32p), ("N_tot", C.c_int32), ("prob", f64p), ("prob_coeff", f64p),
         ("scen_global0", C.c_int32), ("S_global", C.c_int32), ("virt_nproc", C.c_int32),
+        ("prob_coeff_var", f64p),
     ]
 
 

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
             const int kg = sg.kofs + k0 + k;
             for (int s = sg.s0 + so; s < sg.s1; s += q) {
                 const double xv = a.xN[(long)s * a.N + kg];
-                const double p = a.pc[(long)s * a.L + sg.level];
+                const double p = a.pcv ? a.pcv[(long)s * a.N + kg] : a.pc[(long)s * a.L + sg.level];
                 s1 += p * xv;
                 s2 += p * xv * xv;
             }
@@ -140,7 +140,8 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
         const double xv = a.xN[e];
         const double xb = nodesum[a.xidx[e]];
         const double d = xv - xb;
-        a.W[e] += a.rho[e] * d;
+        // variable probability: W of a zero-probability nonant stays 0 (prob0_mask)
+        a.W[e] = (a.pcv && a.pcv[e] == 0.0) ? 0.0 : a.W[e] + a.rho[e] * d;
         acc += fabs(d);
         if (a.smooth_on) a.Z[e] += a.beta[e] * (xv - a.Z[e]);   // Update_z (smoothed PH)
     }

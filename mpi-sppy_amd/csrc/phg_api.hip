@@ -551,6 +551,11 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     if (dput(h, &ip, level_kofs.data(), L)) return -1; a.level_kofs = ip;
     if (dput(h, &ip, b->nonant_level, N)) return -1; a.nonant_level = ip;
     if (dput(h, &dp, b->prob_coeff, (size_t)S * L)) return -1; a.pc = dp;
+    a.pcv = nullptr;
+    if (b->prob_coeff_var) {
+        if (dput(h, &dp, b->prob_coeff_var, (size_t)S * N)) return -1;
+        a.pcv = dp;
+    }
     if (dput(h, &ip, cv.data(), cv.size())) return -1; a.cseg_v = ip;
     if (dput(h, &ip, cs0.data(), cs0.size())) return -1; a.cseg_s0 = ip;
     if (dput(h, &ip, cs1.data(), cs1.size())) return -1; a.cseg_s1 = ip;

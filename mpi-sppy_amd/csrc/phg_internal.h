@@ -133,6 +133,7 @@ struct PhArgs {
     const double* rho;      // [S*N]
     const int* xidx;        // [S*N]
     const double* pc;       // [S*L]
+    const double* pcv;      // [S*N] per-nonant prob coefficients (variable probability) or null
     int L;
     const int* nonant_level;// [N]
     const NodeSeg* seg;     // [n_seg]

@@ -69,6 +69,9 @@ class BatchArrays:
         self.N_tot = tot
         self.scen_node = np.zeros((S, self.L), np.int32)
         self.prob_coeff = np.zeros((S, self.L))
+        # variable_probability (spbase.py:398-438): per-nonant coefficients, else None
+        varprob = any(getattr(md._mpisppy_data, "has_variable_probability", False) for md in models)
+        self.prob_coeff_var = np.zeros((S, self.N)) if varprob else None
         for s, md in enumerate(models):
             nl = md._mpisppy_node_list
             if len(nl) != self.L:
@@ -79,7 +82,14 @@ class BatchArrays:
                 if nd.name not in node_id:
                     raise RuntimeError(f"Tree node '{nd.name}' not in all_nodenames")
                 self.scen_node[s, l] = node_id[nd.name]
-                self.prob_coeff[s, l] = md._mpisppy_data.prob_coeff[nd.name]
+                pcn = md._mpisppy_data.prob_coeff[nd.name]
+                if isinstance(pcn, np.ndarray):
+                    self.prob_coeff[s, l] = np.nan      # per-variable: only prob_coeff_var is meaningful
+                    self.prob_coeff_var[s, self.nonant_level == l] = pcn
+                else:
+                    self.prob_coeff[s, l] = pcn
+                    if self.prob_coeff_var is not None:
+                        self.prob_coeff_var[s, self.nonant_level == l] = pcn
         self.prob = np.asarray(prob, np.float64)
         self.scen_global0, self.S_global, self.virt_nproc = scen_global0, S_global, virt_nproc
 
@@ -103,6 +113,7 @@ class BatchArrays:
         b.n_nodes, b.node_off, b.N_tot = len(self.all_nodenames), k(as_i32(self.node_off)), self.N_tot
         b.prob, b.prob_coeff = k(as_f64(self.prob)), k(as_f64(self.prob_coeff))
         b.scen_global0, b.S_global, b.virt_nproc = self.scen_global0, self.S_global, self.virt_nproc
+        b.prob_coeff_var = k(as_f64(self.prob_coeff_var)) if self.prob_coeff_var is not None else None
         return b, keep
 
 

@@ -49,9 +49,7 @@ class SPBase:
         self.cylinder_rank = self.mpicomm.Get_rank()
         self.global_rank = self.cylinder_rank
         self.E1_tolerance = E1_tolerance
-        if variable_probability is not None:
-            raise NotImplementedError("variable_probability is not supported by the GPU engine yet")
-        self.variable_probability = None
+        self.variable_probability = variable_probability
         self.bundling = False
         self._calculate_scenario_ranks()
         self._create_scenarios(scenario_creator_kwargs or {})
@@ -60,6 +58,7 @@ class SPBase:
         self._attach_nlens()
         self._attach_nonant_indices()
         self._verify_nonant_lengths()
+        self._use_variable_probability_setter()
         self._set_sense()
         self._spcomm = None
 
@@ -130,6 +129,55 @@ class SPBase:
         for nd in set().union(*[[n.name for n in s._mpisppy_node_list] for s in self.local_scenarios.values()]):
             if nd not in self.all_nodenames:
                 raise RuntimeError(f"Tree node '{nd}' not in all_nodenames list {self.all_nodenames}")
+
+    def _use_variable_probability_setter(self, verbose=False):
+        """``spbase.py:398-438``: variable_probability(scenario, **kw) -> [(vardata or id, prob)]
+        makes prob_coeff per nonant for the nodes it touches; prob0_mask zeroes W of
+        zero-probability variables (phbase.py:323-326)."""
+        if self.variable_probability is None:
+            for s in self.local_scenarios.values():
+                s._mpisppy_data.has_variable_probability = False
+            return
+        kw = self.options.get("variable_probability_kwargs", {}) or {}
+        for s in self.local_scenarios.values():
+            s._mpisppy_data.has_variable_probability = True
+            for v, prob in self.variable_probability(s, **kw):
+                vid = v if isinstance(v, int) else id(v)
+                ndn, i = s._mpisppy_data.varid_to_nonant_index[vid]
+                if not isinstance(s._mpisppy_data.prob_coeff[ndn], np.ndarray):
+                    nl = s._mpisppy_data.nlens[ndn]
+                    s._mpisppy_data.prob_coeff[ndn] = np.full(nl, s._mpisppy_data.prob_coeff[ndn], dtype="d")
+                    s._mpisppy_data.prob0_mask[ndn] = np.ones(nl, dtype="d")
+                s._mpisppy_data.prob_coeff[ndn][i] = prob
+                if prob == 0:
+                    s._mpisppy_data.prob0_mask[ndn][i] = 0.0
+        if not self.options.get("do_not_check_variable_probabilities", False):
+            self._check_variable_probabilities_sum(verbose)
+
+    def _check_variable_probabilities_sum(self, verbose=False):
+        """``spbase.py:459-500``: per node, the per-variable probabilities must sum to 1 over all
+        scenarios (SUM across ranks)."""
+        sums = {}
+        for s in self.local_scenarios.values():
+            for nd in s._mpisppy_node_list:
+                v = np.full(s._mpisppy_data.nlens[nd.name], 0.0) + s._mpisppy_data.prob_coeff[nd.name]
+                sums[nd.name] = sums.get(nd.name, 0.0) + v
+        for ndn in sorted(sums):
+            tot = np.asarray(self.mpicomm.allreduce_array(np.asarray(sums[ndn], dtype="d"))) \
+                if self.n_proc > 1 else sums[ndn]
+            if not np.allclose(tot, 1.0, atol=self.E1_tolerance):
+                bad = np.nonzero(~np.isclose(tot, 1.0, atol=self.E1_tolerance))[0]
+                raise RuntimeError(f"Node {ndn}, variables indexed {bad.tolist()} have unconditional "
+                                   f"probability sums {tot[bad].tolist()}")
+
+    def is_zero_prob(self, scenario_model, var):
+        """``spbase.py:442-457``."""
+        if self.variable_probability is None:
+            return False
+        d = scenario_model._mpisppy_data
+        ndn, i = d.varid_to_nonant_index[id(var)]
+        pc = d.prob_coeff[ndn]
+        return isinstance(pc, np.ndarray) and float(pc[i]) == 0.0
 
     def _set_sense(self):
         senses = {s.sense for s in self.local_scenarios.values()}

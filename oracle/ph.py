@@ -37,7 +37,7 @@ def rank_slices(S, n_proc):
 
 class OraclePH:
     def __init__(self, options, all_scenario_names, scenario_creator, scenario_creator_kwargs=None,
-                 n_proc=1, scenarios=None, threads=1):
+                 n_proc=1, scenarios=None, threads=1, variable_probability=None):
         self.options = dict(options)
         self.names = list(all_scenario_names)
         kw = scenario_creator_kwargs or {}
@@ -67,6 +67,16 @@ class OraclePH:
             self.keys.append(keys)
             self.prob_coeff.append(np.array(pc))
         self.N = len(self.keys[0])
+        # variable_probability (spbase.py:398-438): callable(OScen) -> [(column, prob)]
+        self.prob0_mask = np.ones((self.S, self.N))
+        self.has_varprob = variable_probability is not None
+        if variable_probability is not None:
+            for k, s in enumerate(self.scen):
+                pos = {col: i for i, col in enumerate(s.nonant_cols())}
+                for col, pr in variable_probability(s):
+                    self.prob_coeff[k][pos[col]] = pr
+                    if pr == 0:
+                        self.prob0_mask[k, pos[col]] = 0.0
         self.cols = np.array([s.nonant_cols() for s in self.scen], dtype=np.int64)
         self.arr = [s.arrays() for s in self.scen]
         rho0 = float(self.options["defaultPHrho"])
@@ -154,7 +164,7 @@ class OraclePH:
                     if ndn not in loc:
                         loc[ndn] = np.zeros(2 * nlen)
                     arr = xs[pos:pos + nlen]
-                    probs = self.prob_coeff[k][pos] * np.ones(nlen)
+                    probs = self.prob_coeff[k][pos:pos + nlen]
                     loc[ndn][:nlen] += probs * arr
                     loc[ndn][nlen:] += probs * arr ** 2
                     pos += nlen
@@ -175,6 +185,8 @@ class OraclePH:
         for k in range(self.S):
             xs = self.nonants(k)
             self.W[k] += self.rho[k] * (xs - self.xbar[k])
+            if self.has_varprob:
+                self.W[k] *= self.prob0_mask[k]
 
     def Update_z(self):
         """``phbase.py:329-346``: z += beta (x - z)."""

@@ -218,3 +218,39 @@ def test_smoothed_ph_vs_oracle(smoothed):
     np.testing.assert_allclose(ph.engine.get(_lib.F_Z).reshape(3, -1), o.z, rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(ph.conv_history, o.history, rtol=1e-5, atol=1e-8)
     assert abs(eobj - oeobj) <= 1e-6 * abs(oeobj)
+
+
+def test_variable_probability_vs_oracle():
+    """variable_probability (spbase.py:398-438, phbase.py:323-326): per-nonant probabilities in the
+    node averages, W of zero-probability nonants held at 0.  Scenario 2 gets probability 0 on the
+    first nonant (CORN0); scenarios 0 and 1 share it 1/2 each; everything else 1/3."""
+    def prob_for(k, i):
+        if i == 0:
+            return (0.5, 0.5, 0.0)[k]
+        return 1.0 / 3.0
+
+    def vp_prod(scen):
+        k = int(scen._scen_index)
+        return [(v, prob_for(k, i)) for i, v in enumerate(scen._mpisppy_node_list[0].nonant_vardata_list)]
+
+    def creator(name, **kw):
+        m = farmer.scenario_creator(name, **kw)
+        m._scen_index = int(name[4:])
+        return m
+
+    opts = _opts(PHIterLimit=6)
+    ph = PH(opts, farmer.scenario_names_creator(3), creator,
+            scenario_creator_kwargs={"crops_multiplier": 1, "num_scens": 3}, variable_probability=vp_prod)
+    conv, eobj, tb = ph.ph_main()
+
+    def vp_oracle(o):
+        k = int(o.name[4:])
+        return [(col, prob_for(k, i)) for i, col in enumerate(o.nonant_cols())]
+
+    o = oph.OraclePH(_opts(PHIterLimit=6), om.farmer_names(3), om.farmer, dict(crops_multiplier=1, num_scens=3),
+                     variable_probability=vp_oracle)
+    oconv, oeobj, otb = o.ph_main()
+    np.testing.assert_allclose(ph.xbars(), o.xbar[0], rtol=1e-6)
+    np.testing.assert_allclose(ph.Ws(), o.W, atol=1e-5)
+    assert ph.Ws()[2, 0] == 0.0
+    np.testing.assert_allclose(ph.conv_history, o.history, rtol=1e-5, atol=1e-8)
