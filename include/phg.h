@@ -175,6 +175,16 @@ int  phg_set_smoothing(phg_handle* h, int32_t on);
 int  phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on);
 
 
+/* Cylinders on one GPU (hub.py:462-616 send_ws / send_nonants, spoke.py; here device-to-device,
+ * ordered after src's queued work by an event, enqueued on dst's stream):
+ *   phg_copy_from : dst.field <- src.field (W for a Lagrangian spoke, phbase.py:397-413)
+ *   phg_fix_from  : dst.fixed[s, :] <- src.xN[scen, :] for all s (xhat candidate = scenario scen's
+ *                   nonants, xhatshufflelooper_bounder.py; two-stage batches)
+ *   phg_query     : *idle = 1 when everything queued on h's stream has finished (non-blocking)  */
+int  phg_copy_from(phg_handle* dst, phg_handle* src, int32_t field);
+int  phg_fix_from(phg_handle* dst, phg_handle* src, int32_t scen);
+int  phg_query(phg_handle* h, int32_t* idle);
+
 /* launch timing without per-launch synchronisation: phg_timing_reset clears the counters and
  * selects what gets HIP events (enable bit 0: solves, bit 1: PH updates; 0 = none, the
  * production default);

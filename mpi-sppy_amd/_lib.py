@@ -62,6 +62,9 @@ SIGNATURES = {
     "phg_ph_update": (C.c_int, [C.c_void_p, f64p]),
     "phg_solve_summary": (C.c_int, [C.c_void_p, i32p]),
     "phg_set_smoothing": (C.c_int, [C.c_void_p, C.c_int32]),
+    "phg_copy_from": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
+    "phg_fix_from": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
+    "phg_query": (C.c_int, [C.c_void_p, i32p]),
     "phg_eval_objective": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "phg_exchange_buffers": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "phg_timing_reset": (C.c_int, [C.c_void_p, C.c_int32]),

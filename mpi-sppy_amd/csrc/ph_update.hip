@@ -225,6 +225,18 @@ __global__ void eval_obj_kernel(int S, int n, int N, const double* x, const doub
     out[s] = sense * (f + obj_off[s]) + sense * t;
 }
 
+// out[s*N + k] = row[k] for every s (xhat candidate broadcast, phg_fix_from)
+__global__ void broadcast_row_kernel(const double* row, int N, int S, double* out) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < (long)S * N) out[e] = row[e % N];
+}
+
+hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hipStream_t st) {
+    const long tot = (long)S * N;
+    hipLaunchKernelGGL(broadcast_row_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, row, N, S, out);
+    return hipGetLastError();
+}
+
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
     hipLaunchKernelGGL(node_sums_kernel, dim3(a.n_seg), dim3(256), 0, st, a, nodesum);
     return hipGetLastError();

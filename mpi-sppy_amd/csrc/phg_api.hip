@@ -32,6 +32,7 @@ hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t piece_gather_launch(const double* vals, int nnz, const int* perm, int E, int S, double* out,
                                hipStream_t st);
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
+hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hipStream_t st);
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
 hipError_t eval_obj_launch(int S, int n, int N, const double* x, const double* c, const double* obj_off,
                            const int* nonant_col, const double* xN, const double* W, const double* rho,
@@ -177,6 +178,53 @@ int phg_set_stream(phg_handle* h, void* s) {
     }
     h->stream = (hipStream_t)s;
     return 0;
+}
+
+static double* field_ptr(phg_handle* h, int f, size_t* count);
+
+// ------------------------------------------------------------------------------ cylinders
+// Device-to-device hand-offs between handles on the same GPU (hub -> spoke), ordered across
+// their streams by an event: the copy on dst's stream waits for src's work so far.
+static int cross_stream_wait(phg_handle* dst, phg_handle* src) {
+    hipEvent_t e;
+    CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    CK(hipEventRecord(e, src->stream));
+    CK(hipStreamWaitEvent(dst->stream, e, 0));
+    CK(hipEventDestroy(e));
+    return 0;
+}
+
+int phg_copy_from(phg_handle* dst, phg_handle* src, int32_t field) {
+    if (!dst || !src || !dst->loaded || !src->loaded) return fail("phg_copy_from: handles not loaded");
+    if (dst->device != src->device) return fail("phg_copy_from: handles on different devices");
+    size_t nd = 0, ns = 0;
+    double* pd = field_ptr(dst, field, &nd);
+    double* ps = field_ptr(src, field, &ns);
+    if (!pd || !ps) return fail("phg_copy_from: unknown field");
+    if (nd != ns) return fail("phg_copy_from: field sizes differ (different batches)");
+    CK(hipSetDevice(dst->device));
+    if (cross_stream_wait(dst, src)) return -1;
+    CK(hipMemcpyAsync(pd, ps, nd * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
+    return 0;
+}
+
+int phg_fix_from(phg_handle* dst, phg_handle* src, int32_t scen) {
+    if (!dst || !src || !dst->loaded || !src->loaded) return fail("phg_fix_from: handles not loaded");
+    if (dst->L != 1 || src->N != dst->N) return fail("phg_fix_from: two-stage batches with equal nonant counts only");
+    if (scen < 0 || scen >= src->S) return fail("phg_fix_from: scenario index out of range");
+    CK(hipSetDevice(dst->device));
+    if (cross_stream_wait(dst, src)) return -1;
+    // fixed[s, :] = src.xN[scen, :] for every s (same device: read straight from src's buffer)
+    CK(broadcast_row_launch(src->xN + (size_t)scen * src->N, dst->N, dst->S, dst->fixed, dst->stream));
+    return 0;
+}
+
+int phg_query(phg_handle* h, int32_t* idle) {
+    if (!h) return fail("null handle");
+    const hipError_t e = hipStreamQuery(h->stream);
+    if (e == hipSuccess) { *idle = 1; return 0; }
+    if (e == hipErrorNotReady) { *idle = 0; return 0; }
+    return fail(std::string("phg_query: ") + hipGetErrorString(e));
 }
 
 int phg_set_smoothing(phg_handle* h, int32_t on) {

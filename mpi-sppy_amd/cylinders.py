@@ -1,0 +1,217 @@
+"""Bound spokes on the MI355X engine (restates ``mpisppy/cylinders/lagrangian_bounder.py:13-98``,
+``mpisppy/cylinders/xhatshufflelooper_bounder.py:14-240`` and the spoke side of
+``mpisppy/cylinders/spoke.py``).
+
+The reference runs every cylinder in its own MPI ranks and exchanges W / nonants / bounds through
+one-sided MPI windows.  Here a spoke is a second (third) ``libphg`` handle on the SAME GPU as the
+hub, holding the same scenario batch, with its own HIP stream:
+
+* the hub's ``sync`` (once per PH iteration, ``phbase.py:1037-1040``) hands W / nonants over
+  device-to-device (``phg_copy_from`` / ``phg_fix_from``: an event on the hub's stream orders the
+  copy behind the hub's queued work, nothing goes through the host);
+* the spoke's batched solve then runs on its own stream, overlapping the hub's next PDHG launch;
+* at the next ``sync`` the hub collects the bound only if the spoke's stream is idle
+  (``phg_query``), so the hub never waits on a spoke -- the asynchrony of the reference's wheel.
+
+Bounds are expectations ``sum_s p_s (.)`` (``spopt.py:344-422``), ``math.fsum`` per rank and a SUM
+across ranks (the collect / skip decision is made collectively so every rank takes part).
+"""
+import math
+import random
+
+import numpy as np
+
+from . import _lib
+from .engine import Engine
+
+
+class _BoundSpoke:
+    converger_spoke_char = "?"
+    bound_kind = None            # "outer" or "inner"
+
+    def __init__(self, hub_opt, options=None):
+        self.hub_opt = hub_opt
+        self.options = dict(options or {})
+        he = hub_opt.engine
+        if he is None:
+            raise RuntimeError("the hub's engine must exist before its spokes (call PH_Prep first)")
+        dev = int(hub_opt.options.get("device", 0))
+        try:
+            import torch
+            if torch.cuda.is_available():
+                dev = torch.cuda.current_device()
+        except ImportError:
+            pass
+        # same batch (host arrays), same layout; the spoke's handle creates its own stream
+        self.engine = Engine(he.batch, device=dev, stream=None, exchange=None,
+                             layout=hub_opt.options.get("pdhg_layout", "auto"))
+        self.engine.set(_lib.F_RHO, he.get(_lib.F_RHO))
+        self.pending = False
+        self.bound = None
+        self.launches = 0
+        self.collected = 0
+
+    # ------------------------------------------------------------------ collective helpers
+    def _all_idle(self):
+        idle = self.engine.idle()
+        if self.hub_opt.n_proc > 1:
+            return self.hub_opt.mpicomm.allreduce_scalar(0.0 if idle else 1.0) == 0.0
+        return idle
+
+    def _rank_fsum(self, vals):
+        return self.hub_opt._rank_fsum(vals)
+
+    def _solve_opts(self):
+        o = self.hub_opt._solver_opts()
+        o.update({k: v for k, v in self.options.items() if k.startswith("pdhg_")})
+        return o
+
+    # ------------------------------------------------------------------ protocol
+    def update(self, block=False):
+        """Called from the hub's sync: collect the finished bound (or None), launch the next solve."""
+        b = None
+        if self.pending:
+            if not block and not self._all_idle():
+                return None          # still solving: the hub goes on without waiting
+            self.engine.sync()
+            b = self._collect()
+            self.pending = False
+            self.collected += 1
+            if b is not None:
+                self.bound = b if self.bound is None else self._better(b, self.bound)
+        if self._launch():
+            self.pending = True
+            self.launches += 1
+        return b
+
+    def finalize(self):
+        """Wait for the spoke's last solve and return its best bound."""
+        if self.pending:
+            self.engine.sync()
+            b = self._collect()
+            self.pending = False
+            if b is not None:
+                self.bound = b if self.bound is None else self._better(b, self.bound)
+        return self.bound
+
+    def _better(self, new, old):
+        mini = self.hub_opt.is_minimizing
+        if self.bound_kind == "outer":
+            return max(new, old) if mini else min(new, old)
+        return min(new, old) if mini else max(new, old)
+
+    def close(self):
+        self.engine.close()
+
+
+class LagrangianOuterBound(_BoundSpoke):
+    """``lagrangian_bounder.py``: solve every scenario with the hub's W, prox off; the outer bound
+    is sum_s p_s (dual bound_s) -- the PDHG dual objective, a valid Lagrangian bound."""
+    converger_spoke_char = "L"
+    bound_kind = "outer"
+
+    def _launch(self):
+        self.engine.copy_from(self.hub_opt.engine, _lib.F_W)
+        o = self._solve_opts()
+        self.engine.solve(1, 0, eps=o["pdhg_eps"], max_iter=o["pdhg_max_iter"],
+                          check_every=o["pdhg_check_every"], warm_start=1 if self.launches else 0,
+                          schedule=o["pdhg_schedule"])
+        return True
+
+    def _collect(self):
+        st = self.engine.get_i32(_lib.I_STATUS)
+        ok = float((st == 2).sum() == 0)
+        if self.hub_opt.n_proc > 1:
+            ok = float(self.hub_opt.mpicomm.allreduce_scalar(1.0 - ok) == 0.0)
+        if not ok:
+            return None
+        b = self.engine.get(_lib.F_BOUND)
+        p = self.engine.batch.prob
+        return self._rank_fsum([p[k] * b[k] for k in range(len(b))])
+
+
+class XhatShuffleInnerBound(_BoundSpoke):
+    """``xhatshufflelooper_bounder.py``: cycle through the scenarios in a seeded shuffle
+    (``random.Random(42).sample``); each try fixes every scenario's nonants to the candidate
+    scenario's current hub nonants (two-stage) and solves all scenarios; if all are solved the
+    inner bound is sum_s p_s obj_s (W and prox off, ``xhat_eval.py:102-170``)."""
+    converger_spoke_char = "X"
+    bound_kind = "inner"
+
+    def __init__(self, hub_opt, options=None):
+        super().__init__(hub_opt, options)
+        if self.engine.batch.L != 1:
+            raise NotImplementedError("XhatShuffleInnerBound on the GPU engine supports two-stage problems")
+        rs = random.Random()
+        rs.seed(42)
+        names = list(enumerate(hub_opt.all_scenario_names))
+        self.order = [k for k, _ in rs.sample(names, len(names))]
+        self.pos = 0
+        self.current = None
+        self.best_candidate = None
+        # an infeasible fixing would run PDHG to its cap: tries use a smaller one
+        self.max_iter = int(self.options.get("xhat_max_iter", 20000))
+
+    def _candidate_row(self, gidx):
+        """Nonants of global scenario gidx from the hub (host vector; summed over ranks)."""
+        ho = self.hub_opt
+        loc = gidx - ho.scen_global0
+        N = ho.engine.N
+        row = np.zeros(N)
+        if 0 <= loc < ho.engine.S:
+            row = ho.engine.get(_lib.F_XN).reshape(ho.engine.S, N)[loc].copy()
+        if ho.n_proc > 1:
+            row = np.asarray(ho.mpicomm.allreduce_array(row))
+        return row
+
+    def _launch(self):
+        gidx = self.order[self.pos % len(self.order)]
+        self.pos += 1
+        ho = self.hub_opt
+        loc = gidx - ho.scen_global0
+        if ho.n_proc == 1:
+            self.engine.fix_from(ho.engine, loc)
+        else:
+            self.engine.set(_lib.F_FIXED, np.tile(self._candidate_row(gidx), self.engine.S))
+        self.current = gidx
+        o = self._solve_opts()
+        self.engine.solve(0, 0, eps=o["pdhg_eps"], max_iter=min(self.max_iter, o["pdhg_max_iter"]),
+                          check_every=o["pdhg_check_every"], warm_start=1 if self.launches else 0,
+                          fix_nonants=True, schedule=o["pdhg_schedule"])
+        return True
+
+    def _collect(self):
+        st = self.engine.get_i32(_lib.I_STATUS)
+        bad = float((st != 0).sum())
+        if self.hub_opt.n_proc > 1:
+            bad = self.hub_opt.mpicomm.allreduce_scalar(bad)
+        if bad:
+            return None              # infeasible (or not solved to tolerance): no bound
+        obj = self.engine.get(_lib.F_OBJ)
+        p = self.engine.batch.prob
+        val = self._rank_fsum([p[k] * obj[k] for k in range(len(obj))])
+        if self.bound is None or self._better(val, self.bound) == val:
+            self.best_candidate = self.current
+        return val
+
+
+def spoke_from_dict(hub_opt, spoke_dict):
+    """Build a spoke from a reference-shaped spoke dict (``spin_the_wheel.py``):
+    {"spoke_class": cls, "opt_kwargs": {"options": {...}}, "spoke_kwargs": {...}}."""
+    cls = spoke_dict["spoke_class"]
+    opts = dict((spoke_dict.get("opt_kwargs") or {}).get("options", {}) or {})
+    opts.update((spoke_dict.get("spoke_kwargs") or {}).get("options", {}) or {})
+    return cls(hub_opt, options=opts)
+
+
+def gaps(hub):
+    """``hub.py:82-103``: absolute and relative gap between the best inner and outer bounds."""
+    if hub.opt.is_minimizing:
+        abs_gap = hub.BestInnerBound - hub.BestOuterBound
+    else:
+        abs_gap = hub.BestOuterBound - hub.BestInnerBound
+    if math.isfinite(abs_gap) and hub.BestOuterBound != 0 and math.isfinite(hub.BestOuterBound):
+        rel_gap = abs_gap / abs(hub.BestOuterBound)
+    else:
+        rel_gap = float("inf")
+    return abs_gap, rel_gap

@@ -220,6 +220,19 @@ class Engine:
         _lib.check(self.lib.phg_conv_finish(self.h, cp, ctypes.byref(v)))
         return v.value
 
+    def copy_from(self, src, field):
+        """Device-to-device copy of ``field`` from another handle on the same GPU (stream-ordered)."""
+        _lib.check(self.lib.phg_copy_from(self.h, src.h, int(field)))
+
+    def fix_from(self, src, scen):
+        """Fix every scenario's nonants to ``src``'s scenario ``scen`` nonants (two-stage xhat)."""
+        _lib.check(self.lib.phg_fix_from(self.h, src.h, int(scen)))
+
+    def idle(self):
+        out = np.zeros(1, np.int32)
+        _lib.check(self.lib.phg_query(self.h, ptr(out)))
+        return bool(out[0])
+
     def set_smoothing(self, on):
         _lib.check(self.lib.phg_set_smoothing(self.h, int(bool(on))))
 

@@ -310,6 +310,29 @@ class OraclePH:
         self.x, self.obj, self.outer = savex, saveobj, saveouter
         return b
 
+    def xhat_eval(self, xhat):
+        """Inner bound of a two-stage candidate (``xhat_eval.py:102-170``, ``xhatbase.py:42-235``):
+        fix every scenario's nonants to ``xhat``, solve with W and prox off; sum_s p_s obj_s if every
+        scenario is feasible, else None."""
+        vals = []
+        for k in range(self.S):
+            a = self.arr[k]
+            lo, hi = a["col_lo"].copy(), a["col_hi"].copy()
+            lo[self.cols[k]] = xhat
+            hi[self.cols[k]] = xhat
+            sg = 1.0 if self.scen[k].sense == 1 else -1.0
+            # feasibility tolerance 1e-6: a candidate from a first-order solve (PDHG, eps 1e-9 relative)
+            # meets first-stage rows to ~1e-9 relative (5e-7 on the farmer acreage row), not 1e-10 absolute
+            r = highs.solve(sg * a["c"], a["rowptr"], a["colidx"], a["vals"], a["row_lo"], a["row_hi"], lo, hi,
+                            tol=1e-6)
+            if not r.ok:
+                return None
+            vals.append(self.prob[k] * sg * r.obj)
+        out = 0.0
+        for sl in self.slices:
+            out += math.fsum(vals[k] for k in sl)
+        return out
+
 
 def ef_solve(scenarios, probs=None):
     """Extensive form (``mpisppy/utils/sputils.py:143-357`` create_EF): block-diagonal scenario

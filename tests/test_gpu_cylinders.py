@@ -1,0 +1,81 @@
+"""GPU bound spokes (cylinders.py) against the CPU oracle and the reference's pinned answers.
+
+* Lagrangian outer bound with the hub's W (lagrangian_bounder.py): the reference pins
+  -109499.5160897 (test_with_cylinders.py:153, places=1) for farmer 3 scenarios after 5 PH
+  iterations; the oracle's lagrangian_bound(W) with the same W agrees to 1e-6 relative.
+* Xhat inner bound (xhatshufflelooper_bounder.py, xhat_eval.py): a candidate scenario's nonants
+  fixed in every scenario; compared with the oracle's xhat_eval of the same candidate.
+* Wheel: hub + both spokes on one GPU terminate on rel_gap with outer <= EF optimum <= inner.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from mpisppy_amd import _lib  # noqa: E402
+from mpisppy_amd.cylinders import LagrangianOuterBound, XhatShuffleInnerBound  # noqa: E402
+from mpisppy_amd.examples import farmer  # noqa: E402
+from mpisppy_amd.hub import PHHub, WheelSpinner  # noqa: E402
+from mpisppy_amd.ph import PH  # noqa: E402
+from oracle import models as om  # noqa: E402
+from oracle import ph as oph  # noqa: E402
+
+
+def _opts(**kw):
+    o = {"solver_name": "phg", "PHIterLimit": 5, "defaultPHrho": 1.0, "convthresh": 1e-10,
+         "verbose": False, "display_progress": False}
+    o.update(kw)
+    return o
+
+
+def _ph(S=3, cm=1, **kw):
+    return PH(_opts(**kw), farmer.scenario_names_creator(S), farmer.scenario_creator,
+              scenario_creator_kwargs={"crops_multiplier": cm, "num_scens": S})
+
+
+def test_lagrangian_spoke_reference_value():
+    ph = _ph()
+    ph.ph_main(finalize=False)
+    sp = LagrangianOuterBound(ph)
+    sp.update()
+    b = sp.finalize()
+    assert abs(b - (-109499.5160897)) < 0.05, b
+    o = oph.OraclePH(_opts(), om.farmer_names(3), om.farmer, dict(crops_multiplier=1, num_scens=3))
+    ob = o.lagrangian_bound(ph.Ws())
+    assert abs(b - ob) <= 1e-6 * abs(ob), (b, ob)
+    sp.close()
+
+
+@pytest.mark.parametrize("S,cm", [(3, 1), (12, 2)])
+def test_xhat_spoke_vs_oracle(S, cm):
+    ph = _ph(S, cm)
+    ph.ph_main(finalize=False)
+    sp = XhatShuffleInnerBound(ph)
+    sp.update()
+    b = sp.finalize()
+    cand = sp.current
+    xhat = ph.nonants()[cand]
+    o = oph.OraclePH(_opts(), om.farmer_names(S), om.farmer, dict(crops_multiplier=cm, num_scens=S))
+    ob = o.xhat_eval(xhat)
+    assert ob is not None and b is not None
+    assert abs(b - ob) <= 1e-6 * abs(ob), (b, ob)
+    sp.close()
+
+
+def test_wheel_hub_and_spokes_gap():
+    S = 3
+    hub_dict = {"hub_class": PHHub, "hub_kwargs": {"options": {"rel_gap": 0.01}}, "opt_class": PH,
+                "opt_kwargs": {"options": _opts(PHIterLimit=200), "all_scenario_names": farmer.scenario_names_creator(S),
+                               "scenario_creator": farmer.scenario_creator,
+                               "scenario_creator_kwargs": {"crops_multiplier": 1, "num_scens": S}}}
+    spokes = [{"spoke_class": LagrangianOuterBound}, {"spoke_class": XhatShuffleInnerBound}]
+    wheel = WheelSpinner(hub_dict, spokes).spin()
+    ob, ib = wheel.BestOuterBound, wheel.BestInnerBound
+    ef = -108390.0                      # farmer EF optimum (doc/src/examples.rst:382)
+    assert ob <= ef + 1e-3 and ib >= ef - 1e-3, (ob, ib)
+    assert (ib - ob) / abs(ob) <= 0.01 + 1e-9, (ob, ib)
+    assert wheel.spcomm.opt._PHIter < 200
