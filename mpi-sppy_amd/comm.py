@@ -36,6 +36,9 @@ class SingleComm:
     def bcast_object(self, obj, root=0):
         return obj
 
+    def gather_object(self, obj, root=0):
+        return [obj]
+
 
 class TorchComm:
     """SUM all-reduces over an initialised ``torch.distributed`` process group."""
@@ -83,3 +86,10 @@ class TorchComm:
         lst = [obj]
         self.dist.broadcast_object_list(lst, src=root, group=self.group)
         return lst[0]
+
+    def gather_object(self, obj, root=0):
+        """Pickled objects of every rank, in rank order, on ``root`` (None elsewhere): the
+        ``comm.gather`` of the reference's file writers (control data only, never the data path)."""
+        out = [None] * self.size
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out if self.rank == root else None

@@ -149,6 +149,7 @@ class XhatShuffleInnerBound(_BoundSpoke):
         self.pos = 0
         self.current = None
         self.best_candidate = None
+        self.best_X = None           # local scenarios x n: the incumbent's full solution
         # an infeasible fixing would run PDHG to its cap: tries use a smaller one
         self.max_iter = int(self.options.get("xhat_max_iter", 20000))
 
@@ -191,7 +192,9 @@ class XhatShuffleInnerBound(_BoundSpoke):
         p = self.engine.batch.prob
         val = self._rank_fsum([p[k] * obj[k] for k in range(len(obj))])
         if self.bound is None or self._better(val, self.bound) == val:
+            # spoke.py:335-367 (update_if_improving / _cache_best_solution): keep the incumbent
             self.best_candidate = self.current
+            self.best_X = self.engine.get(_lib.F_X).reshape(self.engine.S, -1)
         return val
 
 

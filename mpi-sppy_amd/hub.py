@@ -11,8 +11,10 @@ device-to-device from then on (see ``cylinders.py``).  Termination on the inter-
 ``hub.py:130-166``.
 """
 import math
+import os
 
-from . import cylinders
+from . import _lib, cylinders
+from .utils import sputils
 
 
 class PHHub:
@@ -149,3 +151,68 @@ class WheelSpinner:
         for sp in hub.spokes:
             sp.close()
         return self
+
+    # ------------------------------------------------------------------ solutions (spin_the_wheel.py:166-213)
+    def _incumbent_spoke(self):
+        """The inner-bound spoke holding the best incumbent (``_determine_innerbound_winner``)."""
+        best = None
+        for sp in self.spcomm.spokes:
+            if sp.bound_kind == "inner" and getattr(sp, "best_X", None) is not None:
+                if best is None or sp._better(sp.bound, best.bound) == sp.bound:
+                    best = sp
+        return best
+
+    def _with_incumbent(self, fn):
+        opt = self.spcomm.opt
+        sp = self._incumbent_spoke()
+        if sp is None:
+            if opt.cylinder_rank == 0:
+                print("No incumbent solution available to write!")
+            return False
+        saved = {}
+        for k, (sname, s) in enumerate(opt.local_scenarios.items()):
+            saved[sname] = s._solution
+            s._solution = sp.best_X[k]
+        try:
+            fn(opt)
+        finally:
+            for sname, s in opt.local_scenarios.items():
+                s._solution = saved[sname]
+        return True
+
+    def write_first_stage_solution(self, solution_file_name,
+                                   first_stage_solution_writer=sputils.first_stage_nonant_writer):
+        """Writes the incumbent's ROOT nonants (``spbase.py:639-655``) on rank 0."""
+        def w(opt):
+            if opt.cylinder_rank == 0:
+                d = os.path.dirname(solution_file_name)
+                if d:
+                    os.makedirs(d, exist_ok=True)
+                s = opt.local_scenarios[opt.local_scenario_names[0]]
+                first_stage_solution_writer(solution_file_name, s, False)
+        return self._with_incumbent(w)
+
+    def write_tree_solution(self, solution_directory_name,
+                            scenario_tree_solution_writer=sputils.scenario_tree_solution_writer):
+        """One file per scenario with the incumbent's full solution (``spbase.py:657-675``)."""
+        def w(opt):
+            if opt.cylinder_rank == 0:
+                os.makedirs(solution_directory_name, exist_ok=True)
+            opt.mpicomm.Barrier()
+            for sname, s in opt.local_scenarios.items():
+                scenario_tree_solution_writer(solution_directory_name, sname, s, False)
+        return self._with_incumbent(w)
+
+    def local_nonant_cache(self):
+        """{node name: nonant values} of the hub's local scenarios (``spin_the_wheel.py:197-209``)."""
+        opt = self.spcomm.opt
+        xn = opt.engine.get(_lib.F_XN).reshape(opt.engine.S, -1)
+        out = {}
+        for k, s in enumerate(opt.local_scenarios.values()):
+            pos = 0
+            for nd in s._mpisppy_node_list:
+                ln = len(nd.nonant_vardata_list)
+                if nd.name not in out:
+                    out[nd.name] = list(xn[k, pos:pos + ln])
+                pos += ln
+        return out

@@ -86,6 +86,7 @@ class LinearModel:
         self._hi = []
         self._cost = []
         self._rows = []          # (dict col->coef, lo, hi, name)
+        self._blocks = []        # VarBlocks in creation order
         self.sense = minimize
         self.obj_offset = 0.0
         self._solution = None    # filled by the engine after a solve (x of this scenario)
@@ -105,6 +106,7 @@ class LinearModel:
             self._lo[vd.col] = -INF if lo is None else float(lo)
             self._hi[vd.col] = INF if hi is None else float(hi)
         setattr(self, name, blk)
+        self._blocks.append(blk)
         return blk
 
     def add_row(self, coefs, lo=-INF, hi=INF, name=""):
