@@ -169,7 +169,10 @@ def main():
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("pdhg_bytes_per_launch")
+            tj = json.load(open(args.traffic_json))
+            # PMC bytes only count for the kernel (layout) they were measured on
+            if tj.get("layout") == eng.layout and args.case == "farmer":
+                traffic = tj.get("pdhg_bytes_per_launch")
         except Exception:
             traffic = None
     # fused xbar/W/conv kernels: algorithmic bytes: 8 S N (x read, W read+write,
@@ -204,7 +207,7 @@ def main():
                      {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "bytes_per_pdhg_iter_per_scen": bytes_it,
                       "nnz_distinct": nnz_distinct, "tflops_fp64": round(achieved_tf, 4)}) | {
-                     "traffic": traffic if args.case == "farmer" else None,
+                     "traffic": traffic,
                      "kernel": {"local": "pdhg_local_kernel (lane-local, fp64 VALU; fp64 vector peak == matrix peak)",
                                 "gather": "pdhg_kernel (wave LDS-gather, fp64 VALU)",
                                 "block": "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)"}[eng.layout],

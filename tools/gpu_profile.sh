@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
-B="python3 bench.py --steps ${STEPS:-10} --warmup 3 --conv-iters 0 --cpu-seconds 0 ${BENCH_ARGS:-}"
+B="python3 bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-5} --conv-iters 0 --cpu-seconds 0 ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- $B > gpurun_out/prof/trace.log 2>&1
 rc=$?; echo "trace exit $rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/prof/trace.log; exit $rc; }
 if [ -n "${PMC:-}" ]; then
