@@ -1,0 +1,96 @@
+"""Parity at the bench's full sizes (BASELINE.json configs): farmer cm=10 x 10 000 scenarios
+(local kernel), sslp_15_45_10 x 2 048 and netdes x 1 024 (block kernel).
+
+The whole batch is too large for the oracle, so the checks are
+* size-independent properties of every scenario: status 0 (relative KKT <= eps), primal objective
+  = dual bound (each subproblem's own optimality certificate), x̄ = the probability-weighted mean
+  of the nonants (recomputed on the host from the device nonants), sum_s p_s W_s = 0 (the W update
+  keeps W dual feasible, ``wxbarutils._check_W``'s test), W_new - W_old = rho (x - x̄);
+* a seeded random sample of scenarios re-solved by the oracle with the SAME W / x̄ the device
+  used: nonants and objectives within the north_star tolerances (1e-6 relative; x 1e-5).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from mpisppy_amd import _lib  # noqa: E402
+from mpisppy_amd.examples import farmer, netdes, sslp  # noqa: E402
+from mpisppy_amd.ph import PH  # noqa: E402
+from oracle import models as om  # noqa: E402
+from oracle import ph as oph  # noqa: E402
+
+EPS = 1e-9
+
+CASES = {
+    "farmer": (10000, lambda S: farmer.scenario_names_creator(S), farmer.scenario_creator,
+               lambda S: {"crops_multiplier": 10, "num_scens": S},
+               lambda nm, S: om.farmer(nm, crops_multiplier=10, num_scens=S), 8, "local"),
+    "sslp": (2048, lambda S: sslp.scenario_names_creator(S), sslp.scenario_creator, lambda S: {},
+             lambda nm, S: om.sslp(nm), 3, "block"),
+    "netdes": (1024, lambda S: netdes.scenario_names_creator(S), netdes.scenario_creator,
+               lambda S: {"num_scens": S}, lambda nm, S: om.netdes(nm, num_scens=S), 2, "block"),
+}
+
+
+def _opts(**kw):
+    o = {"solver_name": "phg", "PHIterLimit": 3, "defaultPHrho": 1.0, "convthresh": 1e-10,
+         "verbose": False, "display_progress": False,
+         "iterk_solver_options": {"pdhg_eps": EPS}, "iter0_solver_options": {"pdhg_eps": EPS}}
+    o.update(kw)
+    return o
+
+
+def _certificates(ph):
+    st = ph.engine.get_i32(_lib.I_STATUS)
+    assert (st == 0).all(), np.bincount(st + 1)
+    obj, bnd = ph.engine.get(_lib.F_OBJ), ph.engine.get(_lib.F_BOUND)
+    gap = np.abs(obj - bnd) / (1.0 + np.abs(obj))
+    assert gap.max() <= 1e-6, gap.max()
+
+
+@pytest.mark.parametrize("case", ["farmer", "sslp", "netdes"])
+def test_full_size_properties_and_sampled_parity(case):
+    S, pn, pc, pkw, ob, nsamp, layout = CASES[case]
+    names = pn(S)
+    ph = PH(_opts(), names, pc, scenario_creator_kwargs=pkw(S))
+    ph.PH_Prep()
+    assert ph.engine.layout == layout
+    ph.Iter0()
+    _certificates(ph)
+    p = ph.engine.batch.prob
+
+    # one PH update: x̄ and W against host arithmetic on the device nonants
+    x = ph.nonants().copy()
+    W0 = ph.Ws().copy()
+    ph.Compute_Xbar()
+    ph.Update_W()
+    xbar = ph.xbars()
+    xb_host = (p[:, None] * x).sum(0)            # prob_coeff = p_s (two-stage), phbase.py:32-112
+    np.testing.assert_allclose(xbar, xb_host, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(xb_host).max()))
+    W = ph.Ws().copy()
+    np.testing.assert_allclose(W - W0, 1.0 * (x - xbar[None, :]), rtol=1e-12,
+                               atol=1e-12 * max(1.0, np.abs(x).max()))
+    assert np.abs((p[:, None] * W).sum(0)).max() <= 1e-9 * max(1.0, np.abs(W).max())
+
+    # the prox-QP solve with this W / x̄; a seeded sample re-solved by the oracle
+    ph.solve_loop()
+    _certificates(ph)
+    rng = np.random.default_rng(1134)
+    sample = sorted(rng.choice(S, size=nsamp, replace=False).tolist())
+    o = oph.OraclePH(_opts(), [names[k] for k in sample], None,
+                     scenarios=[ob(names[k], S) for k in sample])
+    o.W = W[sample].copy()
+    o.xbar = np.tile(xbar, (len(sample), 1))
+    o.W_on, o.prox_on = 1, 1
+    xg = ph.nonants()[sample]
+    og = ph.engine.get(_lib.F_OBJ)[sample]
+    for i in range(len(sample)):
+        o.solve_one(i)
+        xo = o.nonants(i)
+        np.testing.assert_allclose(xg[i], xo, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(xo).max()))
+        assert abs(og[i] - o.obj[i]) <= 1e-6 * max(1.0, abs(o.obj[i])), (sample[i], og[i], o.obj[i])
