@@ -139,6 +139,12 @@ int  phg_set_layout(phg_handle* h, int32_t policy);
  * lanes used, 0}                                                                               */
 int  phg_plan(const phg_batch* b, int32_t* out8);
 
+/* singleton-row presolve, on by default (call before phg_load_batch): rows with one nonzero on a
+ * non-nonant column become bounds on that column (same LP; PDHG handles bounds exactly).  phg_get /
+ * phg_set of PHG_F_Y keep the caller's row numbering; folded rows read back 0.
+ * phg_presolve_info: out2 = {rows folded, rows kept}                                          */
+int  phg_set_presolve(phg_handle* h, int32_t on);
+int  phg_presolve_info(phg_handle* h, int32_t* out2);
 int  phg_load_batch(phg_handle* h, const phg_batch* b);
 int  phg_set(phg_handle* h, int32_t field, const double* host_in);
 int  phg_get(phg_handle* h, int32_t field, double* host_out);

@@ -47,6 +47,8 @@ SIGNATURES = {
     "phg_destroy": (None, [C.c_void_p]),
     "phg_last_error": (C.c_char_p, []),
     "phg_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "phg_set_presolve": (C.c_int, [C.c_void_p, C.c_int32]),
+    "phg_presolve_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "phg_sync": (C.c_int, [C.c_void_p]),
     "phg_set_layout": (C.c_int, [C.c_void_p, C.c_int32]),
     "phg_plan": (C.c_int, [C.POINTER(PhgBatch), i32p]),

@@ -519,10 +519,13 @@ struct LocalVariant {
 #define PHG_L(a_, b_, c_, d_) {a_, b_, c_, d_, pdhg_local_kernel<a_, b_, c_, d_>}
 // ordered by preference: fewest lanes per scenario first, then smallest register footprint
 static const LocalVariant kLocalVariants[] = {
+    PHG_L(16, 4, 2, 1),
     PHG_L(16, 4, 3, 1),
     PHG_L(16, 4, 4, 2),
+    PHG_L(32, 4, 2, 1),
     PHG_L(32, 4, 3, 1),
     PHG_L(32, 4, 4, 2),
+    PHG_L(64, 4, 2, 1),
     PHG_L(64, 4, 3, 1),
     PHG_L(64, 4, 4, 2),
 };

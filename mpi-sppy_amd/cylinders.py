@@ -44,7 +44,8 @@ class _BoundSpoke:
             pass
         # same batch (host arrays), same layout; the spoke's handle creates its own stream
         self.engine = Engine(he.batch, device=dev, stream=None, exchange=None,
-                             layout=hub_opt.options.get("pdhg_layout", "auto"))
+                             layout=hub_opt.options.get("pdhg_layout", "auto"),
+                             presolve=hub_opt.options.get("pdhg_presolve", True))
         self.engine.set(_lib.F_RHO, he.get(_lib.F_RHO))
         self.pending = False
         self.bound = None

@@ -137,7 +137,7 @@ class Engine:
 
     LAYOUTS = {"auto": 0, "gather": 1, "local": 2, "block": 3}
 
-    def __init__(self, batch, device=0, stream=None, exchange=None, layout="auto"):
+    def __init__(self, batch, device=0, stream=None, exchange=None, layout="auto", presolve=True):
         self.lib = _lib.load()
         self.batch = batch
         import ctypes
@@ -147,6 +147,7 @@ class Engine:
         if stream is not None:
             _lib.check(self.lib.phg_set_stream(self.h, ctypes.c_void_p(int(stream))))
         _lib.check(self.lib.phg_set_layout(self.h, self.LAYOUTS[layout]))
+        _lib.check(self.lib.phg_set_presolve(self.h, int(bool(presolve))))
         b, keep = batch.c_struct()
         _lib.check(self.lib.phg_load_batch(self.h, ctypes.byref(b)))
         del keep
@@ -157,6 +158,9 @@ class Engine:
         self.variant = int(info[6])
         self.lanes_per_scenario = int(info[7])
         self.layout = "block" if self.variant >= 200 else ("local" if self.variant >= 100 else "gather")
+        pi = np.zeros(2, np.int32)
+        _lib.check(self.lib.phg_presolve_info(self.h, ptr(pi)))
+        self.rows_folded, self.rows_kept = int(pi[0]), int(pi[1])
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:

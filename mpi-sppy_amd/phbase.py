@@ -97,7 +97,8 @@ class PHBase(SPBase):
                             len(self.all_scenario_names), self._virt_nproc())
         device, stream, exchange = self._device_setup(batch)
         self.engine = Engine(batch, device=device, stream=stream, exchange=exchange,
-                             layout=self.options.get("pdhg_layout", "auto"))
+                             layout=self.options.get("pdhg_layout", "auto"),
+                             presolve=self.options.get("pdhg_presolve", True))
         self.engine.set(_lib.F_RHO, float(self.options["defaultPHrho"]))
 
     def _device_setup(self, batch):

@@ -254,3 +254,24 @@ def test_variable_probability_vs_oracle():
     np.testing.assert_allclose(ph.Ws(), o.W, atol=1e-5)
     assert ph.Ws()[2, 0] == 0.0
     np.testing.assert_allclose(ph.conv_history, o.history, rtol=1e-5, atol=1e-8)
+
+
+# ----------------------------------------------------------------------------- presolve
+def test_singleton_row_presolve_same_solutions():
+    """phg_set_presolve: farmer's EnforceQuotas rows fold into column bounds; the PH trajectory is
+    the same LP/QP sequence, so x̄, W and the bounds agree with the un-presolved run (1e-6)."""
+    res = []
+    for pre in (True, False):
+        ph = _farmer_ph(5, cm=2, PHIterLimit=6, pdhg_presolve=pre)
+        conv, eobj, tb = ph.ph_main()
+        e = ph.engine
+        res.append((tb, eobj, ph.xbars(), ph.Ws(), e.rows_folded, e.get(_lib.F_Y).reshape(e.S, -1)))
+    (tb1, e1, xb1, W1, f1, y1), (tb0, e0, xb0, W0, f0, y0) = res
+    assert f1 == 2 * 3 and f0 == 0          # one EnforceQuotas row per crop (cm=2: 6 crops)
+    assert abs(tb1 - tb0) <= 1e-7 * abs(tb0) and abs(e1 - e0) <= 1e-6 * abs(e0)
+    np.testing.assert_allclose(xb1, xb0, rtol=1e-6)
+    np.testing.assert_allclose(W1, W0, atol=1e-5)
+    assert y1.shape == y0.shape             # caller's row numbering; folded rows read back 0
+    m = farmer.scenario_creator("scen0", crops_multiplier=2, num_scens=5)
+    folded = [i for i, r in enumerate(m._rows) if len(r[0]) == 1]
+    assert len(folded) == 6 and np.all(y1[:, folded] == 0.0)

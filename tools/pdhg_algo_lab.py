@@ -83,7 +83,7 @@ class Lab:
                        + (pobj - dobj) ** 2)
 
     # ------------------------------------------------------------------ one solve
-    def solve(self, c, q, x0, y0, variant="ra", gamma=1.0, bs=0.2, bnec=0.8, ba=0.36, th=0.5):
+    def solve(self, c, q, x0, y0, variant="ra", gamma=1.0, bs=0.2, bnec=0.8, ba=0.36, th=0.5, noavg=0.0):
         b = self.b
         S = b.S
         dc, dr = self.dc, self.dr
@@ -146,7 +146,9 @@ class Lab:
                 rc_, pc = self.rel(x, y, cs, qs, cl, cu, rl, ru, Ax, ATy)
                 ra_, pa = self.rel(xav, yav, cs, qs, cl, cu, rl, ru)
                 kc, ka = self.wkkt(pc, omega), self.wkkt(pa, omega)
-                ua = ka < kc
+                ua = (ka < kc) & (noavg == 0.0)
+                if noavg:
+                    ra_ = np.full_like(rc_, np.inf)
                 cand = np.where(ua, ka, kc)
                 fin_ = (np.minimum(rc_, ra_) <= self.eps) & ~done
                 xf = np.where(ua[b.sc] & (ra_ < rc_)[b.sc], xav, x)
@@ -192,6 +194,26 @@ class Lab:
         return xout * dc, yout * dr, iters
 
 
+def singleton_rows_to_bounds(a, keep_cols):
+    """Rows with one nonzero on a non-nonant column become bounds on that column."""
+    rp, ci, v = a["rowptr"], a["colidx"], a["vals"]
+    cl, cu = a["col_lo"].copy(), a["col_hi"].copy()
+    keep = []
+    for i in range(len(rp) - 1):
+        if rp[i + 1] - rp[i] == 1 and ci[rp[i]] not in keep_cols and v[rp[i]] != 0:
+            j, aa = ci[rp[i]], v[rp[i]]
+            lo, hi = a["row_lo"][i] / aa, a["row_hi"][i] / aa
+            if aa < 0:
+                lo, hi = hi, lo
+            cl[j], cu[j] = max(cl[j], lo), min(cu[j], hi)
+        else:
+            keep.append(i)
+    rows = [(ci[rp[i]:rp[i + 1]], v[rp[i]:rp[i + 1]]) for i in keep]
+    nrp = np.concatenate([[0], np.cumsum([len(r[0]) for r in rows])]).astype(np.int32)
+    return dict(a, rowptr=nrp, colidx=np.concatenate([r[0] for r in rows]), vals=np.concatenate([r[1] for r in rows]),
+                row_lo=a["row_lo"][keep], row_hi=a["row_hi"][keep], col_lo=cl, col_hi=cu)
+
+
 def main():
     S = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     cm = int(sys.argv[2]) if len(sys.argv) > 2 else 10
@@ -200,6 +222,9 @@ def main():
     from oracle import models as om
     scens = [om.farmer(nm, crops_multiplier=cm, num_scens=S) for nm in om.farmer_names(S)]
     arrs = [s.arrays() for s in scens]
+    if os.environ.get("LAB_PRESOLVE"):
+        arrs = [singleton_rows_to_bounds(a, set(scens[0].nonant_cols())) for a in arrs]
+        print("presolve: m", len(arrs[0]["row_lo"]), flush=True)
     b = Batch(arrs)
     cols = np.array(scens[0].nonant_cols())
     N = len(cols)
