@@ -22,14 +22,22 @@ namespace phg {
 // Per-lane "cold" state (read only at the every-`check_every` restart/termination test) lives in
 // LDS as [item][lane] doubles -- conflict-free ds_read_b64 -- so the registers hold only what the
 // PDHG iteration itself touches.
+// cold items per lane: XR/YR/YDR restart point, Q diagonal, IDC/IDR/IDRD inverse scalings (unscaled
+// residuals), BLO/BHI/DLO/DHI the scaled row bounds (the registers hold them times -sigma), then
+// per-group scalars (CNORM, BNORM, ... replicated in every lane of the group)
+constexpr int cold_items(int CPL, int RPL, int D) { return 3 * CPL + 4 * RPL + 4 * (D > 0 ? D : 1) + 11; }
+
 template <int CPL, int RPL, int D>
 struct Cold {
     static constexpr int DD = D > 0 ? D : 1;
-    static constexpr int XR = 0, Q = CPL, IDC = 2 * CPL, YR = 3 * CPL, IDR = 3 * CPL + RPL,
-                         YDR = 3 * CPL + 2 * RPL, IDRD = 3 * CPL + 2 * RPL + DD,
-                         SC = 3 * CPL + 2 * RPL + 2 * DD;
-    enum { CNORM = 0, BNORM, ETA, PROX, OMEGA, KRST, KPREV, NSC };
+    static constexpr int XR = 0, Q = CPL, IDC = 2 * CPL, YR = 3 * CPL, IDR = YR + RPL, BLO = IDR + RPL,
+                         BHI = BLO + RPL, YDR = BHI + RPL, IDRD = YDR + DD, DLO = IDRD + DD, DHI = DLO + DD,
+                         SC = DHI + DD;
+    // KRST / KPREV hold SQUARED weighted KKT errors; TP / TD the squared termination thresholds
+    // (eps (1 + ||b||))^2, (eps (1 + ||c||))^2; W2 / IW2 = omega^2, 1 / omega^2
+    enum { CNORM = 0, BNORM, ETA, PROX, OMEGA, KRST, KPREV, TP, TD, W2, IW2, NSC };
     static constexpr int N = SC + NSC;
+    static_assert(N == cold_items(CPL, RPL, D), "cold layout");
 };
 
 template <int LPS, int CPL, int RPL, int D>
@@ -108,6 +116,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 y[r] = yy;
             }
             CS(CI::YR + r) = y[r];
+            CS(CI::BLO + r) = rlo[r];
+            CS(CI::BHI + r) = rhi[r];
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 const int p = L.blk_p[(gl * RPL + r) * CPL + k];
@@ -138,6 +148,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 yd[d] = yy;
             }
             CS(CI::YDR + d) = yd[d];
+            CS(CI::DLO + d) = dlo[d];
+            CS(CI::DHI + d) = dhi[d];
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 const int p = L.cpl_p[(d * LPS + gl) * CPL + k];
@@ -199,55 +211,48 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
     const double eta = a.eta[s];
     CS(CI::SC + CI::BNORM) = a.bnorm[s];
     CS(CI::SC + CI::ETA) = eta;
+    {
+        const double tp = a.eps * (1.0 + a.bnorm[s]), td = a.eps * (1.0 + CS(CI::SC + CI::CNORM));
+        CS(CI::SC + CI::TP) = tp * tp;
+        CS(CI::SC + CI::TD) = td * td;
+    }
     double tau = eta / omega, sig = eta * omega;
-    // row bounds are held pre-multiplied by -sig (the dual step; re-derived from memory at
+    // row bounds are held pre-multiplied by -sig (the dual step; re-derived from the LDS copy at
     // restarts), so the dual projection is one v_max_f64 + one v_min_f64 without modifiers
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) { rlo[r] *= -sig; rhi[r] *= -sig; }
-#pragma unroll
-    for (int d = 0; d < D; ++d) { dlo[d] *= -sig; dhi[d] *= -sig; }
     auto rescale_bounds = [&]() {
-        const int sl = launder(s);
-        const long sm = (long)sl * a.m;
 #pragma unroll
-        for (int r = 0; r < RPL; ++r) {
-            seq();
-            const int i = L.row_of[gl * RPL + r];
-            if (i >= 0) { rlo[r] = -sig * a.rl[sm + i]; rhi[r] = -sig * a.ru[sm + i]; }
-        }
+        for (int r = 0; r < RPL; ++r) { rlo[r] = -sig * CS(CI::BLO + r); rhi[r] = -sig * CS(CI::BHI + r); }
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            seq();
-            const int i = L.cpl_row[d];
-            if (i >= 0) { dlo[d] = -sig * a.rl[sm + i]; dhi[d] = -sig * a.ru[sm + i]; }
-        }
+        for (int d = 0; d < D; ++d) { dlo[d] = -sig * CS(CI::DLO + d); dhi[d] = -sig * CS(CI::DHI + d); }
     };
+    rescale_bounds();
 #pragma unroll
     for (int k = 0; k < CPL; ++k) ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
 
     mv_ax(x, ax, axd);
     mv_aty(y, yd, aty);
 
-    // KKT pieces of one iterate over the scenario (group): [0] ||pr||^2 scaled, [1] ||dres||^2
-    // scaled, [2] ||pr||^2 unscaled, [3] ||dres||^2 unscaled, [4] primal objective, [5] dual
-    // objective.  The iterate is given element-wise (xf, atf: column k; yf, axf: local row r;
-    // ydf: coupling row d; axdp: coupling row d's LOCAL partial of A x, reduced here together with
-    // the KKT sums, scaled by `scale`) so the average iterate is never materialised in registers.
-    // Row/column scalings are re-read from memory (cold path).
-    auto kkt = [&](auto xf, auto atf, auto yf, auto axf, auto ydf, auto axdp, double scale, double* o) {
-        double t[6 + DD];
+    // KKT pieces of an iterate over the scenario (group): [0] omega^2 ||pr||^2 + ||dres||^2 /
+    // omega^2 on the scaled problem (PDLP's restart metric without the gap term), [1] unused,
+    // [2] ||pr||^2 unscaled, [3] ||dres||^2 unscaled, [4] primal objective, [5] dual objective.  The iterate is given element-wise (xf, atf: column k; yf, axf: local row r;
+    // axdp: coupling row d's LOCAL partial of A x) so the average iterate is never materialised in
+    // registers.  Padded column / row slots hold zeros everywhere, so no per-element branches.
+    constexpr int KT = 5 + DD;   // reduced values per iterate
+    // slot of coupling row d's A x partial: 1 (free in the reduced vector), then 6, 7, ...
+    auto cslot = [](int d) { return d == 0 ? 1 : 5 + d; };
+    auto kkt_part = [&](auto xf, auto atf, auto yf, auto axf, auto axdp, double* t) {
 #pragma unroll
-        for (int u = 0; u < 6 + DD; ++u) t[u] = 0.0;
-        const double isg = -1.0 / sig;   // registers hold -sig * (row bounds)
+        for (int u = 0; u < KT; ++u) t[u] = 0.0;
+        double pr2 = 0.0, dr2 = 0.0;
         // element by element (seq() stops the scheduler from hoisting every element's loads and
         // products at once, which would hold them all in registers beside the hot state)
 #pragma unroll
         for (int r = 0; r < RPL; ++r) {
             seq();
             const double axx = axf(r), yy = yf(r);
-            const double bl = rlo[r] * isg, bu = rhi[r] * isg;
-            const double pr = axx - clampd(axx, bl, bu);   // 0 on empty slots
-            t[0] += pr * pr;
+            const double bl = CS(CI::BLO + r), bu = CS(CI::BHI + r);
+            const double pr = axx - clampd(axx, bl, bu);
+            pr2 += pr * pr;
             const double pu = pr * CS(CI::IDR + r);
             t[2] += pu * pu;
             if (fin(bl)) t[5] += bl * fmax(yy, 0.0);
@@ -256,91 +261,109 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             seq();
-            if (cj[k] >= 0) {
-                const double xx = xf(k);
-                const double qk = CS(CI::Q + k);
-                const double rc_ = c[k] + qk * xx - atf(k);
-                double dres = 0.0;
-                if (!fin(lo[k]) && rc_ > 0.0) dres += rc_;
-                if (!fin(hi[k]) && rc_ < 0.0) dres += rc_;
-                t[1] += dres * dres;
-                const double du = dres * CS(CI::IDC + k);
-                t[3] += du * du;
-                t[4] += c[k] * xx + 0.5 * qk * xx * xx;
-                if (fin(lo[k])) t[5] += lo[k] * fmax(rc_, 0.0);
-                if (fin(hi[k])) t[5] += hi[k] * fmin(rc_, 0.0);
-                t[5] -= 0.5 * qk * xx * xx;
-            }
+            const double xx = xf(k);
+            const double qk = CS(CI::Q + k);
+            const double rc_ = c[k] + qk * xx - atf(k);
+            double dres = 0.0;
+            if (!fin(lo[k]) && rc_ > 0.0) dres += rc_;
+            if (!fin(hi[k]) && rc_ < 0.0) dres += rc_;
+            dr2 += dres * dres;
+            const double du = dres * CS(CI::IDC + k);
+            t[3] += du * du;
+            const double hq = 0.5 * qk * xx * xx;
+            t[4] += c[k] * xx + hq;
+            if (fin(lo[k])) t[5] += lo[k] * fmax(rc_, 0.0);
+            if (fin(hi[k])) t[5] += hi[k] * fmin(rc_, 0.0);
+            t[5] -= hq;
         }
+        t[0] = fma(CS(CI::SC + CI::W2), pr2, dr2 * CS(CI::SC + CI::IW2));
 #pragma unroll
-        for (int d = 0; d < D; ++d) t[6 + d] = axdp(d);
-        gsum_many<LPS, 6 + DD>(t);
-        // replicated coupling rows, added once after the group reduction
+        for (int d = 0; d < D; ++d) t[cslot(d)] = axdp(d);
+    };
+    // replicated coupling rows, added once after the group reduction
+    auto kkt_coupling = [&](double* t, auto ydf, double scale) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             seq();
-            const double axx = t[6 + d] * scale, yy = ydf(d);
-            const double bl = dlo[d] * isg, bu = dhi[d] * isg;
-            const double pr = axx - clampd(axx, bl, bu);   // 0 on unused coupling slots
-            t[0] += pr * pr;
+            const double axx = t[cslot(d)] * scale, yy = ydf(d);
+            const double bl = CS(CI::DLO + d), bu = CS(CI::DHI + d);
+            const double pr = axx - clampd(axx, bl, bu);
+            t[0] = fma(CS(CI::SC + CI::W2), pr * pr, t[0]);
             const double pu = pr * CS(CI::IDRD + d);
             t[2] += pu * pu;
             if (fin(bl)) t[5] += bl * fmax(yy, 0.0);
             if (fin(bu)) t[5] += bu * fmin(yy, 0.0);
         }
-#pragma unroll
-        for (int u = 0; u < 6; ++u) o[u] = t[u];
     };
-    // the current iterate: coupling products are already reduced, so their "partial" is the
-    // value divided by the group size... instead pass the lane-0 share: value on gl == 0, else 0
-    auto kkt_cur = [&](double* o) {
-        kkt([&](int k) { return x[k]; }, [&](int k) { return aty[k]; }, [&](int r) { return y[r]; },
-            [&](int r) { return ax[r]; }, [&](int d) { return yd[d]; },
-            [&](int d) { return gl == 0 ? axd[d] : 0.0; }, 1.0, o);
+    // the current iterate (its coupling products are already reduced: lane 0 of the group
+    // contributes them) and, with AVG, the average iterate: one group reduction for both
+    auto kkt_both = [&](bool avg, double inv, double* oc, double* oa) {
+        double t[2 * KT];
+        kkt_part([&](int k) { return x[k]; }, [&](int k) { return aty[k]; }, [&](int r) { return y[r]; },
+                 [&](int r) { return ax[r]; }, [&](int d) { return gl == 0 ? axd[d] : 0.0; }, t);
+        if (avg) {
+            kkt_part([&](int k) { return xsum[k] * inv; },
+                     [&](int k) {
+                         double acc = blk[0][k] * ysum[0];
+#pragma unroll
+                         for (int r = 1; r < RPL; ++r) acc = fma(blk[r][k], ysum[r], acc);
+#pragma unroll
+                         for (int d = 0; d < D; ++d) acc = fma(cf[d][k], ydsum[d], acc);
+                         return acc * inv;
+                     },
+                     [&](int r) { return ysum[r] * inv; },
+                     [&](int r) {
+                         double acc = blk[r][0] * xsum[0];
+#pragma unroll
+                         for (int k = 1; k < CPL; ++k) acc = fma(blk[r][k], xsum[k], acc);
+                         return acc * inv;
+                     },
+                     [&](int d) {
+                         double acc = cf[d][0] * xsum[0];
+#pragma unroll
+                         for (int k = 1; k < CPL; ++k) acc = fma(cf[d][k], xsum[k], acc);
+                         return acc;
+                     },
+                     t + KT);
+            gsum_many<LPS, 2 * KT>(t);
+        } else {
+            gsum_many<LPS, KT>(*reinterpret_cast<double(*)[KT]>(t));
+        }
+        kkt_coupling(t, [&](int d) { return yd[d]; }, 1.0);
+#pragma unroll
+        for (int u = 0; u < 6; ++u) oc[u] = t[u];
+        if (avg) {
+            kkt_coupling(t + KT, [&](int d) { return ydsum[d] * inv; }, inv);
+#pragma unroll
+            for (int u = 0; u < 6; ++u) oa[u] = t[KT + u];
+        }
     };
-    auto kkt_avg = [&](double inv, double* o) {
-        kkt([&](int k) { return xsum[k] * inv; },
-            [&](int k) {
-                double acc = blk[0][k] * ysum[0];
-#pragma unroll
-                for (int r = 1; r < RPL; ++r) acc = fma(blk[r][k], ysum[r], acc);
-#pragma unroll
-                for (int d = 0; d < D; ++d) acc = fma(cf[d][k], ydsum[d], acc);
-                return acc * inv;
-            },
-            [&](int r) { return ysum[r] * inv; },
-            [&](int r) {
-                double acc = blk[r][0] * xsum[0];
-#pragma unroll
-                for (int k = 1; k < CPL; ++k) acc = fma(blk[r][k], xsum[k], acc);
-                return acc * inv;
-            },
-            [&](int d) { return ydsum[d] * inv; },
-            [&](int d) {
-                double acc = cf[d][0] * xsum[0];
-#pragma unroll
-                for (int k = 1; k < CPL; ++k) acc = fma(cf[d][k], xsum[k], acc);
-                return acc;
-            },
-            inv, o);
-    };
+    // relative KKT error (reported in the epilogue only)
     auto rel_of = [&](const double* o) {
         const double p = sqrt(o[2]) / (1.0 + CS(CI::SC + CI::BNORM));
         const double d = sqrt(o[3]) / (1.0 + CS(CI::SC + CI::CNORM));
         const double g = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
         return fmax(fmax(p, d), g);
     };
-    auto wkkt_of = [&](const double* o, double w) {
+    // rel_of(o) <= eps without square roots or divisions
+    auto converged = [&](const double* o) {
+        return o[2] <= CS(CI::SC + CI::TP) && o[3] <= CS(CI::SC + CI::TD) &&
+               fabs(o[4] - o[5]) <= a.eps * (1.0 + fabs(o[4]) + fabs(o[5]));
+    };
+    // squared primal-weighted KKT error (PDLP's restart metric)
+    auto wkkt2_of = [&](const double* o) {
         const double g = o[4] - o[5];
-        return sqrt(w * w * o[0] + o[1] / (w * w) + g * g);
+        return fma(g, g, o[0]);
     };
 
+    CS(CI::SC + CI::OMEGA) = omega;
+    CS(CI::SC + CI::W2) = omega * omega;
+    CS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
     {
         double o[6];
-        kkt_cur(o);
-        CS(CI::SC + CI::KRST) = wkkt_of(o, omega);
+        kkt_both(false, 0.0, o, o);
+        CS(CI::SC + CI::KRST) = wkkt2_of(o);
         CS(CI::SC + CI::KPREV) = INFINITY;
-        CS(CI::SC + CI::OMEGA) = omega;
     }
     int it = 0, since = 0, cnt = 0;
     bool live = true;
@@ -442,13 +465,13 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         // ---------------------------------------------------------- restart / termination check
         const double inv = 1.0 / (double)cnt;
         double oc[6], oa[6];
-        kkt_cur(oc);
-        kkt_avg(inv, oa);
-        const double rel_cur = rel_of(oc), rel_avg = rel_of(oa);
-        const bool nan = !(rel_cur == rel_cur);
-        const bool term = live && (nan || rel_cur <= a.eps || rel_avg <= a.eps);
+        kkt_both(true, inv, oc, oa);
+        const bool nan = !(oc[2] + oc[3] + oc[4] + oc[5] == oc[2] + oc[3] + oc[4] + oc[5]);
+        const bool ok_cur = converged(oc), ok_avg = converged(oa);
+        const bool term = live && (nan || ok_cur || ok_avg);
         const bool cap = live && !term && it >= a.max_iter;
         if (term || cap) {
+            const double rel_cur = rel_of(oc), rel_avg = rel_of(oa);
             const bool ua = !nan && rel_avg < rel_cur;
             finish(ua, inv, ua ? rel_avg : rel_cur, ua ? oa[4] : oc[4], ua ? oa[5] : oc[5],
                    nan ? 2 : (term ? 0 : 1));
@@ -456,23 +479,27 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         }
         if (!wave_any(live)) break;
 
-        omega = CS(CI::SC + CI::OMEGA);
-        const double k_cur = wkkt_of(oc, omega), k_avg = wkkt_of(oa, omega);
+        const double k_cur = wkkt2_of(oc), k_avg = wkkt2_of(oa);
         const bool use_avg = k_avg < k_cur;
         const double cand = use_avg ? k_avg : k_cur;
         const double krst = CS(CI::SC + CI::KRST);
-        const bool restart = live && ((cand <= a.beta_suf * krst) ||
-                                      (cand <= a.beta_nec * krst && cand > CS(CI::SC + CI::KPREV)) ||
+        const bool restart = live && ((cand <= a.beta_suf * a.beta_suf * krst) ||
+                                      (cand <= a.beta_nec * a.beta_nec * krst && cand > CS(CI::SC + CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
         CS(CI::SC + CI::KPREV) = cand;
         if (wave_any(restart)) {
             const bool ra = restart && use_avg;
+            if (wave_any(ra)) {
 #pragma unroll
-            for (int k = 0; k < CPL; ++k) x[k] = ra ? xsum[k] * inv : x[k];
+                for (int k = 0; k < CPL; ++k) x[k] = ra ? xsum[k] * inv : x[k];
 #pragma unroll
-            for (int r = 0; r < RPL; ++r) y[r] = ra ? ysum[r] * inv : y[r];
+                for (int r = 0; r < RPL; ++r) y[r] = ra ? ysum[r] * inv : y[r];
 #pragma unroll
-            for (int d = 0; d < D; ++d) yd[d] = ra ? ydsum[d] * inv : yd[d];
+                for (int d = 0; d < D; ++d) yd[d] = ra ? ydsum[d] * inv : yd[d];
+                // exact products at the new point; groups that keep their point recompute the same
+                mv_ax(x, ax, axd);
+                mv_aty(y, yd, aty);
+            }
             // primal weight update (theta = 0.5) from the movement since the last restart
             double mv[2] = {0.0, 0.0};
 #pragma unroll
@@ -482,15 +509,12 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             gsum_many<LPS, 2>(mv);
 #pragma unroll
             for (int d = 0; d < D; ++d) { const double t = yd[d] - CS(CI::YDR + d); mv[1] += t * t; }
-            const double dx = sqrt(mv[0]), dy = sqrt(mv[1]);
-            if (restart && dx > 1e-10 && dy > 1e-10) omega = sqrt(dy / dx * omega);   // exp(.5 log(dy/dx) + .5 log w)
+            omega = CS(CI::SC + CI::OMEGA);
+            if (restart && mv[0] > 1e-20 && mv[1] > 1e-20) omega = sqrt(sqrt(mv[1] / mv[0]) * omega);
             const double et = CS(CI::SC + CI::ETA);
             tau = et / omega;
             sig = et * omega;
             rescale_bounds();
-            // exact products at the (possibly new) point; unchanged groups recompute the same values
-            mv_ax(x, ax, axd);
-            mv_aty(y, yd, aty);
 #pragma unroll
             for (int k = 0; k < CPL; ++k) ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
             if (restart) {
@@ -501,6 +525,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) { CS(CI::YDR + d) = yd[d]; ydsum[d] = 0.0; }
                 CS(CI::SC + CI::OMEGA) = omega;
+                CS(CI::SC + CI::W2) = omega * omega;
+                CS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
                 CS(CI::SC + CI::KRST) = cand;
                 CS(CI::SC + CI::KPREV) = INFINITY;
                 cnt = 0;
@@ -541,7 +567,8 @@ void pdhg_local_variant_shape(int v, int* out4) {
 size_t pdhg_local_lds_bytes(int v) {
     const LocalVariant& V = kLocalVariants[v];
     const int DD = V.D > 0 ? V.D : 1;
-    return (size_t)(3 * V.CPL + 2 * V.RPL + 2 * DD + 7) * 64 * sizeof(double);   // Cold<CPL,RPL,D>::N
+    (void)DD;
+    return (size_t)cold_items(V.CPL, V.RPL, V.D) * 64 * sizeof(double);
 }
 
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream) {
