@@ -88,6 +88,10 @@ typedef struct phg_opts {
     double  beta_sufficient;   /* default 0.2  */
     double  beta_necessary;    /* default 0.8  */
     double  beta_artificial;   /* default 0.25 (tuned on PH prox-QPs; PDLP uses 0.36) */
+    /* primal weight smoothing at restarts, omega <- (dy/dx)^theta omega^(1-theta);
+     * (0, 1], <= 0 selects the default 0.8 (PDLP uses 0.5; 0.8 measured on MI355X: farmer
+     * 10k +10 %, sslp 2048 +16 %, netdes 1024 -1 % solves/s)                                 */
+    double  primal_weight_theta;
 } phg_opts;
 
 /* solve modes (mpisppy/phbase.py:670-760: W_on / prox_on toggles) */

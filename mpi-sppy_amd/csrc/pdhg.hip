@@ -344,7 +344,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
             for (int r = 0; r < RPL; ++r) { const double d = y[r] - yr[r]; mv[1] += d * d; }
             wsum_many<2>(mv);
             const double dx = sqrt(mv[0]), dy = sqrt(mv[1]);
-            if (dx > 1e-10 && dy > 1e-10) omega = sqrt(dy / dx * omega);
+            omega = primal_weight(omega, dx * dx, dy * dy, a.theta);
             tau = eta / omega;
             sig = eta * omega;
             // exact products at the restart point

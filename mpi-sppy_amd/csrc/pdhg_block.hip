@@ -360,7 +360,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             }
             block_sum<NT, 2>(mv, red);
             const double dx = sqrt(mv[0]), dy = sqrt(mv[1]);
-            if (dx > 1e-10 && dy > 1e-10) omega = sqrt(dy / dx * omega);
+            omega = primal_weight(omega, dx * dx, dy * dy, a.theta);
             tau = eta / omega;
             sig = eta * omega;
 #pragma unroll

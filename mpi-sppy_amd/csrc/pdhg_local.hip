@@ -22,15 +22,15 @@ namespace phg {
 // Per-lane "cold" state (read only at the every-`check_every` restart/termination test) lives in
 // LDS as [item][lane] doubles -- conflict-free ds_read_b64 -- so the registers hold only what the
 // PDHG iteration itself touches.
-// cold items per lane: XR/YR/YDR restart point, Q diagonal, IDC/IDR/IDRD inverse scalings (unscaled
+// cold items per lane: XR/YR/YDR restart point, Q diagonal, C scaled cost, IDC/IDR/IDRD inverse scalings (unscaled
 // residuals), BLO/BHI/DLO/DHI the scaled row bounds (the registers hold them times -sigma), then
 // per-group scalars (CNORM, BNORM, ... replicated in every lane of the group)
-constexpr int cold_items(int CPL, int RPL, int D) { return 3 * CPL + 4 * RPL + 4 * (D > 0 ? D : 1) + 11; }
+constexpr int cold_items(int CPL, int RPL, int D) { return 4 * CPL + 4 * RPL + 4 * (D > 0 ? D : 1) + 11; }
 
 template <int CPL, int RPL, int D>
 struct Cold {
     static constexpr int DD = D > 0 ? D : 1;
-    static constexpr int XR = 0, Q = CPL, IDC = 2 * CPL, YR = 3 * CPL, IDR = YR + RPL, BLO = IDR + RPL,
+    static constexpr int XR = 0, Q = CPL, IDC = 2 * CPL, C = 3 * CPL, YR = 4 * CPL, IDR = YR + RPL, BLO = IDR + RPL,
                          BHI = BLO + RPL, YDR = BHI + RPL, IDRD = YDR + DD, DLO = IDRD + DD, DHI = DLO + DD,
                          SC = DHI + DD;
     // KRST / KPREV hold SQUARED weighted KKT errors; TP / TD the squared termination thresholds
@@ -58,7 +58,12 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
 
     // ------------------------------------------------------------------ columns of this lane
     int cj[CPL];
-    double x[CPL], aty[CPL], c[CPL], lo[CPL], hi[CPL], ip[CPL], xsum[CPL];
+    // the primal step is x+ = clamp(x ip + A^T y tip - ctip) with ip = 1 / (1 + tau q),
+    // tip = tau ip, ctip = c tip (re-derived whenever tau changes; c itself is read from LDS):
+    // 2 instead of 3 fp64 ops per column, for 2 more registers per column -- only where they
+    // fit (the widest variants would spill; they keep x+ = clamp((x + tau (A^T y - c)) ip))
+    constexpr bool FOLD = RPL * CPL + D * CPL <= 12;
+    double x[CPL], aty[CPL], c[CPL], lo[CPL], hi[CPL], ip[CPL], tip[CPL], ctip[CPL], xsum[CPL];
     double prox_const = 0.0, c2 = 0.0;
     {
         const long sn = (long)s * a.n, sN = (long)s * a.N;
@@ -226,8 +231,19 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         for (int d = 0; d < D; ++d) { dlo[d] = -sig * CS(CI::DLO + d); dhi[d] = -sig * CS(CI::DHI + d); }
     };
     rescale_bounds();
+    auto step_coefs = [&]() {
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
+        for (int k = 0; k < CPL; ++k) {
+            ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
+            if constexpr (FOLD) {
+                tip[k] = tau * ip[k];
+                ctip[k] = CS(CI::C + k) * tip[k];
+            }
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) CS(CI::C + k) = c[k];
+    step_coefs();
 
     mv_ax(x, ax, axd);
     mv_aty(y, yd, aty);
@@ -263,7 +279,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             seq();
             const double xx = xf(k);
             const double qk = CS(CI::Q + k);
-            const double rc_ = c[k] + qk * xx - atf(k);
+            const double ck = FOLD ? CS(CI::C + k) : c[k];
+            const double rc_ = ck + qk * xx - atf(k);
             double dres = 0.0;
             if (!fin(lo[k]) && rc_ > 0.0) dres += rc_;
             if (!fin(hi[k]) && rc_ < 0.0) dres += rc_;
@@ -271,7 +288,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             const double du = dres * CS(CI::IDC + k);
             t[3] += du * du;
             const double hq = 0.5 * qk * xx * xx;
-            t[4] += c[k] * xx + hq;
+            t[4] += ck * xx + hq;
             if (fin(lo[k])) t[5] += lo[k] * fmax(rc_, 0.0);
             if (fin(hi[k])) t[5] += hi[k] * fmin(rc_, 0.0);
             t[5] -= hq;
@@ -428,7 +445,9 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             // primal step: exact prox of the diagonal quadratic + box (1/(1+tau q) precomputed)
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
-                const double xn = vmin(vmax(fma(tau, aty[k] - c[k], x[k]) * ip[k], lo[k]), hi[k]);
+                double xn;
+                if constexpr (FOLD) xn = vmin(vmax(fma(aty[k], tip[k], fma(x[k], ip[k], -ctip[k])), lo[k]), hi[k]);
+                else xn = vmin(vmax(fma(tau, aty[k] - c[k], x[k]) * ip[k], lo[k]), hi[k]);
                 x[k] = xn;
                 xsum[k] += xn;
             }
@@ -510,13 +529,12 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
 #pragma unroll
             for (int d = 0; d < D; ++d) { const double t = yd[d] - CS(CI::YDR + d); mv[1] += t * t; }
             omega = CS(CI::SC + CI::OMEGA);
-            if (restart && mv[0] > 1e-20 && mv[1] > 1e-20) omega = sqrt(sqrt(mv[1] / mv[0]) * omega);
+            if (restart) omega = primal_weight(omega, mv[0], mv[1], a.theta);
             const double et = CS(CI::SC + CI::ETA);
             tau = et / omega;
             sig = et * omega;
             rescale_bounds();
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
+            step_coefs();
             if (restart) {
 #pragma unroll
                 for (int k = 0; k < CPL; ++k) { CS(CI::XR + k) = x[k]; xsum[k] = 0.0; }

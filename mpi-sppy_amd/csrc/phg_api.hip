@@ -1141,6 +1141,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.beta_suf = o->beta_sufficient > 0 ? o->beta_sufficient : 0.2;
     a.beta_nec = o->beta_necessary > 0 ? o->beta_necessary : 0.8;
     a.beta_art = o->beta_artificial > 0 ? o->beta_artificial : 0.25;
+    a.theta = o->primal_weight_theta > 0 && o->primal_weight_theta <= 1 ? o->primal_weight_theta : 0.8;
     if (h->local_variant >= 0) a.check_every = (a.check_every + 1) & ~1;   // 2 iterations per trip
     if (timing_event(h, 0, 0)) return -1;
     a.loc = h->loc;

@@ -103,6 +103,7 @@ struct PdhgArgs {
     int w_on, prox_on, fix_nonants, warm, max_iter, check_every;
     double eps, sense;
     double beta_suf, beta_nec, beta_art;   // restart rule
+    double theta;                          // primal weight smoothing (1: no smoothing)
 };
 
 struct PrepArgs {
@@ -178,6 +179,19 @@ __device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, double& cc, 
             pc += 0.5 * p * z * z;
         }
     }
+}
+
+// PDLP primal weight update at a restart: omega <- (dy/dx)^theta omega^(1-theta), from the squared
+// primal / dual movements since the last restart (dx2, dy2; unchanged if either is ~0).  theta 1
+// and 0.5 are exact square roots; other values go through the fp32 log2 / exp2 units (a heuristic
+// step-size balance: fp32 precision is plenty).
+__device__ __forceinline__ double primal_weight(double omega, double dx2, double dy2, double theta) {
+    if (!(dx2 > 1e-20 && dy2 > 1e-20)) return omega;
+    const double r = sqrt(dy2 / dx2);
+    if (theta == 1.0) return r;
+    if (theta == 0.5) return sqrt(r * omega);
+    const float l = (float)theta * __log2f((float)r) + (1.0f - (float)theta) * __log2f((float)omega);
+    return (double)exp2f(l);
 }
 
 }  // namespace phg

@@ -199,9 +199,10 @@ class Engine:
 
     # ------------------------------------------------------------------ hot path
     def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=32, warm_start=3,
-              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0)):
+              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0), theta=0.0):
         o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(warm_start),
-                         int(bool(fix_nonants)), int(bool(schedule)), *[float(v) for v in beta])
+                         int(bool(fix_nonants)), int(bool(schedule)), *[float(v) for v in beta],
+                         float(theta))
         import ctypes
         _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))
 

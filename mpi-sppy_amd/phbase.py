@@ -30,7 +30,7 @@ from .spbase import SPBase
 # e.g. "mipgap" or "threads", belong to CPU solvers and are ignored)
 _SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": 32, "pdhg_keep_omega": False,
                     "pdhg_schedule": True, "pdhg_beta_sufficient": 0.0, "pdhg_beta_necessary": 0.0,
-                    "pdhg_beta_artificial": 0.0}
+                    "pdhg_beta_artificial": 0.0, "pdhg_primal_weight_theta": 0.0}
 
 
 class PHBase(SPBase):
@@ -195,7 +195,8 @@ class PHBase(SPBase):
                           check_every=o["pdhg_check_every"],
                           warm_start=(1 | (2 if o["pdhg_keep_omega"] else 0)) if warm_start else 0,
                           schedule=o["pdhg_schedule"],
-                          beta=(o["pdhg_beta_sufficient"], o["pdhg_beta_necessary"], o["pdhg_beta_artificial"]))
+                          beta=(o["pdhg_beta_sufficient"], o["pdhg_beta_necessary"], o["pdhg_beta_artificial"]),
+                          theta=o["pdhg_primal_weight_theta"])
         self.solve_count += self.engine.S
         # The launch is asynchronous: the statuses reach the host with the next convergence
         # readback (phg_solve_summary, checked in convergence_diff), so a PH iteration costs one
