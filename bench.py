@@ -108,12 +108,10 @@ def main():
     b = eng.batch
     S_loc = eng.S
 
-    def step():
-        ph.Compute_Xbar()
-        ph.Update_W()
-        conv = ph.convergence_diff()
-        ph.solve_loop(solver_options=ph.iterk_solver_options)
-        return conv
+    ph.current_solver_options = ph.iterk_solver_options
+
+    def step():   # one PH iteration k >= 1, as PHBase.iterk_loop runs it
+        return ph.update_and_solve()
 
     for _ in range(args.warmup):
         step()

@@ -92,6 +92,11 @@ typedef struct phg_opts {
      * (0, 1], <= 0 selects the default 0.8 (PDLP uses 0.5; 0.8 measured on MI355X: farmer
      * 10k +10 %, sslp 2048 +16 %, netdes 1024 -1 % solves/s)                                 */
     double  primal_weight_theta;
+    /* > 0: the solve is a device-side no-op when the convergence metric of the handle's last
+     * phg_conv_start is below this value (PH's "conv < convthresh: stop before solve_loop",
+     * phbase.py:1008-1010, decided on the device so the solve can be enqueued before conv is
+     * read back); 0: always solve                                                             */
+    double  skip_if_conv_below;
 } phg_opts;
 
 /* solve modes (mpisppy/phbase.py:670-760: W_on / prox_on toggles) */
@@ -171,6 +176,11 @@ int  phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* opt
 int  phg_node_sums(phg_handle* h, double* dev_nodesum);
 int  phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpart);
 int  phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_conv);
+/* phg_conv_finish split in two: phg_conv_start enqueues the conv computation (into the handle's
+ * device gate, read by predicated solves) and its copy to the host; phg_conv_wait blocks until
+ * that copy has landed -- work enqueued in between (the next solve) keeps the GPU busy         */
+int  phg_conv_start(phg_handle* h, const double* dev_convpart);
+int  phg_conv_wait(phg_handle* h, double* host_conv);
 /* status summary of the solve preceding the last PH update, read back by phg_conv_finish with the
  * convergence partials (dev_convpart[2P], [2P+1]; summed over GPUs by the same all-reduce):
  * out2 = {scenarios not at the KKT tolerance, scenarios with a numerical failure}            */

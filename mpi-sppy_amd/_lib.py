@@ -34,7 +34,8 @@ class PhgOpts(C.Structure):
     _fields_ = [("eps_rel", C.c_double), ("max_iter", C.c_int32), ("check_every", C.c_int32),
                 ("warm_start", C.c_int32), ("fix_nonants", C.c_int32), ("schedule", C.c_int32),
                 ("beta_sufficient", C.c_double), ("beta_necessary", C.c_double),
-                ("beta_artificial", C.c_double), ("primal_weight_theta", C.c_double)]
+                ("beta_artificial", C.c_double), ("primal_weight_theta", C.c_double),
+                ("skip_if_conv_below", C.c_double)]
 
 
 (F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART, F_OMEGA,
@@ -48,6 +49,8 @@ SIGNATURES = {
     "phg_last_error": (C.c_char_p, []),
     "phg_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "phg_set_presolve": (C.c_int, [C.c_void_p, C.c_int32]),
+    "phg_conv_start": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "phg_conv_wait": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     "phg_presolve_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "phg_sync": (C.c_int, [C.c_void_p]),
     "phg_set_layout": (C.c_int, [C.c_void_p, C.c_int32]),

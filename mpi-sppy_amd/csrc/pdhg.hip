@@ -26,6 +26,7 @@ __device__ __forceinline__ void wsum_many(double (&v)[K]) { gsum_many<64, K>(v);
 
 template <int CPL, int KCS, int RPL, int KRS, int D, int KD>
 __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
+    if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int s = a.order ? a.order[blockIdx.x] : blockIdx.x;
     const int l = threadIdx.x;

@@ -45,6 +45,7 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
 
 template <int NT, int CPL, int RPL, int PPT, int QPT>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
+    if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const BlockLayout& B = a.blk;
     const int t = threadIdx.x;

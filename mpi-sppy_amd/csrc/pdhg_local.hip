@@ -42,6 +42,7 @@ struct Cold {
 
 template <int LPS, int CPL, int RPL, int D>
 __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
+    if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
     constexpr int G = 64 / LPS;                    // scenarios per wave
     constexpr int DD = D > 0 ? D : 1;
     using CI = Cold<CPL, RPL, D>;

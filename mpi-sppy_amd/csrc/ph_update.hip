@@ -38,14 +38,41 @@ __device__ __forceinline__ bool last_workgroup(unsigned* counter) {
     return s_last != 0u;
 }
 
+// conv = (1/P) sum_v convpart[2v] / convpart[2v+1] (phbase.py:349-371; virtual ranks with no
+// nonants contribute 0), then the two status counts: gate = {conv, not optimal, NaN}.  The same
+// three values go to fine-grained pinned host memory followed (system-scope fences) by the
+// sequence number `seq` in gate_host[3]: the host polls that word, so no event has to pass
+// through the GPU's queue.  One 256-thread workgroup, fixed-order tree over the virtual ranks.
+__device__ void conv_gate_block(const double* convpart, int P, double* gate, double* gate_host, double seq) {
+    __shared__ double red[256];
+    double t = 0.0;
+    for (int v = threadIdx.x; v < P; v += 256)
+        if (convpart[2 * v + 1] > 0.0) t += convpart[2 * v] / convpart[2 * v + 1];
+    red[threadIdx.x] = t;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double g[3] = {red[0] / (double)P, convpart[2 * P], convpart[2 * P + 1]};
+        for (int i = 0; i < 3; ++i) gate[i] = g[i];
+        if (gate_host) {
+            for (int i = 0; i < 3; ++i) __hip_atomic_store(&gate_host[i], g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+            __hip_atomic_store(&gate_host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 // Node sums (first half of _Compute_Xbar).  One workgroup per node segment; thread t handles
 // nonant k = t % klen of scenarios s0 + t / klen + q*i (q = 256 / klen lanes per nonant) ->
 // coalesced rows of xN.  The last workgroup adds every node's segment partials in segment order:
 // nodesum[e] = sum p x, nodesum[N_tot + e] = sum p x^2 (the buffer the cross-GPU all-reduce sums).
 __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
     __shared__ double sh[2 * 256];
-    const NodeSeg sg = a.seg[blockIdx.x];
     const int tid = threadIdx.x;
+    const NodeSeg sg = a.seg[blockIdx.x];
     double* out = a.segpart + (long)blockIdx.x * 2 * a.maxk;
     for (int k0 = 0; k0 < sg.klen; k0 += 256) {
         const int kl = min(256, sg.klen - k0);
@@ -195,6 +222,10 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
             convpart[2 * a.P + 1] = (double)(bad[4] + bad[5] + bad[6] + bad[7]);
         }
     }
+    if (a.gate) {   // single GPU: nothing to all-reduce, finish convergence_diff here
+        __syncthreads();
+        conv_gate_block(convpart, a.P, a.gate, a.gate_host, a.gate_seq);
+    }
 }
 
 // per-scenario objective value with the current W / xbar / rho (pyo.value(objfct))
@@ -234,6 +265,17 @@ __global__ void broadcast_row_kernel(const double* row, int N, int S, double* ou
 hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hipStream_t st) {
     const long tot = (long)S * N;
     hipLaunchKernelGGL(broadcast_row_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, row, N, S, out);
+    return hipGetLastError();
+}
+
+__global__ void conv_gate_kernel(const double* __restrict__ convpart, int P, double* gate, double* gate_host,
+                                 double seq) {
+    conv_gate_block(convpart, P, gate, gate_host, seq);
+}
+
+hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double* gate_host, double seq,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(conv_gate_kernel, dim3(1), dim3(256), 0, st, convpart, P, gate, gate_host, seq);
     return hipGetLastError();
 }
 

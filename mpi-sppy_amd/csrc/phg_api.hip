@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -34,6 +35,9 @@ hipError_t piece_gather_launch(const double* vals, int nnz, const int* perm, int
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
 hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hipStream_t st);
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
+hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double* gate_host, double seq,
+                            hipStream_t st);
+constexpr int kSchedEvery = 4;
 hipError_t eval_obj_launch(int S, int n, int N, const double* x, const double* c, const double* obj_off,
                            const int* nonant_col, const double* xN, const double* W, const double* rho,
                            const double* xbar, const int* xidx, int w_on, int prox_on, double sense,
@@ -104,6 +108,14 @@ struct phg_handle {
     // singleton-row presolve (presolve_singletons): rows of the caller's batch -> kept rows
     int presolve = 1;
     int m_orig = 0;
+    // device-side convergence metric (phg_conv_start / phg_conv_wait, predicated solves)
+    double* gate = nullptr;          // device {conv, not optimal, NaN}
+    double* gate_host = nullptr;     // fine-grained pinned host copy + sequence word [3]
+    long long gate_seq = 0;          // sequence number of the last enqueued gate computation
+    bool gate_fused = false;         // the last phg_apply_xbar already computed the gate
+    // the launch schedule is recomputed after every kSchedEvery-th solve (iteration counts move
+    // slowly under warm starts; the sort is a latency-bound single-workgroup launch)
+    int solves = 0;
     std::vector<int> row_map;  // original row -> kept row, or -1 (folded into a column bound)
 };
 
@@ -166,6 +178,7 @@ void phg_destroy(phg_handle* h) {
     (void)hipStreamSynchronize(h->stream);
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->pinned) (void)hipHostFree(h->pinned);
+    if (h->gate_host) (void)hipHostFree(h->gate_host);
     for (auto& v : h->tev)
         for (auto& e : v) (void)hipEventDestroy(e);
     if (h->own_stream) (void)hipStreamDestroy(h->stream);
@@ -623,6 +636,9 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     a.xidx = h->xidx;
     if (dalloc(h, &h->nodesum, 2 * (size_t)b->N_tot)) return -1;
     if (dalloc(h, &h->convpart, 2 * (size_t)P + 2)) return -1;
+    if (dalloc(h, &h->gate, 4)) return -1;
+    CK(hipHostMalloc((void**)&h->gate_host, 4 * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
+    for (int i = 0; i < 4; ++i) h->gate_host[i] = 0.0;
     return 0;
 }
 
@@ -1146,14 +1162,17 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     if (timing_event(h, 0, 0)) return -1;
     a.loc = h->loc;
     a.blk = h->blk;
+    a.gate = o->skip_if_conv_below > 0 ? h->gate : nullptr;
+    a.gate_below = o->skip_if_conv_below;
     if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
     if (timing_event(h, 0, 1)) return -1;
-    if (o->schedule) {
+    if (o->schedule && (h->solves % kSchedEvery == 0 || !h->have_order)) {
         CK(schedule_launch(h->iters, h->S, a.check_every, h->order, h->stream));
         h->have_order = true;
     }
+    ++h->solves;
     return 0;
 }
 
@@ -1168,27 +1187,52 @@ int phg_node_sums(phg_handle* h, double* dev_nodesum) {
 int phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpart) {
     if (!h || !h->loaded) return fail("phg_apply_xbar: no batch loaded");
     CK(hipSetDevice(h->device));
-    CK(w_update_launch(h->ph, dev_nodesum ? dev_nodesum : h->nodesum,
+    PhArgs a = h->ph;
+    h->gate_fused = dev_convpart == nullptr;   // one GPU: the last workgroup finishes conv too
+    if (h->gate_fused) {
+        a.gate = h->gate;
+        a.gate_host = h->gate_host;
+        a.gate_seq = (double)(++h->gate_seq);
+    }
+    CK(w_update_launch(a, dev_nodesum ? dev_nodesum : h->nodesum,
                        dev_convpart ? dev_convpart : h->convpart, h->stream));
     if (timing_event(h, 1, 1)) return -1;
     return 0;
 }
 
-int phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_conv) {
-    if (!h || !h->loaded) return fail("phg_conv_finish: no batch loaded");
-    const size_t ncp = 2 * (size_t)h->P + 2;
-    if (!h->pinned) CK(hipHostMalloc((void**)&h->pinned, ncp * sizeof(double), hipHostMallocDefault));
-    double* cp = h->pinned;
-    CK(hipMemcpyAsync(cp, dev_convpart ? dev_convpart : h->convpart, ncp * sizeof(double),
-                      hipMemcpyDeviceToHost, h->stream));
-    CK(hipStreamSynchronize(h->stream));
-    double tot = 0.0;
-    for (int v = 0; v < h->P; ++v)
-        if (cp[2 * v + 1] > 0.0) tot += cp[2 * v] / cp[2 * v + 1];
-    *host_conv = tot / (double)h->P;
-    h->summary[0] = (int)cp[2 * (size_t)h->P];
-    h->summary[1] = (int)cp[2 * (size_t)h->P + 1];
+int phg_conv_start(phg_handle* h, const double* dev_convpart) {
+    if (!h || !h->loaded) return fail("phg_conv_start: no batch loaded");
+    CK(hipSetDevice(h->device));
+    if (!(h->gate_fused && dev_convpart == nullptr))   // after an all-reduce: a small kernel
+        CK(conv_gate_launch(dev_convpart ? dev_convpart : h->convpart, h->P, h->gate, h->gate_host,
+                            (double)(++h->gate_seq), h->stream));
+    h->gate_fused = false;
     return 0;
+}
+
+int phg_conv_wait(phg_handle* h, double* host_conv) {
+    if (!h || !h->loaded || h->gate_seq == 0) return fail("phg_conv_wait: no phg_conv_start pending");
+    // poll the sequence word the kernel stores last; every 2^16 polls make sure the stream has not
+    // failed (an error would otherwise leave us spinning)
+    volatile double* g = h->gate_host;
+    const double want = (double)h->gate_seq;
+    for (unsigned long spin = 1; g[3] != want; ++spin) {
+        if ((spin & 0xFFFF) == 0) {
+            const hipError_t e = hipStreamQuery(h->stream);
+            if (e != hipSuccess && e != hipErrorNotReady) return fail(std::string("phg_conv_wait: ") + hipGetErrorString(e));
+            if (e == hipSuccess && g[3] != want) return fail("phg_conv_wait: stream idle but no convergence value");
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    *host_conv = g[0];
+    h->summary[0] = (int)g[1];
+    h->summary[1] = (int)g[2];
+    return 0;
+}
+
+int phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_conv) {
+    if (phg_conv_start(h, dev_convpart)) return -1;
+    return phg_conv_wait(h, host_conv);
 }
 
 int phg_solve_summary(phg_handle* h, int32_t* out2) {

@@ -104,6 +104,12 @@ struct PdhgArgs {
     double eps, sense;
     double beta_suf, beta_nec, beta_art;   // restart rule
     double theta;                          // primal weight smoothing (1: no smoothing)
+    // predicated solve: when gate != nullptr and gate[0] (the convergence metric computed on the
+    // device by phg_conv_start) < gate_below, the launch is a no-op -- PH's "break before
+    // solve_loop when conv < convthresh" decided on the device, so the host can enqueue the solve
+    // before it has read conv back
+    const double* gate;
+    double gate_below;
 };
 
 struct PrepArgs {
@@ -160,7 +166,13 @@ struct PhArgs {
     const double* beta;     // [S*N]
     int smooth_on;
     unsigned* ticket;       // [2] last-workgroup counters of the two kernels (zeroed)
+    // single-GPU PH update: the last w_update workgroup also computes conv into gate (device, read
+    // by predicated solves) and gate_host (pinned host memory, read after the handle's event)
+    double* gate;
+    double* gate_host;
+    double gate_seq;
 };
+
 
 // PH terms of nonant t = s*N + k in the min-form subproblem objective (phbase.py:670-760):
 //   c += w_on W;  prox_on: c -= rho xbar (+ p z), q = rho (+ p), const += rho/2 xbar^2 (+ p/2 z^2)

@@ -199,10 +199,10 @@ class Engine:
 
     # ------------------------------------------------------------------ hot path
     def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=32, warm_start=3,
-              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0), theta=0.0):
+              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0), theta=0.0, skip_below=0.0):
         o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(warm_start),
                          int(bool(fix_nonants)), int(bool(schedule)), *[float(v) for v in beta],
-                         float(theta))
+                         float(theta), float(skip_below))
         import ctypes
         _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))
 
@@ -217,6 +217,16 @@ class Engine:
         ns = None if self.exchange is None else self.exchange[0].data_ptr()
         cp = None if self.exchange is None else self.exchange[1].data_ptr()
         _lib.check(self.lib.phg_apply_xbar(self.h, ns, cp))
+
+    def conv_start(self):
+        cp = None if self.exchange is None else self.exchange[1].data_ptr()
+        _lib.check(self.lib.phg_conv_start(self.h, cp))
+
+    def conv_wait(self):
+        import ctypes
+        v = ctypes.c_double()
+        _lib.check(self.lib.phg_conv_wait(self.h, ctypes.byref(v)))
+        return v.value
 
     def conv_finish(self):
         import ctypes

@@ -176,8 +176,10 @@ class PHBase(SPBase):
     # ------------------------------------------------------------------------------- solves
     def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,
                    dis_W=False, dis_prox=False, gripe=False, disable_pyomo_signal_handling=False,
-                   tee=False, verbose=False, need_solution=True, warm_start=True):
-        """``phbase.py:522-603`` + ``spopt.py:250-341``: one batched launch for all local scenarios."""
+                   tee=False, verbose=False, need_solution=True, warm_start=True, skip_below=0.0):
+        """``phbase.py:522-603`` + ``spopt.py:250-341``: one batched launch for all local scenarios.
+        skip_below > 0 makes the launch a device-side no-op when the conv of the last
+        ``engine.conv_start`` is below it (see :meth:`update_and_solve`)."""
         saved = (self.W_on, self.prox_on)
         if dis_W:
             self._disable_W()
@@ -196,7 +198,7 @@ class PHBase(SPBase):
                           warm_start=(1 | (2 if o["pdhg_keep_omega"] else 0)) if warm_start else 0,
                           schedule=o["pdhg_schedule"],
                           beta=(o["pdhg_beta_sufficient"], o["pdhg_beta_necessary"], o["pdhg_beta_artificial"]),
-                          theta=o["pdhg_primal_weight_theta"])
+                          theta=o["pdhg_primal_weight_theta"], skip_below=skip_below)
         self.solve_count += self.engine.S
         # The launch is asynchronous: the statuses reach the host with the next convergence
         # readback (phg_solve_summary, checked in convergence_diff), so a PH iteration costs one
@@ -260,6 +262,40 @@ class PHBase(SPBase):
             self.mpicomm.allreduce_sum_(self.engine.exchange[1])
         conv = self.engine.conv_finish()
         self._check_status_summary()
+        return conv
+
+    def _can_pipeline(self):
+        """The pipelined iteration (:meth:`update_and_solve`) enqueues the solve before the host
+        has seen conv, so nothing may act between convergence_diff and solve_loop: no extension
+        (miditer), no converger object, no time limit, no per-solve timing."""
+        o = self.options
+        return (self.extobject is None and self.ph_converger is None and o.get("time_limit") is None
+                and not o.get("display_timing", False) and o.get("pdhg_pipeline", True))
+
+    def update_and_solve(self, verbose=False):
+        """One PH iteration k >= 1 -- Compute_Xbar, Update_W, convergence_diff and, unless
+        conv < convthresh, solve_loop (``phbase.py:990-1035``) -- with one host synchronisation that
+        overlaps the solve: conv is computed on the device, the solve is enqueued gated on it
+        (``phg_opts.skip_if_conv_below``: a no-op when PH has converged, exactly the reference's
+        break before solve_loop), and only then does the host wait for conv.  Returns conv."""
+        self.Compute_Xbar(verbose)
+        self.Update_W(verbose)
+        if self.engine.exchange is not None:
+            self.mpicomm.allreduce_sum_(self.engine.exchange[1])
+        self.engine.conv_start()
+        pending = getattr(self, "_status_pending", None)
+        thr = float(self.options["convthresh"])
+        self.solve_loop(solver_options=self.current_solver_options, gripe=verbose, verbose=verbose,
+                        skip_below=thr if thr > 0 else 0.0)
+        launched = self._status_pending
+        self._status_pending = pending
+        conv = self.engine.conv_wait()
+        self._check_status_summary()          # statuses of the PREVIOUS solve, as convergence_diff
+        if conv < thr:                        # the gated solve did nothing on the device
+            self.solve_count -= self.engine.S
+            self._status_pending = None
+        else:
+            self._status_pending = launched
         return conv
 
     # ------------------------------------------------------------------------------- expectations
@@ -405,11 +441,15 @@ class PHBase(SPBase):
         self.conv = None
         max_iterations = int(self.options["PHIterLimit"])
         self.conv_history = []
+        pipelined = self._can_pipeline()
         for self._PHIter in range(1, max_iterations + 1):
             iteration_start_time = time.time()
-            self.Compute_Xbar(verbose)
-            self.Update_W(verbose)
-            self.conv = self.convergence_diff()
+            if pipelined:   # same statements, the solve already enqueued (gated on conv)
+                self.conv = self.update_and_solve(verbose)
+            else:
+                self.Compute_Xbar(verbose)
+                self.Update_W(verbose)
+                self.conv = self.convergence_diff()
             self.conv_history.append(self.conv)
             if self.extobject is not None:
                 self.extobject.miditer()
@@ -423,8 +463,9 @@ class PHBase(SPBase):
                     over = self.mpicomm.allreduce_scalar(float(over)) > 0
                 if over:
                     break
-            self.solve_loop(solver_options=self.current_solver_options, dtiming=self.options["display_timing"],
-                            gripe=verbose, verbose=verbose)
+            if not pipelined:
+                self.solve_loop(solver_options=self.current_solver_options, dtiming=self.options["display_timing"],
+                                gripe=verbose, verbose=verbose)
             if self.extobject is not None:
                 self.extobject.enditer()
             if self.spcomm is not None:

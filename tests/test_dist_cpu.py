@@ -56,7 +56,9 @@ class NumpyEngine:
     def sync(self):
         pass
 
-    def solve(self, w_on, prox_on, **kw):
+    def solve(self, w_on, prox_on, skip_below=0.0, **kw):
+        if skip_below > 0 and getattr(self, "_gate", None) is not None and self._gate < skip_below:
+            return                    # predicated solve (phg_opts.skip_if_conv_below)
         b = self.batch
         X = []
         for s in range(self.S):
@@ -109,6 +111,12 @@ class NumpyEngine:
     def conv_finish(self):
         cp = self.exchange[1].numpy()
         return sum(cp[2 * v] / cp[2 * v + 1] for v in range(self.P) if cp[2 * v + 1] > 0) / self.P
+
+    def conv_start(self):             # phg_conv_start: conv into the device gate
+        self._gate = self.conv_finish()
+
+    def conv_wait(self):
+        return self._gate
 
     def eval_objective(self, w_on, prox_on):
         return self.obj.copy()

@@ -275,3 +275,20 @@ def test_singleton_row_presolve_same_solutions():
     m = farmer.scenario_creator("scen0", crops_multiplier=2, num_scens=5)
     folded = [i for i, r in enumerate(m._rows) if len(r[0]) == 1]
     assert len(folded) == 6 and np.all(y1[:, folded] == 0.0)
+
+
+# ----------------------------------------------------------------------------- pipelined PH loop
+def test_pipelined_iteration_matches_sequential():
+    """PHBase.update_and_solve (solve enqueued gated on the device conv, phg_conv_start/wait) runs
+    the same PH as the sequential Compute_Xbar / Update_W / convergence_diff / solve_loop loop,
+    including the break before solve_loop at conv < convthresh (the gated solve is a no-op)."""
+    out = []
+    for pipe in (True, False):
+        ph = _farmer_ph(4, cm=1, PHIterLimit=200, convthresh=1e-3, pdhg_pipeline=pipe)
+        conv, eobj, tb = ph.ph_main()
+        out.append((ph._PHIter, conv, eobj, ph.conv_history, ph.Ws().copy(), ph.xbars().copy(),
+                    ph.nonants().copy(), ph.solve_count))
+    (i1, c1, e1, h1, W1, x1, n1, k1), (i0, c0, e0, h0, W0, x0, n0, k0) = out
+    assert i1 == i0 < 200 and c1 < 1e-3
+    assert h1 == h0 and c1 == c0 and e1 == e0 and k1 == k0
+    assert np.array_equal(W1, W0) and np.array_equal(x1, x0) and np.array_equal(n1, n0)
