@@ -6,6 +6,17 @@ engine, for
   * "hal" : reflected restarted Halpern PDHG (Lu & Yang 2024; cuPDLPx): z+ = k+1/k+2 ((1+g) T(z) -
             g z) + 1/k+2 z0, restarts on the fixed-point residual, restart to T(z).
 Usage: python tools/pdhg_algo_lab.py [S] [cm] [ph_iters] [variant ...]
+(LAB_PRESOLVE=1: fold singleton rows into bounds first, as phg_load_batch does.)
+
+Findings kept for the record (farmer cm=10, 100 scenarios, 30 PH iterations, eps 1e-9):
+  * singleton-row presolve: 594 -> 369 mean PDHG iterations per solve (adopted);
+  * primal weight smoothing theta 0.5 -> 0.8: 369 -> 322 (adopted, confirmed on MI355X);
+  * carrying the primal weight across PH iterations (keepw=1): 322 -> 257 here, but on the GPU
+    the 10k-scenario PH then stalls (conv 4e-4 after 2 489 PH iterations vs converged at 5 185 in
+    1.4 s): not adopted;
+  * restart to the current iterate only (noavg=1): +2 % iterations here, but 136 of 10 000
+    scenarios hit the iteration cap late in a long PH run on the GPU: not adopted;
+  * Halpern / reflected Halpern ("hal"): 20-110 % more iterations: not adopted.
 """
 import os
 import sys
@@ -83,7 +94,8 @@ class Lab:
                        + (pobj - dobj) ** 2)
 
     # ------------------------------------------------------------------ one solve
-    def solve(self, c, q, x0, y0, variant="ra", gamma=1.0, bs=0.2, bnec=0.8, ba=0.36, th=0.5, noavg=0.0):
+    def solve(self, c, q, x0, y0, variant="ra", gamma=1.0, bs=0.2, bnec=0.8, ba=0.36, th=0.5, noavg=0.0,
+              keepw=0.0):
         b = self.b
         S = b.S
         dc, dr = self.dc, self.dr
@@ -99,6 +111,8 @@ class Lab:
         cn = np.sqrt(seg_sum(cs * cs, b.sc, S))
         bn = np.sqrt(seg_sum(np.where(np.isfinite(rl), rl, 0) ** 2 + np.where(np.isfinite(ru), ru, 0) ** 2, b.sr, S))
         omega = np.where((cn > 1e-10) & (bn > 1e-10), cn / np.maximum(bn, 1e-300), 1.0)
+        if keepw and getattr(self, "_omega_prev", None) is not None:
+            omega = self._omega_prev if keepw == 1.0 else np.sqrt(self._omega_prev * omega)
         done = np.zeros(S, bool)
         iters = np.zeros(S, int)
         xr, yr = x.copy(), y.copy()
@@ -191,6 +205,7 @@ class Lab:
                 Ax, ATy = A @ x, AT @ y
         xout = np.where(done[b.sc], xout, x)
         yout = np.where(done[b.sr], yout, y)
+        self._omega_prev = omega
         return xout * dc, yout * dr, iters
 
 
