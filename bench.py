@@ -157,7 +157,9 @@ def main():
     ms_per_step = el / args.steps * 1e3
 
     # roofline of the dominant kernel (batched PDHG), per launch, from HIP events on its stream
-    f_it = pdhg_flops_per_iter(b.n, b.m, b.nnz)
+    # on the problem the solver runs: singleton rows folded into bounds (one nonzero each) by
+    # phg_load_batch's presolve are not part of an iteration
+    f_it = pdhg_flops_per_iter(b.n, b.m - eng.rows_folded, b.nnz - eng.rows_folded)
     flops_per_launch = f_it * pdhg_iters / args.steps
     avg_launch_s = pdhg_ms / args.steps / 1e3
     achieved_tf = flops_per_launch / avg_launch_s / 1e12
@@ -166,7 +168,8 @@ def main():
     nnz_distinct = int((b.vals != b.vals[0]).any(axis=0).sum()) if b.S > 1 else 0
     c_var = bool((b.c != b.c[0]).any()) or True     # PH terms make every scenario's cost differ
     b_var = bool((b.rl != b.rl[0]).any() or (b.ru != b.ru[0]).any())
-    bytes_it = 16 * nnz_distinct + 16 * b.n + 16 * b.m + 8 * (b.n * c_var + b.m * b_var)
+    m_run = b.m - eng.rows_folded
+    bytes_it = 16 * nnz_distinct + 16 * b.n + 16 * m_run + 8 * (b.n * c_var + m_run * b_var)
     achieved_gbs = bytes_it * pdhg_iters / args.steps / avg_launch_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
