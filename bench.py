@@ -43,7 +43,9 @@ def parse():
     ap.add_argument("--check-every", type=int, default=32, help="PDHG restart/termination check interval")
     ap.add_argument("--beta-art", type=float, default=0.0, help="artificial restart fraction (0: default)")
     ap.add_argument("--theta", type=float, default=0.0, help="primal weight smoothing (0: default)")
-    ap.add_argument("--keep-omega", action="store_true", help="carry PDHG primal weights across PH iterations")
+    ap.add_argument("--keep-omega", default="blend", choices=["fresh", "carry", "blend"],
+                    help="PDHG primal weight at each solve: fresh estimate, the previous solve's, or "
+                         "their geometric mean (default)")
     ap.add_argument("--no-presolve", action="store_true", help="keep singleton rows as rows")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
@@ -96,7 +98,7 @@ def main():
             "convthresh": 1e-4, "verbose": False, "display_progress": False, "pdhg_layout": args.layout,
             "pdhg_schedule": not args.no_schedule, "pdhg_check_every": args.check_every,
             "pdhg_beta_artificial": args.beta_art, "pdhg_primal_weight_theta": args.theta, "pdhg_presolve": not args.no_presolve,
-            "pdhg_keep_omega": args.keep_omega,
+            "pdhg_keep_omega": {"fresh": False, "carry": True, "blend": "blend"}[args.keep_omega],
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps}}
     t_setup = time.perf_counter()
     ph = PH(dict(opts), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw)

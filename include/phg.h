@@ -78,7 +78,8 @@ typedef struct phg_opts {
     double  eps_rel;       /* relative KKT tolerance (PDLP-style), e.g. 1e-9            */
     int32_t max_iter;      /* PDHG iteration limit per scenario                         */
     int32_t check_every;   /* iterations between restart/termination checks (e.g. 64)   */
-    int32_t warm_start;    /* bit 0: start from the previous x, y; bit 1: keep its primal weight */
+    int32_t warm_start;    /* bit 0: start from the previous x, y; bit 1: keep its primal weight;
+                              bit 2: start from sqrt(previous x fresh) primal weight          */
     int32_t fix_nonants;   /* 1: nonants fixed to the values set by phg_set_fixed (xhat) */
     int32_t schedule;      /* 1: launch scenarios heaviest-first by the previous solve's PDHG
                               iteration counts (device counting sort after each solve)       */

@@ -198,6 +198,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
         wsum_many<2>(rr);
         const double cn = sqrt(rr[0]), bn = sqrt(rr[1]);
         omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
+        if ((a.warm & 4) && a.omega[s] > 0.0) omega = sqrt(omega * a.omega[s]);   // blend
     }
     double tau = eta / omega, sig = eta * omega;
 

@@ -197,6 +197,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         const double cn_ = sqrt(rr[2]), bn = sqrt(rr[3]);
         omega = (cn_ > 1e-10 && bn > 1e-10) ? cn_ / bn : 1.0;
         if ((a.warm & 2) && a.omega[s] > 0.0) omega = a.omega[s];
+        else if ((a.warm & 4) && a.omega[s] > 0.0) omega = sqrt(omega * a.omega[s]);
     }
     const double bnorm = a.bnorm[s];
     const double eta = a.eta[s];

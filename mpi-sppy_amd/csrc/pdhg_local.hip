@@ -213,6 +213,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
         omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
         if ((a.warm & 2) && a.omega[s] > 0.0) omega = a.omega[s];
+        else if ((a.warm & 4) && a.omega[s] > 0.0) omega = sqrt(omega * a.omega[s]);   // blend
     }
     const double eta = a.eta[s];
     CS(CI::SC + CI::BNORM) = a.bnorm[s];

@@ -28,7 +28,16 @@ from .spbase import SPBase
 
 # PDHG controls read from iter0_solver_options / iterk_solver_options (other solver options,
 # e.g. "mipgap" or "threads", belong to CPU solvers and are ignored)
-_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": 32, "pdhg_keep_omega": False,
+def _omega_bits(keep):
+    """pdhg_keep_omega: False re-initialises the primal weight every solve, True carries it over
+    (phg_opts.warm_start bit 1), "blend" starts from the geometric mean of the carried and the fresh
+    estimate (bit 2)."""
+    if keep == "blend":
+        return 4
+    return 2 if keep else 0
+
+
+_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": 32, "pdhg_keep_omega": "blend",
                     "pdhg_schedule": True, "pdhg_beta_sufficient": 0.0, "pdhg_beta_necessary": 0.0,
                     "pdhg_beta_artificial": 0.0, "pdhg_primal_weight_theta": 0.0}
 
@@ -195,7 +204,7 @@ class PHBase(SPBase):
         t0 = time.perf_counter()
         self.engine.solve(w_on, prox_on, eps=o["pdhg_eps"], max_iter=o["pdhg_max_iter"],
                           check_every=o["pdhg_check_every"],
-                          warm_start=(1 | (2 if o["pdhg_keep_omega"] else 0)) if warm_start else 0,
+                          warm_start=(1 | _omega_bits(o["pdhg_keep_omega"])) if warm_start else 0,
                           schedule=o["pdhg_schedule"],
                           beta=(o["pdhg_beta_sufficient"], o["pdhg_beta_necessary"], o["pdhg_beta_artificial"]),
                           theta=o["pdhg_primal_weight_theta"], skip_below=skip_below)
