@@ -65,9 +65,47 @@ __device__ void conv_gate_block(const double* convpart, int P, double* gate, dou
     }
 }
 
-// Node sums (first half of _Compute_Xbar).  One workgroup per node segment; thread t handles
-// nonant k = t % klen of scenarios s0 + t / klen + q*i (q = 256 / klen lanes per nonant) ->
-// coalesced rows of xN.  The last workgroup adds every node's segment partials in segment order:
+// "Last K workgroups" hand-off: as last_workgroup, but the K workgroups that arrive last all
+// return a rank r in [0, K) (the others -1) once EVERY workgroup has arrived, so a final reduction
+// too large for one workgroup is split K ways by rank -- deterministic, since the work of rank r
+// does not depend on which workgroup holds it.  The K ranked workgroups spin only on arrivals of
+// workgroups that are already running (K is far below the resident capacity).  finish_k() re-arms
+// the counters for the next launch once all K are done.
+__device__ __forceinline__ int last_k_workgroups(unsigned* counter, int K) {
+    __shared__ int s_rank;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int rank = (int)prev - ((int)gridDim.x - K);
+        if (rank >= 0) {
+            while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x)
+                __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        s_rank = rank;
+    }
+    __syncthreads();
+    return s_rank;
+}
+
+__device__ __forceinline__ void finish_k(unsigned* counter, unsigned* done, int K) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)K - 1) {
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// Node sums (first half of _Compute_Xbar).  One workgroup per node segment (a contiguous scenario
+// range inside one node, sized on the host so that large batches get ~512 segments per level);
+// thread t handles nonant k = t % klen of scenarios s0 + t / klen + q*i (q = 256 / klen lanes per
+// nonant) -> coalesced rows of xN, 4 rows in flight per thread.  The last K workgroups then add
+// every node's segment partials in segment order (element range split K ways):
 // nodesum[e] = sum p x, nodesum[N_tot + e] = sum p x^2 (the buffer the cross-GPU all-reduce sums).
 __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
     __shared__ double sh[2 * 256];
@@ -82,12 +120,28 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
         double s1 = 0.0, s2 = 0.0;
         if (so < q) {
             const int kg = sg.kofs + k0 + k;
-            for (int s = sg.s0 + so; s < sg.s1; s += q) {
-                const double xv = a.xN[(long)s * a.N + kg];
-                const double p = a.pcv ? a.pcv[(long)s * a.N + kg] : a.pc[(long)s * a.L + sg.level];
-                s1 += p * xv;
-                s2 += p * xv * xv;
+            auto px = [&](int s, double& p, double& xv) {
+                xv = a.xN[(long)s * a.N + kg];
+                p = a.pcv ? a.pcv[(long)s * a.N + kg] : a.pc[(long)s * a.L + sg.level];
+            };
+            int s = sg.s0 + so;
+            // four independent rows per step (fixed pairing: deterministic), then the remainder
+            double t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
+            for (; s + 3 * q < sg.s1; s += 4 * q) {
+                double p[4], xv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) px(s + u * q, p[u], xv[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) { t1[u] += p[u] * xv[u]; t2[u] += p[u] * xv[u] * xv[u]; }
             }
+            for (; s < sg.s1; s += q) {
+                double p, xv;
+                px(s, p, xv);
+                t1[0] += p * xv;
+                t2[0] += p * xv * xv;
+            }
+            s1 = (t1[0] + t1[1]) + (t1[2] + t1[3]);
+            s2 = (t2[0] + t2[1]) + (t2[2] + t2[3]);
         }
         sh[tid] = s1;
         sh[256 + tid] = s2;
@@ -100,18 +154,22 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
         }
         __syncthreads();
     }
-    if (!last_workgroup(a.ticket)) return;
-    // T lanes per node element (power of two <= 64), each summing every T-th segment of the node,
-    // then a fixed xor-butterfly over the T lanes: wide enough to hide the L2 latency when N_tot is
-    // small, one lane per element when it is large
+    const int K = min(a.n_final, (int)gridDim.x);
+    const int rank = last_k_workgroups(a.ticket, K);
+    if (rank < 0) return;
+    // elements [e_lo, e_hi) of this rank; T lanes per element (power of two <= 64), each summing
+    // every T-th segment of the node, then a fixed xor-butterfly over the T lanes: wide enough to
+    // hide the L2 latency when there are few elements per rank, one lane per element otherwise
+    const int e_lo = (int)((long)a.N_tot * rank / K), e_hi = (int)((long)a.N_tot * (rank + 1) / K);
+    const int ne = e_hi - e_lo;
     int T = 1;
-    while (T < 64 && T * 2 * a.N_tot <= 256) T *= 2;
+    while (T < 64 && T * 2 * ne <= 256) T *= 2;
     const int E = 256 / T;
     const int sub = tid % T;
-    for (int e0 = 0; e0 < a.N_tot; e0 += E) {
+    for (int e0 = e_lo; e0 < e_hi; e0 += E) {
         const int e = e0 + tid / T;
         double t1 = 0.0, t2 = 0.0;
-        if (e < a.N_tot) {
+        if (e < e_hi) {
             // node g with node_off[g] <= e < node_off[g] + level_len[level[g]]
             int lo = 0, hi = a.n_nodes - 1;
             while (lo < hi) {
@@ -129,11 +187,12 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
             t1 += __shfl_xor(t1, o, 64);
             t2 += __shfl_xor(t2, o, 64);
         }
-        if (e < a.N_tot && sub == 0) {
+        if (e < e_hi && sub == 0) {
             nodesum[e] = t1;
             nodesum[a.N_tot + e] = t2;
         }
     }
+    finish_k(a.ticket, a.ticket + 2, K);
 }
 
 // fixed-order sum of v[first..last) by all 256 threads of the workgroup (same result in every thread)
@@ -163,15 +222,29 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
     const int s0 = a.cseg_s0[b], s1 = a.cseg_s1[b];
     const long e0 = (long)s0 * a.N, e1 = (long)s1 * a.N;
     double acc = 0.0;
-    for (long e = e0 + tid; e < e1; e += 256) {
-        const double xv = a.xN[e];
-        const double xb = nodesum[a.xidx[e]];
+    auto upd = [&](long e, double xv, double xb, double w, double r) {
         const double d = xv - xb;
         // variable probability: W of a zero-probability nonant stays 0 (prob0_mask)
-        a.W[e] = (a.pcv && a.pcv[e] == 0.0) ? 0.0 : a.W[e] + a.rho[e] * d;
-        acc += fabs(d);
+        a.W[e] = (a.pcv && a.pcv[e] == 0.0) ? 0.0 : w + r * d;
         if (a.smooth_on) a.Z[e] += a.beta[e] * (xv - a.Z[e]);   // Update_z (smoothed PH)
+        return fabs(d);
+    };
+    long e = e0 + tid;
+    // four elements in flight per thread (all loads before the stores), then the remainder
+    for (; e + 3 * 256 < e1; e += 4 * 256) {
+        double xv[4], xb[4], w[4], r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long f = e + u * 256;
+            xv[u] = a.xN[f];
+            xb[u] = nodesum[a.xidx[f]];
+            w[u] = a.W[f];
+            r[u] = a.rho[f];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += upd(e + u * 256, xv[u], xb[u], w[u], r[u]);
     }
+    for (; e < e1; e += 256) acc += upd(e, a.xN[e], nodesum[a.xidx[e]], a.W[e], a.rho[e]);
     int nb = 0, nn = 0;
     if (a.status)
         for (int s = s0 + tid; s < s1; s += 256) {

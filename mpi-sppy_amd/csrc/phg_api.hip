@@ -537,7 +537,8 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
         const int klen = b->level_len[lv];
         // ~8 scenarios per thread of a 256-thread workgroup: enough workgroups to hide the load
         // latency at small S, whole-row coalesced streaming at large S
-        const int chunk = klen >= 256 ? 8 : 8 * (256 / std::max(1, klen));
+        // and at most ~512 segments per level, so the final per-node sums stay short at large S
+        const int chunk = std::max(klen >= 256 ? 8 : 8 * (256 / std::max(1, klen)), (S + 511) / 512);
         int s = 0;
         while (s < S) {
             const int g = b->scen_node[s * L + lv];
@@ -570,7 +571,8 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
         }
     }
     std::vector<int> cv, cs0, cs1, vfirst(P + 1, 0);
-    const int cchunk = std::max(1, 2048 / std::max(1, N));   // ~8 elements per thread
+    // ~8 elements per thread, at most ~1024 segments
+    const int cchunk = std::max(std::max(1, 2048 / std::max(1, N)), (S + 1023) / 1024);
     {
         int s = 0;
         std::vector<std::vector<int>> tmp0(P), tmp1(P);
@@ -601,6 +603,12 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     a.S = S; a.N = N; a.N_tot = b->N_tot; a.L = L; a.P = P; a.maxk = maxk; a.n_nodes = b->n_nodes;
     a.n_seg = (int)segs.size();
     a.n_cseg = (int)cv.size();
+    {   // final node-sum reduction: ~64K partial loads per workgroup, at most 16 workgroups
+        long loads = 0;
+        for (int g = 0; g < b->n_nodes; ++g)
+            loads += 2L * (first[g + 1] - first[g]) * b->level_len[node_level[g]];
+        a.n_final = (int)std::min<long>(16, std::max<long>(1, (loads + 65535) / 65536));
+    }
     {
         NodeSeg* p;
         if (dput(h, &p, segs.data(), segs.size())) return -1;
@@ -628,7 +636,7 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     if (dalloc(h, &ip, 2 * cv.size())) return -1; a.csegbad = ip;
     {
         unsigned* t;
-        if (dalloc(h, &t, 2)) return -1;
+        if (dalloc(h, &t, 3)) return -1;
         a.ticket = t;
     }
     if (dput(h, &ip, vfirst.data(), vfirst.size())) return -1; a.vr_first = ip;

@@ -165,7 +165,8 @@ struct PhArgs {
     double* Z;              // [S*N] smoothing centre (Update_z, phbase.py:329-346), when smooth_on
     const double* beta;     // [S*N]
     int smooth_on;
-    unsigned* ticket;       // [2] last-workgroup counters of the two kernels (zeroed)
+    unsigned* ticket;       // [3] last-workgroup counters of the two kernels + node_sums' done count
+    int n_final;            // workgroups sharing node_sums' final reduction (last_k_workgroups)
     // single-GPU PH update: the last w_update workgroup also computes conv into gate (device, read
     // by predicated solves) and gate_host (pinned host memory, read after the handle's event)
     double* gate;

@@ -1,0 +1,116 @@
+"""HBM roofline sweep of the fused PH update ("report a sweep S*N in {1e6, 1e7, 1e8}
+for the >= 60 % claim").
+
+A synthetic two-stage batch -- S scenarios with N nonants each, one dense row (sum x <= N) -- is
+loaded through the C ABI (no solves), the nonants are set to seeded random values, and
+node_sums + W update + conv (phg_node_sums / phg_apply_xbar / phg_conv_start+wait) are timed with
+the library's HIP events over R repetitions.  Algorithmic bytes per update:
+8 S N (x read, W read, W write, rho read) + 8 S + 16 N_tot.  The result is checked on the host
+(xbar = mean of the nonants, W = rho (x - xbar)) before timing.
+
+Usage: python tools/ph_update_sweep.py [OUT_JSON]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import _pkg  # noqa: E402
+
+_pkg.load()
+from mpisppy_amd import _lib  # noqa: E402
+from mpisppy_amd.engine import BatchArrays, Engine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def synthetic_batch(S, N):
+    b = BatchArrays.__new__(BatchArrays)
+    n, m = N, 1
+    b.S, b.n, b.m, b.nnz = S, n, m, N
+    b.rowptr = np.array([0, N], np.int32)
+    b.colidx = np.arange(N, dtype=np.int32)
+    b.vals = np.ones((S, N))
+    b.c = np.ones((S, n))
+    b.cl, b.cu = np.zeros((S, n)), np.full((S, n), 10.0)
+    b.rl, b.ru = np.full((S, m), -np.inf), np.full((S, m), float(N))
+    b.off = np.zeros(S)
+    b.sense = 1
+    b.L = 1
+    b.level_len = np.array([N], np.int32)
+    b.nonant_col = np.arange(N, dtype=np.int32)
+    b.N = N
+    b.nonant_level = np.zeros(N, np.int32)
+    b.nonant_pos = np.arange(N, dtype=np.int32)
+    b.all_nodenames = ["ROOT"]
+    b.node_off = np.zeros(1, np.int32)
+    b.N_tot = N
+    b.scen_node = np.zeros((S, 1), np.int32)
+    b.prob = np.full(S, 1.0 / S)
+    b.prob_coeff = np.full((S, 1), 1.0 / S)
+    b.prob_coeff_var = None
+    b.scen_global0, b.S_global, b.virt_nproc = 0, S, 1
+    return b
+
+
+def run(S, N, reps=20):
+    import torch
+    t0 = time.perf_counter()
+    eng = Engine(synthetic_batch(S, N), device=torch.cuda.current_device(), presolve=False)
+    rng = np.random.default_rng(1134)
+    x = rng.uniform(0.0, 10.0, size=S * N)
+    eng.set(_lib.F_XN, x)
+    eng.set(_lib.F_RHO, 1.0)
+    setup = time.perf_counter() - t0
+    # correctness on the first update
+    eng.node_sums()
+    eng.apply_xbar()
+    eng.conv_start()
+    conv = eng.conv_wait()
+    xb = eng.get(_lib.F_XBAR)
+    X = x.reshape(S, N)
+    xb_host = (X / S).sum(0)
+    err_xbar = float(np.abs(xb - xb_host).max() / max(1.0, np.abs(xb_host).max()))
+    W = eng.get(_lib.F_W).reshape(S, N)
+    err_w = float(np.abs(W - (X - xb[None, :])).max())
+    conv_host = float(np.abs(X - xb[None, :]).mean())
+    ok = err_xbar < 1e-12 and err_w < 1e-9 and abs(conv - conv_host) <= 1e-9 * max(1.0, conv_host)
+    # timed updates (HIP events on the library's stream, PH updates only)
+    eng.timing_reset(solves=False, updates=True)
+    for _ in range(reps):
+        eng.node_sums()
+        eng.apply_xbar()
+        eng.conv_start()
+        eng.conv_wait()
+    ms, n_upd, _ = eng.timing(1)
+    eng.timing_reset(solves=False, updates=False)
+    eng.close()
+    avg_s = ms / n_upd / 1e3
+    alg = 8 * S * N * 4 + 8 * S + 16 * N
+    gbs = alg / avg_s / 1e9
+    return {"S": S, "N": N, "SN": S * N, "avg_us": round(avg_s * 1e6, 2), "bytes_per_update": alg,
+            "achieved_GBs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4), "updates": n_upd,
+            "check_ok": bool(ok), "err_xbar": err_xbar, "err_w": err_w, "setup_s": round(setup, 2)}
+
+
+def main():
+    import torch
+    torch.cuda.set_device(0)
+    out = []
+    for S, N in ((10000, 100), (100000, 100), (100000, 1000)):
+        r = run(S, N)
+        print(json.dumps(r), flush=True)
+        out.append(r)
+    if len(sys.argv) > 1:
+        json.dump({"kernel": "node_sums_kernel + w_update_kernel (+ fused conv gate)",
+                   "bytes_formula": "8*S*N*4 + 8*S + 16*N_tot (SURVEY 8(d)3)",
+                   "timing": "HIP events on the library stream around each update (phg_timing(1))",
+                   "results": out}, open(sys.argv[1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
