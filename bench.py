@@ -26,11 +26,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--case", default="farmer", choices=["farmer", "sslp", "netdes"],
+    ap.add_argument("--case", default="farmer", choices=["farmer", "sslp", "netdes", "hydro"],
                     help="workload: farmer (the BASELINE.json headline, configs[1]), sslp_15_45_10 or "
-                         "netdes network-50-30-H-01 LP relaxations (configs[2], configs[4])")
+                         "netdes network-50-30-H-01 LP relaxations (configs[2], configs[4]), or a "
+                         "non-uniform 3-stage hydro tree (configs[3], SURVEY 8(d) M3)")
     ap.add_argument("--scen", type=int, default=None,
-                    help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes")
+                    help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes, 2000 hydro")
     ap.add_argument("--cm", type=int, default=10)
     ap.add_argument("--rho", type=float, default=1.0)
     ap.add_argument("--eps", type=float, default=1e-9)
@@ -67,23 +68,31 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    # one GPU per rank; PHG_DIST_BACKEND=gloo (CPU-staged all-reduces) lets tests put several ranks
+    # on one device -- the production path is nccl (= RCCL over xGMI)
+    backend = os.environ.get("PHG_DIST_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
+    torch.cuda.set_device(device)
     comm = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(f"cuda:{local_rank}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(f"cuda:{device}"))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     import _pkg
     _pkg.load()
     from mpisppy_amd import _lib
     from mpisppy_amd.comm import TorchComm
-    from mpisppy_amd.examples import farmer, netdes, sslp
+    from mpisppy_amd.examples import farmer, hydro, netdes, sslp
     from mpisppy_amd.ph import PH
     if world > 1:
         comm = TorchComm()
 
     if args.scen is None:
-        args.scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024}[args.case]
+        args.scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024, "hydro": 2000}[args.case]
     S = args.scen * world
+    nodenames = None
     if args.case == "farmer":
         names, creator = farmer.scenario_names_creator(S), farmer.scenario_creator
         ckw = {"crops_multiplier": args.cm, "num_scens": S}
@@ -91,6 +100,11 @@ def main():
     elif args.case == "sslp":
         names, creator, ckw = sslp.scenario_names_creator(S), sslp.scenario_creator, {}
         desc = "sslp_15_45_10 LP relaxation"
+    elif args.case == "hydro":
+        fan = hydro.synthetic_fanouts(S)
+        names, creator, ckw = hydro.scenario_names_creator(S), hydro.synthetic_scenario_creator, {"fanouts": fan}
+        nodenames = hydro.synthetic_nodenames(fan)
+        desc = f"hydro 3-stage non-uniform tree, stage-2 fan-outs {list(fan)}"
     else:
         names, creator, ckw = netdes.scenario_names_creator(S), netdes.scenario_creator, {"num_scens": S}
         desc = "netdes network-50-30-H-01 LP relaxation"
@@ -100,8 +114,9 @@ def main():
             "pdhg_beta_artificial": args.beta_art, "pdhg_primal_weight_theta": args.theta, "pdhg_presolve": not args.no_presolve,
             "pdhg_keep_omega": {"fresh": False, "carry": True, "blend": "blend"}[args.keep_omega],
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps}}
+    args.creator_kwargs = ckw
     t_setup = time.perf_counter()
-    ph = PH(dict(opts), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw)
+    ph = PH(dict(opts), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw, all_nodenames=nodenames)
     ph.PH_Prep()
     t_iter0 = time.perf_counter()
     ph.Iter0()
@@ -202,6 +217,8 @@ def main():
         "data": {"farmer": "synthetic (farmer generator of examples/farmer/farmer.py, seeded per scenario)",
                  "sslp": "sslp_15_45_10 data (Scenario1-10) + seeded synthetic ClientPresent beyond 10",
                  "netdes": "network-50-30-H-01 data (30 scenarios) + seeded synthetic cost/capacity noise beyond 30",
+                 "hydro": "hydro model of examples/hydro/hydro.py, synthetic inflows A2~U[10,90] per node, "
+                          "A3~U[40,60] per leaf (default_rng(1134))",
                  }[args.case],
         "config": {"workload": f"{desc}, {S} scenarios ({args.scen} per GPU), PH rho={args.rho}, "
                                f"PDHG eps_rel={args.eps}",
@@ -236,7 +253,8 @@ def main():
     # wall time to PH convergence < 1e-4 (fresh run, same instance)
     if args.conv_iters > 0:
         ph2 = PH(dict(opts, PHIterLimit=args.conv_iters, convthresh=1e-4,
-                      time_limit=args.conv_time), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw)
+                      time_limit=args.conv_time), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw,
+                 all_nodenames=nodenames)
         ph2.PH_Prep()
         torch.cuda.synchronize()
         if comm is not None:
@@ -268,7 +286,7 @@ def _cpu_worker(payload):
     from oracle import highs
     from oracle import models as om
     case, names, kw, W, xbar, rho, budget = payload
-    build = {"farmer": om.farmer, "sslp": om.sslp, "netdes": om.netdes}[case]
+    build = {"farmer": om.farmer, "sslp": om.sslp, "netdes": om.netdes, "hydro": om.hydro_tree}[case]
     cnt = 0
     t0 = _t.perf_counter()
     for k, nm in enumerate(names):
@@ -276,12 +294,16 @@ def _cpu_worker(payload):
         a = sc.arrays()
         cols = np.array(sc.nonant_cols())
         c = a["c"].copy()
-        c[cols] += W[k] - rho * xbar
+        xb = xbar[k]
+        c[cols] += W[k] - rho * xb
         q = np.zeros_like(c)
         q[cols] = rho
-        highs.solve(c, a["rowptr"], a["colidx"], a["vals"], a["row_lo"], a["row_hi"], a["col_lo"],
-                    a["col_hi"], qdiag=q, offset=float(np.sum(rho / 2 * xbar * xbar)),
-                    do_polish=len(c) > 1000)
+        left = budget - (_t.perf_counter() - t0)
+        r = highs.solve(c, a["rowptr"], a["colidx"], a["vals"], a["row_lo"], a["row_hi"], a["col_lo"],
+                        a["col_hi"], qdiag=q, offset=float(np.sum(rho / 2 * xb * xb)),
+                        do_polish=len(c) > 1000, time_limit=left + 1.0)
+        if r.status != "Optimal":   # HiGHS stopped at the sample's time limit: not a completed solve
+            break
         cnt += 1
         if _t.perf_counter() - t0 > budget:
             break
@@ -297,16 +319,22 @@ def cpu_baseline(ph, args):
         P = max(1, min(len(os.sched_getaffinity(0)), 16))
         eng = ph.engine
         W = eng.get(_lib.F_W).reshape(eng.S, eng.N)
-        xbar = eng.get(_lib.F_XBAR)
+        # per-scenario x-bar rows: the nonants of each tree level take their node's x-bar
+        xb_nodes = eng.get(_lib.F_XBAR)
+        b = eng.batch
+        xbar = np.stack([np.concatenate([xb_nodes[b.node_off[g]:b.node_off[g] + b.level_len[lv]]
+                                         for lv, g in enumerate(b.scen_node[s])]) for s in range(eng.S)])
         names = ph.local_scenario_names
         per = max(1, len(names) // P)
-        S = len(ph.all_scenario_names)
-        kw = {"farmer": {"crops_multiplier": args.cm, "num_scens": S}, "sslp": {}, "netdes": {"num_scens": S}}[args.case]
-        payloads = [(args.case, names[i * per:(i + 1) * per], kw, W[i * per:(i + 1) * per], xbar, args.rho,
+        kw = args.creator_kwargs
+        payloads = [(args.case, names[i * per:(i + 1) * per], kw, W[i * per:(i + 1) * per],
+                     xbar[i * per:(i + 1) * per], args.rho,
                      args.cpu_seconds) for i in range(P)]
         ctx = mp.get_context("spawn")
+        print(f"[bench] cpu baseline: {P} processes, ~{args.cpu_seconds:.0f} s sample", file=sys.stderr, flush=True)
         with ctx.Pool(P) as pool:
-            res = pool.map(_cpu_worker, payloads)
+            # hard cap: a worker stuck inside one solve must not hold the GPU measurement hostage
+            res = pool.map_async(_cpu_worker, payloads).get(timeout=3 * args.cpu_seconds + 90)
         n = sum(r[0] for r in res)
         t = max(r[1] for r in res)
         solver = "HiGHS 1.8 via scipy, threads=1 each" if eng.batch.n <= 1000 else \

@@ -5,8 +5,12 @@
 (1-based); the stage-2 node is ``ROOT_{(k-1)//BF[1]}`` with cond. prob 1/BF[0]
 (``hydro.py:187-215``); probability "uniform".  The nine data files differ only in the inflows
 A[2] in {10,50,90} (by (k-1)//3) and A[3] in {40,50,60} (by (k-1)%3); ``inflows`` overrides (A2, A3)
-for the synthetic non-uniform trees of BASELINE M3.
+for the synthetic non-uniform trees of BASELINE M3 (``synthetic_scenario_creator``).
 """
+import functools
+
+import numpy as np
+
 from .. import model as lm
 from ..scenario_tree import ScenarioNode
 from .farmer import extract_num
@@ -69,6 +73,43 @@ def _instance(name, A):
     m.add_row([(sl[None], 1.0), (vol[3], 4166.67)], 4166.67 * V0, None, "fcfe")
     m.set_objective([(sc[t], 1.0) for t in T], lm.minimize)
     return m
+
+
+@functools.lru_cache(maxsize=8)
+def _synthetic_tree(fanouts, seed):
+    """Inflows of a non-uniform 3-stage tree: A[2] ~ U[10, 90] per stage-2 node,
+    A[3] ~ U[40, 60] per leaf (the ranges of the commented ``B`` table in
+    ``examples/hydro/PySP/scenariodata/Scen1.dat:30-33``), numpy ``default_rng(seed)``, node draws
+    first.  Leaves are numbered 1.. in node order."""
+    rng = np.random.default_rng(seed)
+    a2 = rng.uniform(10.0, 90.0, size=len(fanouts))
+    a3 = rng.uniform(40.0, 60.0, size=int(sum(fanouts)))
+    node_of = np.repeat(np.arange(len(fanouts)), fanouts)
+    return a2, a3, node_of
+
+
+def synthetic_fanouts(num_scens):
+    """Stage-2 fan-outs 10 % / 30 % / 60 % of the leaves: 500 -> (50, 150, 300), 2000 -> (200, 600, 1200)."""
+    f1, f2 = num_scens // 10, (3 * num_scens) // 10
+    return (f1, f2, num_scens - f1 - f2)
+
+
+def synthetic_scenario_creator(scenario_name, fanouts=(50, 150, 300), seed=1134):
+    """Leaf ``Scen<k>`` of the non-uniform tree: stage-2 node ``ROOT_b`` (cond. prob 1/B), scenario
+    probability (1/B)/fanouts[b]; same model as ``scenario_creator`` with that leaf's inflows."""
+    fanouts = tuple(int(f) for f in fanouts)
+    a2, a3, node_of = _synthetic_tree(fanouts, seed)
+    k = extract_num(scenario_name) - 1
+    b = int(node_of[k])
+    B = len(fanouts)
+    m = scenario_creator(scenario_name, branching_factors=[B, 1], inflows=(float(a2[b]), float(a3[k])),
+                         node_name=f"ROOT_{b}", cond_prob=1.0 / B)
+    m._mpisppy_probability = (1.0 / B) / fanouts[b]
+    return m
+
+
+def synthetic_nodenames(fanouts):
+    return ["ROOT"] + [f"ROOT_{b}" for b in range(len(fanouts))]
 
 
 def scenario_names_creator(num_scens, start=None):

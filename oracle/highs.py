@@ -33,7 +33,7 @@ def _finite(v):
 
 
 def solve(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=None, offset=0.0,
-          threads=1, tol=1e-10, presolve=None, do_polish=True):
+          threads=1, tol=1e-10, presolve=None, do_polish=True, time_limit=None):
     """min c^T x + 1/2 x^T diag(qdiag) x + offset  s.t. row_lo <= A x <= row_hi, col_lo <= x <= col_hi.
 
     A is given in CSR (rowptr[m+1], colidx[nnz], vals[nnz]).
@@ -53,6 +53,8 @@ def solve(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=None, o
     h.setOptionValue("threads", int(threads))
     if presolve is not None:
         h.setOptionValue("presolve", presolve)
+    if time_limit is not None:   # bounded CPU-baseline samples (bench.py): a cut-off solve is not counted
+        h.setOptionValue("time_limit", float(max(time_limit, 0.01)))
     h.setOptionValue("primal_feasibility_tolerance", tol)
     h.setOptionValue("dual_feasibility_tolerance", tol)
     lp = _hc.HighsLp()

@@ -202,6 +202,23 @@ def hydro(scenario_name, branching_factors=(3, 3), inflow=None):
     return s
 
 
+def hydro_tree(scenario_name, fanouts=(50, 150, 300), seed=1134):
+    """Non-uniform 3-stage hydro tree: stage-2 node b has fanouts[b] leaves, cond.
+    prob 1/B; inflow A2 ~ U[10,90] per node, A3 ~ U[40,60] per leaf, ``default_rng(seed)`` drawing the
+    B node values then the leaf values (ranges: ``PySP/scenariodata/Scen1.dat:30-33``)."""
+    rng = np.random.default_rng(seed)
+    B = len(fanouts)
+    a2 = rng.uniform(10.0, 90.0, size=B)
+    a3 = rng.uniform(40.0, 60.0, size=int(sum(fanouts)))
+    k = extract_num(scenario_name) - 1
+    b = int(np.searchsorted(np.cumsum(fanouts), k, side="right"))
+    s = hydro(scenario_name, inflow=(float(a2[b]), float(a3[k])))
+    s.nodes[1]["name"] = f"ROOT_{b}"
+    s.nodes[1]["cond_prob"] = 1.0 / B
+    s.prob = (1.0 / B) / fanouts[b]
+    return s
+
+
 def hydro_names(num_scens=9):
     return [f"Scen{i}" for i in range(1, num_scens + 1)]
 

@@ -1,0 +1,41 @@
+"""Multi-rank bench path on the one-GPU box: ``bench.py`` under ``torch.distributed.run`` with two
+ranks sharing cuda:0 over the gloo backend (the device exchange buffers are all-reduced through
+host staging; the 8-GPU RCCL run is the driver's).  The 2-rank run shards 2x500 farmer scenarios
+with the reference's slicing; its PH trajectory must match a 1-rank run of the same 1000 scenarios
+(conv to 1e-9 relative: only the node-sum summation order differs)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--steps", "3", "--warmup", "2", "--conv-iters", "0", "--cpu-seconds", "0", "--cm", "2"]
+
+
+def _run(cmd, env):
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_two_ranks_match_one_rank():
+    env = dict(os.environ, PHG_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    one = _run([sys.executable, "bench.py", "--scen", "1000"] + ARGS, env)
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", "2",
+                "--scen", "500"] + ARGS, env)
+    assert two["n_gpus"] == 2 and two["config"]["scenarios"] == 1000
+    assert one["config"]["scenarios"] == 1000
+    assert two["value"] > 0
+    c1, c2 = one["conv_at_end"], two["conv_at_end"]
+    assert abs(c1 - c2) <= 1e-9 * max(1.0, abs(c1)), (c1, c2)

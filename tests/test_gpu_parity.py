@@ -292,3 +292,36 @@ def test_pipelined_iteration_matches_sequential():
     assert i1 == i0 < 200 and c1 < 1e-3
     assert h1 == h0 and c1 == c0 and e1 == e0 and k1 == k0
     assert np.array_equal(W1, W0) and np.array_equal(x1, x0) and np.array_equal(n1, n0)
+
+
+# ----------------------------------------------------------------------------- non-uniform trees (M3)
+@pytest.mark.parametrize("fan", [(2, 1, 4), (5, 15, 30)])
+def test_hydro_nonuniform_tree_vs_oracle(fan):
+    """Synthetic 3-stage hydro trees with unequal fan-outs and per-leaf probabilities: Iter0 trivial
+    bound 1e-7; then the oracle's x fed to the fused kernels: per-node xbar / W / conv to 1e-12."""
+    S = sum(fan)
+    kw = {"fanouts": fan}
+    ph = PH(_opts(), hydro.scenario_names_creator(S), hydro.synthetic_scenario_creator,
+            all_nodenames=hydro.synthetic_nodenames(fan), scenario_creator_kwargs=kw)
+    ph.PH_Prep()
+    tb = ph.Iter0()
+    o = oph.OraclePH(_opts(), om.hydro_names(S), om.hydro_tree, kw)
+    otb = o.Iter0()
+    assert abs(tb - otb) <= 1e-7 * max(1.0, abs(otb)), (tb, otb)
+    for it in range(3):
+        ph.engine.set(_lib.F_XN, np.array([o.nonants(k) for k in range(S)]).ravel())
+        o.Compute_Xbar()
+        o.Update_W()
+        oc = o.convergence_diff()
+        ph.Compute_Xbar()
+        ph.Update_W()
+        c = ph.convergence_diff()
+        want = np.concatenate([o.node_xbar[nd] for nd in hydro.synthetic_nodenames(fan)])
+        np.testing.assert_allclose(ph.xbars(), want, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(ph.Ws(), o.W, rtol=1e-12, atol=1e-9)
+        assert abs(c - oc) <= 1e-12 * max(1.0, abs(oc))
+        o.solve_loop()
+    # sum_s p_s W_s = 0 per node after the updates (phbase.py:301-326 invariant)
+    p = np.array([o.prob[k] for k in range(S)])
+    Wm = ph.Ws().reshape(S, -1)
+    assert np.abs(p @ Wm[:, :4]).max() < 1e-9

@@ -107,3 +107,18 @@ def test_netdes_sizes_and_balance():
     assert (m.n, m.m, len(m.pattern()[1]), len(m._mpisppy_node_list[0].nonant_vardata_list)) == (2940, 1520, 5880, 1470)
     a = m.arrays()
     assert abs(a["row_lo"][1470:].sum()) < 1e-9       # flow balance: sum of node demands is zero
+
+
+@pytest.mark.parametrize("fan", [(50, 150, 300), (2, 1, 4)])
+def test_hydro_synthetic_tree_bit_exact(fan):
+    S = sum(fan)
+    for k in sorted({1, 2, fan[0], fan[0] + 1, S}):
+        m = hydro.synthetic_scenario_creator(f"Scen{k}", fanouts=fan)
+        o = om.hydro_tree(f"Scen{k}", fanouts=fan)
+        _same(m, o)
+        assert m._mpisppy_probability == o.prob
+        assert m._mpisppy_node_list[1].name == o.nodes[1]["name"]
+        assert m._mpisppy_node_list[1].cond_prob == o.nodes[1]["cond_prob"]
+    assert hydro.synthetic_fanouts(500) == (50, 150, 300) and hydro.synthetic_fanouts(2000) == (200, 600, 1200)
+    p = [hydro.synthetic_scenario_creator(f"Scen{k}", fanouts=fan)._mpisppy_probability for k in range(1, S + 1)]
+    assert abs(sum(p) - 1.0) < 1e-12
