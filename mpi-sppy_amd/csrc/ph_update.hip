@@ -214,6 +214,10 @@ __device__ __forceinline__ double block_sum_range(const double* v, int first, in
 // reach the KKT tolerance / failed numerically.  The last workgroup reduces the segment partials
 // per virtual rank (fixed order) into convpart[2v], convpart[2v+1] = (sum, count) and
 // convpart[2P], convpart[2P+1] = the two status counts; workgroup 0 publishes xbar / xsqbar.
+// ROOT_ONLY (two-stage trees, checked on the host: PhArgs::root_only): the x-bar of element e is nodesum[e mod N], tracked per
+// thread by increments instead of the per-element index array (4 fewer bytes and one dependent load
+// less per element); multistage trees read xidx.
+template <bool ROOT_ONLY>
 __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* nodesum, double* convpart) {
     __shared__ double red[4];
     __shared__ int bad[8];
@@ -230,6 +234,10 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
         return fabs(d);
     };
     long e = e0 + tid;
+    // ROOT_ONLY: k = e mod N, advanced by dk = 256 mod N (< N) per 256-element stride
+    const int dk = ROOT_ONLY ? 256 % a.N : 0;
+    int k = ROOT_ONLY ? (int)(e % a.N) : 0;
+    auto adv = [&](int kk) { kk += dk; return kk >= a.N ? kk - a.N : kk; };
     // four elements in flight per thread (all loads before the stores), then the remainder
     for (; e + 3 * 256 < e1; e += 4 * 256) {
         double xv[4], xb[4], w[4], r[4];
@@ -237,14 +245,20 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
         for (int u = 0; u < 4; ++u) {
             const long f = e + u * 256;
             xv[u] = a.xN[f];
-            xb[u] = nodesum[a.xidx[f]];
+            if constexpr (ROOT_ONLY) { xb[u] = nodesum[k]; k = adv(k); }
+            else xb[u] = nodesum[a.xidx[f]];
             w[u] = a.W[f];
             r[u] = a.rho[f];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc += upd(e + u * 256, xv[u], xb[u], w[u], r[u]);
     }
-    for (; e < e1; e += 256) acc += upd(e, a.xN[e], nodesum[a.xidx[e]], a.W[e], a.rho[e]);
+    for (; e < e1; e += 256) {
+        double xb;
+        if constexpr (ROOT_ONLY) { xb = nodesum[k]; k = adv(k); }
+        else xb = nodesum[a.xidx[e]];
+        acc += upd(e, a.xN[e], xb, a.W[e], a.rho[e]);
+    }
     int nb = 0, nn = 0;
     if (a.status)
         for (int s = s0 + tid; s < s1; s += 256) {
@@ -358,7 +372,10 @@ hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
 }
 
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st) {
-    hipLaunchKernelGGL(w_update_kernel, dim3(a.n_cseg), dim3(256), 0, st, a, nodesum, convpart);
+    if (a.root_only)
+        hipLaunchKernelGGL(w_update_kernel<true>, dim3(a.n_cseg), dim3(256), 0, st, a, nodesum, convpart);
+    else
+        hipLaunchKernelGGL(w_update_kernel<false>, dim3(a.n_cseg), dim3(256), 0, st, a, nodesum, convpart);
     return hipGetLastError();
 }
 

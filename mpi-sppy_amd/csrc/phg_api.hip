@@ -599,7 +599,10 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     for (int s = 0; s < S; ++s)
         for (int k = 0; k < N; ++k)
             xidx[(size_t)s * N + k] = b->node_off[b->scen_node[s * L + b->nonant_level[k]]] + b->nonant_pos[k];
+    bool root_only = true;   // x-bar slot == k for every scenario (two-stage): w_update_kernel<true>
+    for (size_t e = 0; e < xidx.size() && root_only; ++e) root_only = xidx[e] == (int)(e % (size_t)N);
     PhArgs& a = h->ph;
+    a.root_only = root_only ? 1 : 0;
     a.S = S; a.N = N; a.N_tot = b->N_tot; a.L = L; a.P = P; a.maxk = maxk; a.n_nodes = b->n_nodes;
     a.n_seg = (int)segs.size();
     a.n_cseg = (int)cv.size();

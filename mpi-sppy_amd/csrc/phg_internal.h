@@ -139,6 +139,7 @@ struct PhArgs {
     double* W;              // [S*N]
     const double* rho;      // [S*N]
     const int* xidx;        // [S*N]
+    int root_only;          // xidx[s*N + k] == k for all s (two-stage trees): xidx is not read
     const double* pc;       // [S*L]
     const double* pcv;      // [S*N] per-nonant prob coefficients (variable probability) or null
     int L;
