@@ -72,6 +72,7 @@ __device__ void conv_gate_block(const double* convpart, int P, double* gate, dou
 // workgroups that are already running (K is far below the resident capacity).  finish_k() re-arms
 // the counters for the next launch once all K are done.
 __device__ __forceinline__ int last_k_workgroups(unsigned* counter, int K) {
+    const int total = (int)(gridDim.x * gridDim.y);
     __shared__ int s_rank;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -79,9 +80,9 @@ __device__ __forceinline__ int last_k_workgroups(unsigned* counter, int K) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int rank = (int)prev - ((int)gridDim.x - K);
+        const int rank = (int)prev - (total - K);
         if (rank >= 0) {
-            while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x)
+            while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)total)
                 __builtin_amdgcn_s_sleep(1);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
@@ -102,9 +103,11 @@ __device__ __forceinline__ void finish_k(unsigned* counter, unsigned* done, int 
 }
 
 // Node sums (first half of _Compute_Xbar).  One workgroup per node segment (a contiguous scenario
-// range inside one node, sized on the host so that large batches get ~512 segments per level);
+// range inside one node, sized on the host so that large batches get ~512 segments per level) and
+// 256-nonant column chunk (blockIdx.y; wide nodes get several workgroups per segment, so the
+// number of loads in flight does not depend on the final reduction's segment count);
 // thread t handles nonant k = t % klen of scenarios s0 + t / klen + q*i (q = 256 / klen lanes per
-// nonant) -> coalesced rows of xN, 4 rows in flight per thread.  The last K workgroups then add
+// nonant) -> coalesced rows of xN, 8 rows in flight per thread.  The last K workgroups then add
 // every node's segment partials in segment order (element range split K ways):
 // nodesum[e] = sum p x, nodesum[N_tot + e] = sum p x^2 (the buffer the cross-GPU all-reduce sums).
 __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
     const int tid = threadIdx.x;
     const NodeSeg sg = a.seg[blockIdx.x];
     double* out = a.segpart + (long)blockIdx.x * 2 * a.maxk;
-    for (int k0 = 0; k0 < sg.klen; k0 += 256) {
+    for (int k0 = 256 * (int)blockIdx.y; k0 < sg.klen; k0 += 256 * (int)gridDim.y) {
         const int kl = min(256, sg.klen - k0);
         const int q = 256 / kl;
         const int k = tid % kl;
@@ -125,14 +128,17 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
                 p = a.pcv ? a.pcv[(long)s * a.N + kg] : a.pc[(long)s * a.L + sg.level];
             };
             int s = sg.s0 + so;
-            // four independent rows per step (fixed pairing: deterministic), then the remainder
-            double t1[4] = {0, 0, 0, 0}, t2[4] = {0, 0, 0, 0};
-            for (; s + 3 * q < sg.s1; s += 4 * q) {
-                double p[4], xv[4];
+            // eight independent rows per step (fixed pairing: deterministic), then the remainder
+            constexpr int R = 8;
+            double t1[R], t2[R];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) px(s + u * q, p[u], xv[u]);
+            for (int u = 0; u < R; ++u) t1[u] = t2[u] = 0.0;
+            for (; s + (R - 1) * q < sg.s1; s += R * q) {
+                double p[R], xv[R];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) { t1[u] += p[u] * xv[u]; t2[u] += p[u] * xv[u] * xv[u]; }
+                for (int u = 0; u < R; ++u) px(s + u * q, p[u], xv[u]);
+#pragma unroll
+                for (int u = 0; u < R; ++u) { t1[u] += p[u] * xv[u]; t2[u] += p[u] * xv[u] * xv[u]; }
             }
             for (; s < sg.s1; s += q) {
                 double p, xv;
@@ -140,8 +146,8 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
                 t1[0] += p * xv;
                 t2[0] += p * xv * xv;
             }
-            s1 = (t1[0] + t1[1]) + (t1[2] + t1[3]);
-            s2 = (t2[0] + t2[1]) + (t2[2] + t2[3]);
+            s1 = ((t1[0] + t1[1]) + (t1[2] + t1[3])) + ((t1[4] + t1[5]) + (t1[6] + t1[7]));
+            s2 = ((t2[0] + t2[1]) + (t2[2] + t2[3])) + ((t2[4] + t2[5]) + (t2[6] + t2[7]));
         }
         sh[tid] = s1;
         sh[256 + tid] = s2;
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
         }
         __syncthreads();
     }
-    const int K = min(a.n_final, (int)gridDim.x);
+    const int K = min(a.n_final, (int)(gridDim.x * gridDim.y));
     const int rank = last_k_workgroups(a.ticket, K);
     if (rank < 0) return;
     // elements [e_lo, e_hi) of this rank; T lanes per element (power of two <= 64), each summing
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
                 if (a.node_off[mid] <= e) lo = mid; else hi = mid - 1;
             }
             const int i = e - a.node_off[lo];
-#pragma unroll 4
+#pragma unroll 8
             for (int g = a.node_first_seg[lo] + sub; g < a.node_first_seg[lo + 1]; g += T) {
                 t1 += a.segpart[(long)g * 2 * a.maxk + i];
                 t2 += a.segpart[(long)g * 2 * a.maxk + a.maxk + i];
@@ -367,7 +373,7 @@ hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double*
 }
 
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
-    hipLaunchKernelGGL(node_sums_kernel, dim3(a.n_seg), dim3(256), 0, st, a, nodesum);
+    hipLaunchKernelGGL(node_sums_kernel, dim3(a.n_seg, (a.maxk + 255) / 256), dim3(256), 0, st, a, nodesum);
     return hipGetLastError();
 }
 
