@@ -13,18 +13,27 @@
 
 namespace phg {
 
-// "Last workgroup done" hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): every storing
-// wave drains its stores, lane 0 releases at agent scope and takes a ticket; the workgroup whose
-// ticket is last acquires at agent scope and finishes the reduction in a FIXED order, so the result
-// does not depend on which workgroup arrived last.  That workgroup also re-zeroes the counter for
-// the next (stream-ordered) launch.
+// Handed-off partials are published write-through: every store of them is an agent-scope (sc1)
+// store, so no workgroup needs an agent-scope release (buffer_wbl2, a write-back of the XCD's whole
+// L2 -- ~0.4 us per workgroup per XCD, serialised, measured on the PH-update sweep).  The consumer
+// side keeps its agent-scope acquire (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores,
+// every storing wave's vmcnt(0), a workgroup barrier, then the counter add; acquire, then loads).
+__device__ __forceinline__ void publish(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// "Last workgroup done" hand-off: every storing wave drains its (published) stores, lane 0 takes a
+// ticket; the workgroup whose ticket is last acquires at agent scope and finishes the reduction in
+// a FIXED order, so the result does not depend on which workgroup arrived last.  That workgroup
+// also re-zeroes the counter for the next (stream-ordered) launch.
 __device__ __forceinline__ bool last_workgroup(unsigned* counter) {
     __shared__ unsigned s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool last = prev == gridDim.x - 1;
         if (last) {
@@ -77,8 +86,6 @@ __device__ __forceinline__ int last_k_workgroups(unsigned* counter, int K) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int rank = (int)prev - (total - K);
         if (rank >= 0) {
@@ -155,8 +162,8 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
         if (tid < kl) {
             double t1 = 0.0, t2 = 0.0;
             for (int j = 0; j < q; ++j) { t1 += sh[j * kl + tid]; t2 += sh[256 + j * kl + tid]; }
-            out[k0 + tid] = t1;
-            out[a.maxk + k0 + tid] = t2;
+            publish(&out[k0 + tid], t1);
+            publish(&out[a.maxk + k0 + tid], t2);
         }
         __syncthreads();
     }
@@ -281,9 +288,9 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
     if ((tid & 63) == 0) { red[tid >> 6] = acc; bad[tid >> 6] = nb; bad[4 + (tid >> 6)] = nn; }
     __syncthreads();
     if (tid == 0) {
-        a.csegpart[b] = ((red[0] + red[1]) + red[2]) + red[3];
-        a.csegbad[2 * b] = bad[0] + bad[1] + bad[2] + bad[3];
-        a.csegbad[2 * b + 1] = bad[4] + bad[5] + bad[6] + bad[7];
+        publish(&a.csegpart[b], ((red[0] + red[1]) + red[2]) + red[3]);
+        publish(&a.csegbad[2 * b], bad[0] + bad[1] + bad[2] + bad[3]);
+        publish(&a.csegbad[2 * b + 1], bad[4] + bad[5] + bad[6] + bad[7]);
     }
     if (b == 0)
         for (int j = tid; j < a.N_tot; j += 256) {
