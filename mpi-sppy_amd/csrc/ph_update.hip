@@ -102,7 +102,8 @@ __device__ __forceinline__ int last_k_workgroups(unsigned* counter, int K) {
 __device__ __forceinline__ void finish_k(unsigned* counter, unsigned* done, int K) {
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)K - 1) {
+        // relaxed: the counters are only re-read by the next (stream-ordered) launch
+        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)K - 1) {
             __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }

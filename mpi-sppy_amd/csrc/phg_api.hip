@@ -610,12 +610,12 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     a.S = S; a.N = N; a.N_tot = b->N_tot; a.L = L; a.P = P; a.maxk = maxk; a.n_nodes = b->n_nodes;
     a.n_seg = (int)segs.size();
     a.n_cseg = (int)cv.size();
-    {   // final node-sum reduction: ~8K partial loads per workgroup, at most 128 workgroups (far
+    {   // final node-sum reduction: ~2K partial loads per workgroup, at most 128 workgroups (far
         // below the resident capacity, so the ranked workgroups' spin never starves a late one)
         long loads = 0;
         for (int g = 0; g < b->n_nodes; ++g)
             loads += 2L * (first[g + 1] - first[g]) * b->level_len[node_level[g]];
-        a.n_final = (int)std::min<long>(128, std::max<long>(1, (loads + 8191) / 8192));
+        a.n_final = (int)std::min<long>(128, std::max<long>(1, (loads + 2047) / 2048));
     }
     {
         NodeSeg* p;
