@@ -403,7 +403,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
             const long b = sn + cj[k];
             a.xs[b] = x[k];
             const double xu = x[k] * dcs[k];
-            a.x_out[b] = xu;
+            if (a.x_out) a.x_out[b] = xu;
             const int kk = L.col_nonant[cj[k]];
             if (kk >= 0) a.xN[sN + kk] = xu;
         }
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
         if (ri[r] >= 0) {
             const long b = sm + ri[r];
             a.ys[b] = y[r];
-            a.y_out[b] = y[r] * drs[r];
+            if (a.y_out) a.y_out[b] = y[r] * drs[r];
         }
     }
     if (l == 0) {

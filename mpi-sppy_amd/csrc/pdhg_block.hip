@@ -387,7 +387,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             const double xv = use_avg_final ? xsum[k] * inv : x[k];
             a.xs[b] = xv;
             const double xu = xv * a.dc[b];
-            a.x_out[b] = xu;
+            if (a.x_out) a.x_out[b] = xu;
             const int kk = a.lay.col_nonant[cj[k]];
             if (kk >= 0) a.xN[sN + kk] = xu;
         }
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             const long b = sm + ri[r];
             const double yv = use_avg_final ? ysum[r] * inv : y[r];
             a.ys[b] = yv;
-            a.y_out[b] = yv * a.dr[b];
+            if (a.y_out) a.y_out[b] = yv * a.dr[b];
         }
     }
     if (t == 0) {

@@ -402,7 +402,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 const double xv = use_avg ? xsum[k] * inv : x[k];
                 a.xs[b] = xv;
                 const double xu = xv * a.dc[b];
-                a.x_out[b] = xu;
+                if (a.x_out) a.x_out[b] = xu;
                 const int kk = col_nonant[j];
                 if (kk >= 0) a.xN[sN + kk] = xu;
             }
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 const long b = sm + i;
                 const double yv = use_avg ? ysum[r] * inv : y[r];
                 a.ys[b] = yv;
-                a.y_out[b] = yv * a.dr[b];
+                if (a.y_out) a.y_out[b] = yv * a.dr[b];
             }
         }
         if (gl == 0) {
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                     const long b = sm + i;
                     const double yv = use_avg ? ydsum[d] * inv : yd[d];
                     a.ys[b] = yv;
-                    a.y_out[b] = yv * a.dr[b];
+                    if (a.y_out) a.y_out[b] = yv * a.dr[b];
                 }
             }
             const double offs = a.obj_off[sl] + (a.prox_on ? CS(CI::SC + CI::PROX) : 0.0);

@@ -363,6 +363,19 @@ __global__ void broadcast_row_kernel(const double* row, int N, int S, double* ou
     if (e < (long)S * N) out[e] = row[e % N];
 }
 
+// out[e] = s[e] * d[e]: the unscaled solution from the scaled warm-start state (x = xs * dc,
+// y = ys * dr -- the same product the PDHG epilogues would store), materialised on demand
+__global__ void unscale_kernel(const double* sv, const double* d, long cnt, double* out) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < cnt) out[e] = sv[e] * d[e];
+}
+
+hipError_t unscale_launch(const double* sv, const double* d, long cnt, double* out, hipStream_t st) {
+    if (cnt <= 0) return hipSuccess;
+    hipLaunchKernelGGL(unscale_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, sv, d, cnt, out);
+    return hipGetLastError();
+}
+
 hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hipStream_t st) {
     const long tot = (long)S * N;
     hipLaunchKernelGGL(broadcast_row_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, row, N, S, out);

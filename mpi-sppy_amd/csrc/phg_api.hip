@@ -35,6 +35,7 @@ hipError_t piece_gather_launch(const double* vals, int nnz, const int* perm, int
                                hipStream_t st);
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
 hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hipStream_t st);
+hipError_t unscale_launch(const double* sv, const double* d, long cnt, double* out, hipStream_t st);
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
 hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double* gate_host, double seq,
                             hipStream_t st);
@@ -66,6 +67,9 @@ struct phg_handle {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     bool loaded = false;
+    // the solves store only the scaled state (xs, ys); the unscaled x / y (x_out, y_out) are
+    // materialised from it when something reads them (materialize_outputs)
+    bool out_stale = false;
     int S = 0, n = 0, m = 0, nnz = 0, N = 0, L = 0, N_tot = 0, n_nodes = 0, P = 1, n_pad = 0;
     double sense = 1.0;
     int variant = -1;          // gather kernel variant (pdhg.hip), or
@@ -144,11 +148,22 @@ static int timing_event(phg_handle* h, int which, int half) {
     const size_t idx = 2 * (size_t)h->tcount[which] + half;
     while (v.size() <= idx) {
         hipEvent_t e;
-        CK(hipEventCreate(&e));
+        // timing only: no system-scope fence (the launch's own end-of-kernel release already
+        // orders the data for the next launch; nothing here is read by the host through the event)
+        CK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         v.push_back(e);
     }
     CK(hipEventRecord(v[idx], h->stream));
     if (half == 1) h->tcount[which]++;
+    return 0;
+}
+
+static int materialize_outputs(phg_handle* h) {
+    if (!h->out_stale) return 0;
+    CK(hipSetDevice(h->device));
+    CK(unscale_launch(h->xs, h->dc, (long)h->S * h->n, h->x_out, h->stream));
+    CK(unscale_launch(h->ys, h->dr, (long)h->S * h->m, h->y_out, h->stream));
+    h->out_stale = false;
     return 0;
 }
 
@@ -220,6 +235,9 @@ int phg_copy_from(phg_handle* dst, phg_handle* src, int32_t field) {
     double* ps = field_ptr(src, field, &ns);
     if (!pd || !ps) return fail("phg_copy_from: unknown field");
     if (nd != ns) return fail("phg_copy_from: field sizes differ (different batches)");
+    if (field == PHG_F_X || field == PHG_F_Y) {
+        if (materialize_outputs(src) || materialize_outputs(dst)) return -1;
+    }
     CK(hipSetDevice(dst->device));
     if (cross_stream_wait(dst, src)) return -1;
     CK(hipMemcpyAsync(pd, ps, nd * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
@@ -1105,6 +1123,7 @@ int phg_set(phg_handle* h, int32_t f, const double* in) {
     size_t cnt = 0;
     double* p = field_ptr(h, f, &cnt);
     if (!p) return fail("phg_set: unknown field");
+    if ((f == PHG_F_X || f == PHG_F_Y) && materialize_outputs(h)) return -1;
     if (f == PHG_F_XBAR) {   // also keep the node-sum buffer consistent
         CK(hipMemcpyAsync(h->nodesum, in, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
     }
@@ -1127,6 +1146,7 @@ int phg_get(phg_handle* h, int32_t f, double* out) {
     size_t cnt = 0;
     double* p = field_ptr(h, f, &cnt);
     if (!p) return fail("phg_get: unknown field");
+    if ((f == PHG_F_X || f == PHG_F_Y) && materialize_outputs(h)) return -1;
     if (f == PHG_F_Y && h->m != h->m_orig) {   // kept rows -> caller's rows (folded rows: 0)
         std::vector<double> packed(cnt);
         CK(hipMemcpyAsync(packed.data(), p, cnt * sizeof(double), hipMemcpyDeviceToHost, h->stream));
@@ -1164,7 +1184,10 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.W = h->W; a.rho = h->rho; a.xbar = h->xbar; a.xidx = h->xidx; a.fixed = h->fixed;
     a.Z = h->Z; a.Psm = h->Psm; a.smooth_on = h->smooth_on;
     a.xs = h->xs; a.ys = h->ys; a.omega = h->omega;
-    a.x_out = h->x_out; a.y_out = h->y_out; a.xN = h->xN; a.obj = h->obj; a.bound = h->bound;
+    // unscaled x / y are not stored by the solve (materialize_outputs derives them on demand);
+    // a gated no-op solve (PH converged) leaves xs / ys, hence the outputs, unchanged
+    a.x_out = nullptr; a.y_out = nullptr; a.xN = h->xN; a.obj = h->obj; a.bound = h->bound;
+    h->out_stale = true;
     a.kkt = h->kkt; a.iters = h->iters; a.status = h->status;
     a.order = (o->schedule && h->have_order) ? h->order : nullptr;
     a.iters_acc = h->iters_acc;
@@ -1266,6 +1289,7 @@ int phg_ph_update(phg_handle* h, double* host_conv) {
 
 int phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on) {
     if (!h || !h->loaded) return fail("phg_eval_objective: no batch loaded");
+    if (materialize_outputs(h)) return -1;
     CK(hipSetDevice(h->device));
     CK(eval_obj_launch(h->S, h->n, h->N, h->x_out, h->c, h->obj_off, h->nonant_col_d, h->xN, h->W,
                        h->rho, h->xbar, h->xidx, w_on, prox_on, h->sense, h->Z, h->Psm, h->smooth_on, h->eval,

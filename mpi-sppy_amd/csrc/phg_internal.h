@@ -90,8 +90,8 @@ struct PdhgArgs {
     double* ys;             // [S*m]
     double* omega;          // [S]
     // outputs
-    double* x_out;          // [S*n] unscaled
-    double* y_out;          // [S*m] unscaled
+    double* x_out;          // [S*n] unscaled, or null: left to phg_get / eval (xs * dc, see unscale_launch)
+    double* y_out;          // [S*m] unscaled, or null (ys * dr)
     double* xN;             // [S*N]
     double* obj;            // [S] model sense
     double* bound;          // [S] model sense
