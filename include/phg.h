@@ -98,6 +98,12 @@ typedef struct phg_opts {
      * phbase.py:1008-1010, decided on the device so the solve can be enqueued before conv is
      * read back); 0: always solve                                                             */
     double  skip_if_conv_below;
+    /* fix_nonants: each fixed value v becomes the box [v - w, v + w], w = fix_tol * max(1, |v|)
+     * (0: exact).  The reference's xhat evaluation fixes exactly and relies on the CPU solver's
+     * primal feasibility tolerance (~1e-6 absolute) when a candidate violates a first-stage row by
+     * round-off (an xbar of first-order solves: farmer 10k sums to 5000 + 2e-7 acres); an exactly
+     * fixed infeasible box sends PDHG's dual iterates off along the infeasibility ray instead.     */
+    double  fix_tol;
 } phg_opts;
 
 /* solve modes (mpisppy/phbase.py:670-760: W_on / prox_on toggles) */
@@ -188,6 +194,29 @@ int  phg_conv_wait(phg_handle* h, double* host_conv);
 int  phg_solve_summary(phg_handle* h, int32_t* out2);
 int  phg_ph_update(phg_handle* h, double* host_conv);
 
+/* Pipelined PH iteration with ONE exchange per iteration (replaces the two Allreduces of
+ * phbase.py:88-92 and :369 inside iterk_loop, phbase.py:976-1035).  The exchange buffer is packed:
+ *     dev_packed = [2*N_tot node sums | 2*virt_nproc+2 conv / status partials | 1 flag]
+ * (phg_exchange_layout: out3 = {node-sum length, partials length, total}; NULL dev_packed = the
+ * handle's own buffer, for one GPU).  One iteration k is
+ *     phg_node_sums(h, dev_packed)      local node sums of the current x (the last solve's)
+ *     (all-reduce SUM of dev_packed across GPUs: node sums of x_k AND the partials of update k-1)
+ *     phg_ph_head(h, dev_packed, thr, k == 1)
+ *                                       conv_{k-1} from the partials -> device gate + host word;
+ *                                       unless conv_{k-1} < thr: xbar, W += rho (x - xbar), and the
+ *                                       partials of update k into dev_packed
+ *     phg_solve(..., skip_if_conv_below = thr)   gated on conv_{k-1} as well
+ *     phg_conv_wait(h, &conv)           conv_{k-1} (+inf at k = 1: no metric yet)
+ * The solve is therefore speculative by one: conv_{k-1} < thr means PH stopped BEFORE solve k-1
+ * (phbase.py:1008-1010).  The device has then skipped update k and solve k, and because solves
+ * double-buffer their state and a gated solve writes nothing, the state is exactly the one before
+ * solve k-1 (x_{k-2}, W_{k-1}, xbar_{k-1}).  After the last iteration, phg_conv_start on the
+ * partials gives conv of the last update; if it is below thr, phg_solve_undo restores the state
+ * before the last solve.                                                                         */
+int  phg_exchange_layout(phg_handle* h, int32_t* out3);
+int  phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t first);
+int  phg_solve_undo(phg_handle* h);
+
 /* smoothed PH (phbase.py:329-346, 641-760): while on, every prox-on solve adds
  * p/2 (x_k - z_k)^2 per nonant and phg_apply_xbar also does Update_z: z += beta (x - z)        */
 int  phg_set_smoothing(phg_handle* h, int32_t on);
@@ -214,7 +243,8 @@ int  phg_query(phg_handle* h, int32_t* idle);
 int  phg_timing_reset(phg_handle* h, int32_t enable);
 int  phg_timing(phg_handle* h, int32_t which, double* total_ms, int32_t* launches, int64_t* pdhg_iters);
 
-/* device pointer of the handle's own exchange buffers (2*N_tot and 2*virt_nproc+2 doubles) */
+/* device pointers into the handle's own packed exchange buffer: its node sums (2*N_tot doubles)
+ * and its conv / status partials (2*virt_nproc+2 doubles, followed by the flag)                */
 int  phg_exchange_buffers(phg_handle* h, double** dev_nodesum, double** dev_convpart);
 
 #ifdef __cplusplus

@@ -35,7 +35,7 @@ class PhgOpts(C.Structure):
                 ("warm_start", C.c_int32), ("fix_nonants", C.c_int32), ("schedule", C.c_int32),
                 ("beta_sufficient", C.c_double), ("beta_necessary", C.c_double),
                 ("beta_artificial", C.c_double), ("primal_weight_theta", C.c_double),
-                ("skip_if_conv_below", C.c_double)]
+                ("skip_if_conv_below", C.c_double), ("fix_tol", C.c_double)]
 
 
 (F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART, F_OMEGA,
@@ -74,6 +74,9 @@ SIGNATURES = {
     "phg_exchange_buffers": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "phg_timing_reset": (C.c_int, [C.c_void_p, C.c_int32]),
     "phg_timing": (C.c_int, [C.c_void_p, C.c_int32, f64p, i32p, C.POINTER(C.c_int64)]),
+    "phg_exchange_layout": (C.c_int, [C.c_void_p, i32p]),
+    "phg_ph_head": (C.c_int, [C.c_void_p, C.c_void_p, C.c_double, C.c_int32]),
+    "phg_solve_undo": (C.c_int, [C.c_void_p]),
 }
 
 _lib = None

@@ -39,6 +39,9 @@ class SingleComm:
     def gather_object(self, obj, root=0):
         return [obj]
 
+    def allgather_object(self, obj):
+        return [obj]
+
 
 class TorchComm:
     """SUM all-reduces over an initialised ``torch.distributed`` process group."""
@@ -93,3 +96,9 @@ class TorchComm:
         out = [None] * self.size
         self.dist.all_gather_object(out, obj, group=self.group)
         return out if self.rank == root else None
+
+    def allgather_object(self, obj):
+        """Pickled objects of every rank, in rank order, on every rank (setup-time control data)."""
+        out = [None] * self.size
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out

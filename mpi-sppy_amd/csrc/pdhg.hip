@@ -58,14 +58,14 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
             if (kk >= 0) {
                 const long t = sN + kk;
                 ph_terms(a, t, cc, qq, prox_const);
-                if (a.fix_nonants) { lo_ = hi_ = a.fixed[t] / d; }
+                if (a.fix_nonants) fixed_box(a, t, d, lo_, hi_);
             }
             dcs[k] = d;
             c[k] = cc * d;
             q[k] = qq * d * d;
             lo[k] = lo_;
             hi[k] = hi_;
-            x[k] = clampd((a.warm & 1) ? a.xs[b] : 0.0, lo_, hi_);
+            x[k] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
 #pragma unroll
             for (int t = 0; t < KCS; ++t) {
                 const int idx = (l * CPL + k) * KCS + t;
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
             rlo[r] = a.rl[b];
             rhi[r] = a.ru[b];
             drs[r] = a.dr[b];
-            y[r] = (a.warm & 1) ? a.ys[b] : 0.0;
+            y[r] = (a.warm & 1) ? a.ys_in[b] : 0.0;
 #pragma unroll
             for (int t = 0; t < KRS; ++t) {
                 const int idx = (l * RPL + r) * KRS + t;
@@ -179,8 +179,8 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
     const double bnorm = a.bnorm[s];
     const double eta = a.eta[s];
     double omega;
-    if ((a.warm & 2) && a.omega[s] > 0.0) {
-        omega = a.omega[s];
+    if ((a.warm & 2) && a.omega_in[s] > 0.0) {
+        omega = a.omega_in[s];
     } else {
         // PDLP init: ||c_hat|| / ||b_hat|| in the scaled space
         double rr[2];
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
         wsum_many<2>(rr);
         const double cn = sqrt(rr[0]), bn = sqrt(rr[1]);
         omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
-        if ((a.warm & 4) && a.omega[s] > 0.0) omega = sqrt(omega * a.omega[s]);   // blend
+        if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);   // blend
     }
     double tau = eta / omega, sig = eta * omega;
 

@@ -81,14 +81,14 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             if (kk >= 0) {
                 const long tt = sN + kk;
                 ph_terms(a, tt, cc, qq, prox_const);
-                if (a.fix_nonants) { lo_ = hi_ = a.fixed[tt] / d; }
+                if (a.fix_nonants) fixed_box(a, tt, d, lo_, hi_);
             }
             c2 += cc * cc;
             c[k] = cc * d;
             q[k] = qq * d * d;
             lo[k] = lo_;
             hi[k] = hi_;
-            x[k] = clampd((a.warm & 1) ? a.xs[b] : 0.0, lo_, hi_);
+            x[k] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
             a.xs[b] = x[k];
         }
     }
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             const long b = sm + i;
             rlo[r] = a.rl[b];
             rhi[r] = a.ru[b];
-            double yy = (a.warm & 1) ? a.ys[b] : 0.0;
+            double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
             if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
             if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];
             y[r] = yy;
@@ -196,8 +196,8 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         prox_const = rr[1];
         const double cn_ = sqrt(rr[2]), bn = sqrt(rr[3]);
         omega = (cn_ > 1e-10 && bn > 1e-10) ? cn_ / bn : 1.0;
-        if ((a.warm & 2) && a.omega[s] > 0.0) omega = a.omega[s];
-        else if ((a.warm & 4) && a.omega[s] > 0.0) omega = sqrt(omega * a.omega[s]);
+        if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
+        else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);
     }
     const double bnorm = a.bnorm[s];
     const double eta = a.eta[s];

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 if (kk >= 0) {
                     const long t = sN + kk;
                     ph_terms(a, t, cc, qq, prox_const);
-                    if (a.fix_nonants) { lo_ = hi_ = a.fixed[t] / d; }
+                    if (a.fix_nonants) fixed_box(a, t, d, lo_, hi_);
                 }
                 c2 += cc * cc;
                 CS(CI::IDC + k) = 1.0 / d;
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 qs = qq * d * d;
                 lo[k] = lo_;
                 hi[k] = hi_;
-                x[k] = clampd((a.warm & 1) ? a.xs[b] : 0.0, lo_, hi_);
+                x[k] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
             }
             CS(CI::XR + k) = x[k];
             CS(CI::Q + k) = qs;
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 CS(CI::IDR + r) = 1.0 / a.dr[b];
                 rlo[r] = a.rl[b];
                 rhi[r] = a.ru[b];
-                double yy = (a.warm & 1) ? a.ys[b] : 0.0;
+                double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
                 if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
                 if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];
                 y[r] = yy;
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 CS(CI::IDRD + d) = 1.0 / a.dr[b];
                 dlo[d] = a.rl[b];
                 dhi[d] = a.ru[b];
-                double yy = (a.warm & 1) ? a.ys[b] : 0.0;
+                double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
                 if (!fin(dlo[d])) yy = fmin(yy, 0.0); else b2d += dlo[d] * dlo[d];
                 if (!fin(dhi[d])) yy = fmax(yy, 0.0); else b2d += dhi[d] * dhi[d];
                 yd[d] = yy;
@@ -212,8 +212,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         CS(CI::SC + CI::PROX) = rr[1];
         const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
         omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
-        if ((a.warm & 2) && a.omega[s] > 0.0) omega = a.omega[s];
-        else if ((a.warm & 4) && a.omega[s] > 0.0) omega = sqrt(omega * a.omega[s]);   // blend
+        if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
+        else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);   // blend
     }
     const double eta = a.eta[s];
     CS(CI::SC + CI::BNORM) = a.bnorm[s];

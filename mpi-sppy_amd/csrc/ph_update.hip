@@ -48,12 +48,10 @@ __device__ __forceinline__ bool last_workgroup(unsigned* counter) {
 }
 
 // conv = (1/P) sum_v convpart[2v] / convpart[2v+1] (phbase.py:349-371; virtual ranks with no
-// nonants contribute 0), then the two status counts: gate = {conv, not optimal, NaN}.  The same
-// three values go to fine-grained pinned host memory followed (system-scope fences) by the
-// sequence number `seq` in gate_host[3]: the host polls that word, so no event has to pass
-// through the GPU's queue.  One 256-thread workgroup, fixed-order tree over the virtual ranks.
-__device__ void conv_gate_block(const double* convpart, int P, double* gate, double* gate_host, double seq) {
-    __shared__ double red[256];
+// nonants contribute 0) -- +inf while convpart[2P+2] (the flag a W update sets) is 0, i.e. before
+// the first W update: no convergence metric exists yet.  One 256-thread workgroup, fixed-order tree
+// over the virtual ranks; every thread returns the same value (the same bits wherever computed).
+__device__ double conv_value_block(const double* convpart, int P, double* red) {
     double t = 0.0;
     for (int v = threadIdx.x; v < P; v += 256)
         if (convpart[2 * v + 1] > 0.0) t += convpart[2 * v] / convpart[2 * v + 1];
@@ -63,15 +61,30 @@ __device__ void conv_gate_block(const double* convpart, int P, double* gate, dou
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        const double g[3] = {red[0] / (double)P, convpart[2 * P], convpart[2 * P + 1]};
-        for (int i = 0; i < 3; ++i) gate[i] = g[i];
-        if (gate_host) {
-            for (int i = 0; i < 3; ++i) __hip_atomic_store(&gate_host[i], g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __threadfence_system();
-            __hip_atomic_store(&gate_host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    const double v = convpart[2 * P + 2] > 0.0 ? red[0] / (double)P : INFINITY;
+    __syncthreads();
+    return v;
+}
+
+// gate = {conv, not optimal, NaN} (the status counts ride in convpart[2P], [2P+1]).  The same
+// three values go to fine-grained pinned host memory followed (system-scope fences) by the
+// sequence number `seq` in gate_host[3]: the host polls that word, so no event has to pass
+// through the GPU's queue.  Called by one thread.
+__device__ void publish_gate(double conv, const double* convpart, int P, double* gate, double* gate_host,
+                             double seq) {
+    const double g[3] = {conv, convpart[2 * P], convpart[2 * P + 1]};
+    for (int i = 0; i < 3; ++i) gate[i] = g[i];
+    if (gate_host) {
+        for (int i = 0; i < 3; ++i) __hip_atomic_store(&gate_host[i], g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(&gate_host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+__device__ void conv_gate_block(const double* convpart, int P, double* gate, double* gate_host, double seq) {
+    __shared__ double red[256];
+    const double conv = conv_value_block(convpart, P, red);
+    if (threadIdx.x == 0) publish_gate(conv, convpart, P, gate, gate_host, seq);
 }
 
 // "Last K workgroups" hand-off: as last_workgroup, but the K workgroups that arrive last all
@@ -231,12 +244,29 @@ __device__ __forceinline__ double block_sum_range(const double* v, int first, in
 // ROOT_ONLY (two-stage trees, checked on the host: PhArgs::root_only): the x-bar of element e is nodesum[e mod N], tracked per
 // thread by increments instead of the per-element index array (4 fewer bytes and one dependent load
 // less per element); multistage trees read xidx.
-template <bool ROOT_ONLY>
-__global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* nodesum, double* convpart) {
+//
+// HEAD (phg_ph_head, the pipelined PH iteration): `convpart` holds the PREVIOUS iteration's
+// partials, all-reduced together with this iteration's node sums in one exchange buffer.  Every
+// workgroup first computes that iteration's convergence metric (the same fixed-order tree, so the
+// same bits in every workgroup and as phg_conv_finish); workgroup 0 publishes it (device gate +
+// pinned host word); and if it is below `head_thr` the whole grid returns -- PH had converged
+// before the solve that followed it, so this update must not happen (phbase.py:1008-1010).  The
+// partials of THIS update then overwrite convpart (by the last workgroup, after every workgroup
+// has read the old ones).
+template <bool ROOT_ONLY, bool HEAD>
+__global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* nodesum, double* convpart,
+                                                       double head_thr, int first) {
     __shared__ double red[4];
     __shared__ int bad[8];
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
+    if constexpr (HEAD) {
+        __shared__ double red256[256];
+        // first PH iteration: no update precedes it, whatever the buffer holds
+        const double conv = first ? INFINITY : conv_value_block(convpart, a.P, red256);
+        if (b == 0 && tid == 0) publish_gate(conv, convpart, a.P, a.gate, a.gate_host, a.gate_seq);
+        if (conv < head_thr) return;   // grid-uniform: no workgroup touches the tickets
+    }
     const int s0 = a.cseg_s0[b], s1 = a.cseg_s1[b];
     const long e0 = (long)s0 * a.N, e1 = (long)s1 * a.N;
     double acc = 0.0;
@@ -321,9 +351,10 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
         if (tid == 0) {
             convpart[2 * a.P] = (double)(bad[0] + bad[1] + bad[2] + bad[3]);
             convpart[2 * a.P + 1] = (double)(bad[4] + bad[5] + bad[6] + bad[7]);
+            convpart[2 * a.P + 2] = 1.0;   // the partials are a W update's
         }
     }
-    if (a.gate) {   // single GPU: nothing to all-reduce, finish convergence_diff here
+    if (!HEAD && a.gate) {   // single GPU: nothing to all-reduce, finish convergence_diff here
         __syncthreads();
         conv_gate_block(convpart, a.P, a.gate, a.gate_host, a.gate_seq);
     }
@@ -400,9 +431,19 @@ hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
 
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st) {
     if (a.root_only)
-        hipLaunchKernelGGL(w_update_kernel<true>, dim3(a.n_cseg), dim3(256), 0, st, a, nodesum, convpart);
+        hipLaunchKernelGGL((w_update_kernel<true, false>), dim3(a.n_cseg), dim3(256), 0, st, a, nodesum, convpart, 0.0, 0);
     else
-        hipLaunchKernelGGL(w_update_kernel<false>, dim3(a.n_cseg), dim3(256), 0, st, a, nodesum, convpart);
+        hipLaunchKernelGGL((w_update_kernel<false, false>), dim3(a.n_cseg), dim3(256), 0, st, a, nodesum, convpart, 0.0, 0);
+    return hipGetLastError();
+}
+
+// packed = [2 N_tot node sums | 2P+2 partials | flag] (phg_api.hip: phg_handle::packed)
+hipError_t ph_head_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st) {
+    double* cp = packed + 2 * (long)a.N_tot;
+    if (a.root_only)
+        hipLaunchKernelGGL((w_update_kernel<true, true>), dim3(a.n_cseg), dim3(256), 0, st, a, packed, cp, thr, first);
+    else
+        hipLaunchKernelGGL((w_update_kernel<false, true>), dim3(a.n_cseg), dim3(256), 0, st, a, packed, cp, thr, first);
     return hipGetLastError();
 }
 

@@ -37,6 +37,7 @@ hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
 hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hipStream_t st);
 hipError_t unscale_launch(const double* sv, const double* d, long cnt, double* out, hipStream_t st);
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
+hipError_t ph_head_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st);
 hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double* gate_host, double seq,
                             hipStream_t st);
 constexpr int kSchedEvery = 4;
@@ -92,6 +93,16 @@ struct phg_handle {
     double *xs = nullptr, *ys = nullptr, *omega = nullptr, *x_out = nullptr, *y_out = nullptr;
     double *xN = nullptr, *obj = nullptr, *bound = nullptr, *kkt = nullptr, *eval = nullptr;
     int *iters = nullptr, *status = nullptr;
+    // Solve state is double-buffered: a solve reads the "front" copy (warm start) and writes the
+    // "back" copy, then the two are swapped.  So the state before the last solve survives it, which
+    // is what lets the PH iteration be speculative by one solve (phg_ph_head): a solve found to be
+    // past convergence is undone by swapping back (phg_solve_undo), and a solve gated off on the
+    // device writes nothing, so its own swap restores the state before the previous solve.
+    struct SolveState {
+        double *xs, *ys, *omega, *xN, *obj, *bound, *kkt;
+        int *iters, *status;
+    } back{};
+    int swaps = 0;             // solves since load (parity of the front copy; phg_solve_undo)
     int* order = nullptr;      // launch schedule (schedule.hip)
     bool have_order = false;
     double* pinned = nullptr;  // page-locked readback buffer (convergence partials)
@@ -101,7 +112,9 @@ struct phg_handle {
     LocalLayout loc{};
     BlockLayout blk{};
     PhArgs ph{};
-    double *nodesum = nullptr, *convpart = nullptr;
+    // the one cross-GPU exchange buffer: [2*N_tot node sums | 2P+2 convergence / status partials |
+    // 1 flag (> 0: the partials hold a W update's values)] -- one all-reduce per PH iteration
+    double *packed = nullptr, *nodesum = nullptr, *convpart = nullptr;
     std::vector<int> nonant_col_h;
     // timing of the last launches (HIP events on the handle's stream)
     // per-launch timing since the last phg_timing_reset: event pairs of every solve (0) and every
@@ -167,6 +180,22 @@ static int materialize_outputs(phg_handle* h) {
     return 0;
 }
 
+// front <-> back copy of the solve state (see phg_handle::SolveState)
+static void swap_state(phg_handle* h) {
+    std::swap(h->xs, h->back.xs);
+    std::swap(h->ys, h->back.ys);
+    std::swap(h->omega, h->back.omega);
+    std::swap(h->xN, h->back.xN);
+    std::swap(h->obj, h->back.obj);
+    std::swap(h->bound, h->back.bound);
+    std::swap(h->kkt, h->back.kkt);
+    std::swap(h->iters, h->back.iters);
+    std::swap(h->status, h->back.status);
+    h->ph.xN = h->xN;          // the PH update kernels read the front copy
+    h->ph.status = h->status;
+    h->out_stale = true;
+}
+
 extern "C" {
 
 const char* phg_last_error(void) { return g_err.c_str(); }
@@ -217,7 +246,9 @@ static double* field_ptr(phg_handle* h, int f, size_t* count);
 
 // ------------------------------------------------------------------------------ cylinders
 // Device-to-device hand-offs between handles on the same GPU (hub -> spoke), ordered across
-// their streams by an event: the copy on dst's stream waits for src's work so far.
+// their streams by events in BOTH directions: the copy on dst's stream waits for src's work so far,
+// and src's later work waits for the copy (src's buffers are rewritten in place by its next W
+// update / solve; without the second wait a spoke could read a W torn between two PH iterations).
 static int cross_stream_wait(phg_handle* dst, phg_handle* src) {
     hipEvent_t e;
     CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -241,7 +272,9 @@ int phg_copy_from(phg_handle* dst, phg_handle* src, int32_t field) {
     CK(hipSetDevice(dst->device));
     if (cross_stream_wait(dst, src)) return -1;
     CK(hipMemcpyAsync(pd, ps, nd * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
-    return 0;
+    // and the other direction: src's next work (e.g. the hub's W update, which rewrites W in place)
+    // must not start before the copy has read src's buffer
+    return cross_stream_wait(src, dst);
 }
 
 int phg_fix_from(phg_handle* dst, phg_handle* src, int32_t scen) {
@@ -252,7 +285,8 @@ int phg_fix_from(phg_handle* dst, phg_handle* src, int32_t scen) {
     if (cross_stream_wait(dst, src)) return -1;
     // fixed[s, :] = src.xN[scen, :] for every s (same device: read straight from src's buffer)
     CK(broadcast_row_launch(src->xN + (size_t)scen * src->N, dst->N, dst->S, dst->fixed, dst->stream));
-    return 0;
+    // src's next solve rewrites xN: it waits for the broadcast to have read the candidate row
+    return cross_stream_wait(src, dst);
 }
 
 int phg_query(phg_handle* h, int32_t* idle) {
@@ -631,8 +665,8 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     {   // final node-sum reduction: ~2K partial loads per workgroup, at most 128 workgroups (far
         // below the resident capacity, so the ranked workgroups' spin never starves a late one)
         long loads = 0;
-        for (int g = 0; g < b->n_nodes; ++g)
-            loads += 2L * (first[g + 1] - first[g]) * b->level_len[node_level[g]];
+        for (int g = 0; g < b->n_nodes; ++g)   // nodes without local scenarios have no segments
+            if (node_level[g] >= 0) loads += 2L * (first[g + 1] - first[g]) * b->level_len[node_level[g]];
         a.n_final = (int)std::min<long>(128, std::max<long>(1, (loads + 2047) / 2048));
     }
     {
@@ -668,8 +702,9 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     if (dput(h, &ip, vfirst.data(), vfirst.size())) return -1; a.vr_first = ip;
     if (dput(h, &ip, xidx.data(), xidx.size())) return -1; h->xidx = ip;
     a.xidx = h->xidx;
-    if (dalloc(h, &h->nodesum, 2 * (size_t)b->N_tot)) return -1;
-    if (dalloc(h, &h->convpart, 2 * (size_t)P + 2)) return -1;
+    if (dalloc(h, &h->packed, 2 * (size_t)b->N_tot + 2 * (size_t)P + 3)) return -1;
+    h->nodesum = h->packed;
+    h->convpart = h->packed + 2 * (size_t)b->N_tot;
     if (dalloc(h, &h->gate, 4)) return -1;
     CK(hipHostMalloc((void**)&h->gate_host, 4 * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
     for (int i = 0; i < 4; ++i) h->gate_host[i] = 0.0;
@@ -1047,6 +1082,15 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     if (dalloc(h, &h->xs, (size_t)S * n)) return -1;
     if (dalloc(h, &h->ys, (size_t)S * m)) return -1;
     if (dalloc(h, &h->omega, S)) return -1;
+    if (dalloc(h, &h->back.xs, (size_t)S * n)) return -1;
+    if (dalloc(h, &h->back.ys, (size_t)S * m)) return -1;
+    if (dalloc(h, &h->back.omega, S)) return -1;
+    if (dalloc(h, &h->back.xN, (size_t)S * N)) return -1;
+    if (dalloc(h, &h->back.obj, S)) return -1;
+    if (dalloc(h, &h->back.bound, S)) return -1;
+    if (dalloc(h, &h->back.kkt, S)) return -1;
+    if (dalloc(h, &h->back.iters, S)) return -1;
+    if (dalloc(h, &h->back.status, S)) return -1;
     if (dalloc(h, &h->x_out, (size_t)S * n)) return -1;
     if (dalloc(h, &h->y_out, (size_t)S * m)) return -1;
     if (dalloc(h, &h->xN, (size_t)S * N)) return -1;
@@ -1183,15 +1227,16 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.dc = h->dc; a.dr = h->dr; a.eta = h->eta; a.obj_off = h->obj_off; a.bnorm = h->bnorm;
     a.W = h->W; a.rho = h->rho; a.xbar = h->xbar; a.xidx = h->xidx; a.fixed = h->fixed;
     a.Z = h->Z; a.Psm = h->Psm; a.smooth_on = h->smooth_on;
-    a.xs = h->xs; a.ys = h->ys; a.omega = h->omega;
-    // unscaled x / y are not stored by the solve (materialize_outputs derives them on demand);
-    // a gated no-op solve (PH converged) leaves xs / ys, hence the outputs, unchanged
-    a.x_out = nullptr; a.y_out = nullptr; a.xN = h->xN; a.obj = h->obj; a.bound = h->bound;
-    h->out_stale = true;
-    a.kkt = h->kkt; a.iters = h->iters; a.status = h->status;
+    // warm start from the front copy, results into the back copy (swapped after the launch);
+    // unscaled x / y are not stored by the solve (materialize_outputs derives them on demand)
+    a.xs_in = h->xs; a.ys_in = h->ys; a.omega_in = h->omega;
+    a.xs = h->back.xs; a.ys = h->back.ys; a.omega = h->back.omega;
+    a.x_out = nullptr; a.y_out = nullptr; a.xN = h->back.xN; a.obj = h->back.obj; a.bound = h->back.bound;
+    a.kkt = h->back.kkt; a.iters = h->back.iters; a.status = h->back.status;
     a.order = (o->schedule && h->have_order) ? h->order : nullptr;
     a.iters_acc = h->iters_acc;
-    a.w_on = w_on; a.prox_on = prox_on; a.fix_nonants = o->fix_nonants; a.warm = o->warm_start;
+    a.w_on = w_on; a.prox_on = prox_on; a.fix_nonants = o->fix_nonants; a.fix_tol = o->fix_tol > 0 ? o->fix_tol : 0.0;
+    a.warm = o->warm_start;
     a.max_iter = o->max_iter; a.check_every = o->check_every; a.eps = o->eps_rel; a.sense = h->sense;
     a.beta_suf = o->beta_sufficient > 0 ? o->beta_sufficient : 0.2;
     a.beta_nec = o->beta_necessary > 0 ? o->beta_necessary : 0.8;
@@ -1207,6 +1252,8 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
     if (timing_event(h, 0, 1)) return -1;
+    swap_state(h);
+    ++h->swaps;
     if (o->schedule && (h->solves % kSchedEvery == 0 || !h->have_order)) {
         CK(schedule_launch(h->iters, h->S, a.check_every, h->order, h->stream));
         h->have_order = true;
@@ -1236,6 +1283,38 @@ int phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpar
     CK(w_update_launch(a, dev_nodesum ? dev_nodesum : h->nodesum,
                        dev_convpart ? dev_convpart : h->convpart, h->stream));
     if (timing_event(h, 1, 1)) return -1;
+    return 0;
+}
+
+int phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t first) {
+    if (!h || !h->loaded) return fail("phg_ph_head: no batch loaded");
+    CK(hipSetDevice(h->device));
+    PhArgs a = h->ph;
+    a.gate = h->gate;
+    a.gate_host = h->gate_host;
+    a.gate_seq = (double)(++h->gate_seq);
+    if (timing_event(h, 1, 0)) return -1;
+    CK(ph_head_launch(a, dev_packed ? dev_packed : h->packed, convthresh, first, h->stream));
+    if (timing_event(h, 1, 1)) return -1;
+    h->gate_fused = false;
+    return 0;
+}
+
+int phg_solve_undo(phg_handle* h) {
+    if (!h || !h->loaded) return fail("phg_solve_undo: no batch loaded");
+    if (h->swaps <= 0) return fail("phg_solve_undo: no solve to undo");
+    CK(hipSetDevice(h->device));
+    CK(hipStreamSynchronize(h->stream));   // nothing queued may still write the copy being restored
+    swap_state(h);
+    --h->swaps;
+    return 0;
+}
+
+int phg_exchange_layout(phg_handle* h, int32_t* out3) {
+    if (!h || !h->loaded || !out3) return fail("phg_exchange_layout: no batch loaded");
+    out3[0] = 2 * h->N_tot;                 // node sums
+    out3[1] = 2 * h->P + 2;                 // convergence / status partials
+    out3[2] = 2 * h->N_tot + 2 * h->P + 3;  // total, incl. the flag
     return 0;
 }
 

@@ -85,7 +85,11 @@ struct PdhgArgs {
     const double* Z;        // [S*N]   smoothing centre z (smoothed PH, phbase.py:641-760)
     const double* Psm;      // [S*N]   smoothing weight p
     int smooth_on;
-    // state (scaled), persists across solves for warm starts
+    // state (scaled), persists across solves for warm starts: read from the *_in copy, written
+    // to the other (the handle's double-buffered solve state, phg_api.hip SolveState)
+    const double* xs_in;    // [S*n]
+    const double* ys_in;    // [S*m]
+    const double* omega_in; // [S]
     double* xs;             // [S*n]
     double* ys;             // [S*m]
     double* omega;          // [S]
@@ -101,6 +105,7 @@ struct PdhgArgs {
     const int* order;       // [S] launch order (scenario of work item i), or nullptr = identity
     long long* iters_acc;   // [S] PDHG iterations accumulated over solves (phg_timing_reset zeroes)
     int w_on, prox_on, fix_nonants, warm, max_iter, check_every;
+    double fix_tol;                        // fixed nonants: box of half-width fix_tol max(1, |v|)
     double eps, sense;
     double beta_suf, beta_nec, beta_art;   // restart rule
     double theta;                          // primal weight smoothing (1: no smoothing)
@@ -193,6 +198,17 @@ __device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, double& cc, 
             pc += 0.5 * p * z * z;
         }
     }
+}
+
+// scaled box of a fixed nonant t (x = d xhat): [v - w, v + w] / d with w = fix_tol max(1, |v|) --
+// 0 fixes exactly; a small positive tolerance plays the part of a CPU solver's primal feasibility
+// tolerance when a candidate from a first-order solve meets a first-stage row only to ~1e-10
+// (phg_opts.fix_tol)
+__device__ __forceinline__ void fixed_box(const PdhgArgs& a, long t, double d, double& lo, double& hi) {
+    const double v = a.fixed[t];
+    const double w = a.fix_tol * fmax(1.0, fabs(v));
+    lo = (v - w) / d;
+    hi = (v + w) / d;
 }
 
 // PDLP primal weight update at a restart: omega <- (dy/dx)^theta omega^(1-theta), from the squared

@@ -120,8 +120,11 @@ class LagrangianOuterBound(_BoundSpoke):
         return True
 
     def _collect(self):
+        # the PDHG dual objective is a valid Lagrangian bound only where the solve reached the KKT
+        # tolerance: an iteration-limited (status 1) or failed (2) scenario's dual iterate can be
+        # infeasible, and its "bound" could overshoot -- then this spoke reports nothing this round
         st = self.engine.get_i32(_lib.I_STATUS)
-        ok = float((st == 2).sum() == 0)
+        ok = float((st != 0).sum() == 0)
         if self.hub_opt.n_proc > 1:
             ok = float(self.hub_opt.mpicomm.allreduce_scalar(1.0 - ok) == 0.0)
         if not ok:
@@ -153,6 +156,9 @@ class XhatShuffleInnerBound(_BoundSpoke):
         self.best_X = None           # local scenarios x n: the incumbent's full solution
         # an infeasible fixing would run PDHG to its cap: tries use a smaller one
         self.max_iter = int(self.options.get("xhat_max_iter", 20000))
+        # fixed values get a box of half-width xhat_fix_tol * max(1, |v|) (phg_opts.fix_tol): the
+        # CPU solver's feasibility tolerance of the reference's exact fixing
+        self.fix_tol = float(self.options.get("xhat_fix_tol", 1e-9))
 
     def _candidate_row(self, gidx):
         """Nonants of global scenario gidx from the hub (host vector; summed over ranks)."""
@@ -179,7 +185,7 @@ class XhatShuffleInnerBound(_BoundSpoke):
         o = self._solve_opts()
         self.engine.solve(0, 0, eps=o["pdhg_eps"], max_iter=min(self.max_iter, o["pdhg_max_iter"]),
                           check_every=o["pdhg_check_every"], warm_start=1 if self.launches else 0,
-                          fix_nonants=True, schedule=o["pdhg_schedule"])
+                          fix_nonants=True, schedule=o["pdhg_schedule"], fix_tol=self.fix_tol)
         return True
 
     def _collect(self):
@@ -197,6 +203,76 @@ class XhatShuffleInnerBound(_BoundSpoke):
             self.best_candidate = self.current
             self.best_X = self.engine.get(_lib.F_X).reshape(self.engine.S, -1)
         return val
+
+
+def evaluate_xhat(opt, xhat, eps=None, max_iter=200000, fix_tol=1e-9):
+    """Inner bound of a two-stage candidate (``xhat_eval.py:102-170`` / ``xhatbase.py:42-235``):
+    every local scenario's nonants fixed to ``xhat`` (one vector, node order), W and prox off, one
+    batched solve on a temporary handle holding ``opt``'s batch; sum_s p_s obj_s (math.fsum per
+    rank, SUM across ranks) if every scenario reached the KKT tolerance, else None."""
+    he = opt.engine
+    if he.batch.L != 1:
+        raise NotImplementedError("evaluate_xhat: two-stage batches")
+    dev = 0
+    try:
+        import torch
+        if torch.cuda.is_available():
+            dev = torch.cuda.current_device()
+    except ImportError:
+        pass
+    eng = Engine(he.batch, device=dev, stream=None, exchange=None,
+                 layout=opt.options.get("pdhg_layout", "auto"), presolve=opt.options.get("pdhg_presolve", True))
+    try:
+        eng.set(_lib.F_FIXED, np.tile(np.asarray(xhat, np.float64), eng.S))
+        o = opt._solver_opts()
+        eng.solve(0, 0, eps=eps or o["pdhg_eps"], max_iter=max_iter, check_every=o["pdhg_check_every"],
+                  warm_start=0, fix_nonants=True, schedule=False, fix_tol=fix_tol)
+        eng.sync()
+        st = eng.get_i32(_lib.I_STATUS)
+        evaluate_xhat.last_status_counts = np.bincount(st, minlength=3).tolist()
+        bad = float((st != 0).sum())
+        if opt.n_proc > 1:
+            bad = opt.mpicomm.allreduce_scalar(bad)
+        if bad:
+            return None
+        obj = eng.get(_lib.F_OBJ)
+        p = eng.batch.prob
+        return opt._rank_fsum([p[k] * obj[k] for k in range(len(obj))])
+    finally:
+        eng.close()
+
+
+def evaluate_lagrangian(opt, eps=None, max_iter=200000):
+    """Lagrangian outer bound with ``opt``'s current W (``lagrangian_bounder.py:21-44``): every
+    local scenario with W on and prox off, one batched solve on a temporary handle; sum_s p_s
+    bound_s (the PDHG dual objective, valid at KKT-optimal points), or None if any scenario did
+    not reach the tolerance."""
+    he = opt.engine
+    dev = 0
+    try:
+        import torch
+        if torch.cuda.is_available():
+            dev = torch.cuda.current_device()
+    except ImportError:
+        pass
+    eng = Engine(he.batch, device=dev, stream=None, exchange=None,
+                 layout=opt.options.get("pdhg_layout", "auto"), presolve=opt.options.get("pdhg_presolve", True))
+    try:
+        eng.copy_from(he, _lib.F_W)
+        o = opt._solver_opts()
+        eng.solve(1, 0, eps=eps or o["pdhg_eps"], max_iter=max_iter, check_every=o["pdhg_check_every"],
+                  warm_start=0, schedule=False)
+        eng.sync()
+        bad = float((eng.get_i32(_lib.I_STATUS) != 0).sum())
+        if opt.n_proc > 1:
+            bad = opt.mpicomm.allreduce_scalar(bad)
+        if bad:
+            return None
+        b = eng.get(_lib.F_BOUND)
+        p = eng.batch.prob
+        return opt._rank_fsum([p[k] * b[k] for k in range(len(b))])
+    finally:
+        eng.close()
 
 
 def spoke_from_dict(hub_opt, spoke_dict):

@@ -152,7 +152,14 @@ class Engine:
         _lib.check(self.lib.phg_load_batch(self.h, ctypes.byref(b)))
         del keep
         self.S, self.N, self.N_tot, self.P = batch.S, batch.N, batch.N_tot, batch.virt_nproc
-        self.exchange = exchange            # (nodesum tensor, convpart tensor) for multi-GPU, or None
+        # multi-GPU: ONE packed device tensor [2 N_tot node sums | 2P+2 partials | flag]
+        # (include/phg.h, phg_exchange_layout) all-reduced by the communicator; None on one GPU
+        self.exchange = exchange
+        lay = np.zeros(3, np.int32)
+        _lib.check(self.lib.phg_exchange_layout(self.h, ptr(lay)))
+        self.exchange_len = int(lay[2])
+        if exchange is not None and int(exchange.numel()) != self.exchange_len:
+            raise ValueError(f"exchange buffer has {exchange.numel()} doubles, the batch needs {self.exchange_len}")
         info = np.zeros(8, np.int32)
         _lib.check(self.lib.phg_info(self.h, ptr(info)))
         self.variant = int(info[6])
@@ -199,28 +206,48 @@ class Engine:
 
     # ------------------------------------------------------------------ hot path
     def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=32, warm_start=3,
-              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0), theta=0.0, skip_below=0.0):
+              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0), theta=0.0, skip_below=0.0, fix_tol=0.0):
         o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(warm_start),
                          int(bool(fix_nonants)), int(bool(schedule)), *[float(v) for v in beta],
-                         float(theta), float(skip_below))
+                         float(theta), float(skip_below), float(fix_tol))
         import ctypes
         _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))
 
     def sync(self):
         _lib.check(self.lib.phg_sync(self.h))
 
+    # views of the packed exchange buffer (multi-GPU)
+    @property
+    def nodesum_view(self):
+        return None if self.exchange is None else self.exchange[: 2 * self.N_tot]
+
+    @property
+    def convpart_view(self):
+        return None if self.exchange is None else self.exchange[2 * self.N_tot:]
+
+    def _ns_ptr(self):
+        return None if self.exchange is None else self.exchange.data_ptr()
+
+    def _cp_ptr(self):
+        return None if self.exchange is None else self.exchange.data_ptr() + 8 * 2 * self.N_tot
+
     def node_sums(self):
-        dev = None if self.exchange is None else self.exchange[0].data_ptr()
-        _lib.check(self.lib.phg_node_sums(self.h, dev))
+        _lib.check(self.lib.phg_node_sums(self.h, self._ns_ptr()))
 
     def apply_xbar(self):
-        ns = None if self.exchange is None else self.exchange[0].data_ptr()
-        cp = None if self.exchange is None else self.exchange[1].data_ptr()
-        _lib.check(self.lib.phg_apply_xbar(self.h, ns, cp))
+        _lib.check(self.lib.phg_apply_xbar(self.h, self._ns_ptr(), self._cp_ptr()))
+
+    def ph_head(self, convthresh, first):
+        """Gated W update of the pipelined iteration (phg_ph_head): conv of the previous update from
+        the exchanged partials; unless it is below ``convthresh``, xbar / W / this update's partials."""
+        _lib.check(self.lib.phg_ph_head(self.h, self._ns_ptr(), float(convthresh), int(bool(first))))
+
+    def solve_undo(self):
+        """Restore the solve state from before the last solve (phg_solve_undo)."""
+        _lib.check(self.lib.phg_solve_undo(self.h))
 
     def conv_start(self):
-        cp = None if self.exchange is None else self.exchange[1].data_ptr()
-        _lib.check(self.lib.phg_conv_start(self.h, cp))
+        _lib.check(self.lib.phg_conv_start(self.h, self._cp_ptr()))
 
     def conv_wait(self):
         import ctypes
@@ -231,8 +258,7 @@ class Engine:
     def conv_finish(self):
         import ctypes
         v = ctypes.c_double()
-        cp = None if self.exchange is None else self.exchange[1].data_ptr()
-        _lib.check(self.lib.phg_conv_finish(self.h, cp, ctypes.byref(v)))
+        _lib.check(self.lib.phg_conv_finish(self.h, self._cp_ptr(), ctypes.byref(v)))
         return v.value
 
     def copy_from(self, src, field):

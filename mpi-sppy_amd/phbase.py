@@ -14,8 +14,9 @@ go through the communicator (RCCL).  Nothing of size S x n crosses PCIe inside t
 iteration reads back one convergence scalar (2 x virtual-rank doubles).
 
 Documented deviations: per-subproblem extension hooks ``pre_solve``/``post_solve`` cannot run
-inside a batched launch (``pre_solve_loop``/``post_solve_loop`` do);
-``linearize_proximal_terms``, bundles and ``variable_probability`` are not supported yet.
+inside a batched launch (``pre_solve_loop``/``post_solve_loop`` do); ``linearize_proximal_terms``
+raises (the kernels solve the exact prox QP).  ``variable_probability`` (``prob_coeff`` per nonant,
+``prob0_mask``) and smoothed PH are supported.
 """
 import math
 import time
@@ -119,9 +120,9 @@ class PHBase(SPBase):
             if torch.cuda.is_available():
                 device = torch.cuda.current_device() if "device" not in self.options else device
                 stream = torch.cuda.current_stream(device).cuda_stream
-                if self.n_proc > 1:
-                    exchange = (torch.zeros(2 * batch.N_tot, dtype=torch.float64, device=f"cuda:{device}"),
-                                torch.zeros(2 * batch.virt_nproc + 2, dtype=torch.float64, device=f"cuda:{device}"))
+                if self.n_proc > 1:   # one packed buffer, one all-reduce per pipelined iteration
+                    exchange = torch.zeros(2 * batch.N_tot + 2 * batch.virt_nproc + 3, dtype=torch.float64,
+                                           device=f"cuda:{device}")
         except ImportError:
             pass
         return device, stream, exchange
@@ -224,6 +225,7 @@ class PHBase(SPBase):
     def _check_status_now(self, gripe, need_solution):
         """Per-scenario statuses of the last solve (synchronous; spopt.py:194-231 semantics)."""
         status = self.engine.get_i32(_lib.I_STATUS)
+        self._status = status
         self._feasible = status != 2
         self._status_pending = None
         if gripe and (status != 0).any():
@@ -252,7 +254,7 @@ class PHBase(SPBase):
         """``phbase.py:32-112``: node sums on the device, SUM across ranks (RCCL)."""
         self.engine.node_sums()
         if self.engine.exchange is not None:
-            self.mpicomm.allreduce_sum_(self.engine.exchange[0])
+            self.mpicomm.allreduce_sum_(self.engine.nodesum_view)
         self._xbar_pending = True
 
     def Update_W(self, verbose=False):
@@ -268,7 +270,7 @@ class PHBase(SPBase):
     def convergence_diff(self):
         """``phbase.py:349-371``: mean over (virtual) ranks of the per-rank mean |x - xbar|."""
         if self.engine.exchange is not None:
-            self.mpicomm.allreduce_sum_(self.engine.exchange[1])
+            self.mpicomm.allreduce_sum_(self.engine.convpart_view)
         conv = self.engine.conv_finish()
         self._check_status_summary()
         return conv
@@ -276,45 +278,96 @@ class PHBase(SPBase):
     def _can_pipeline(self):
         """The pipelined iteration (:meth:`update_and_solve`) enqueues the solve before the host
         has seen conv, so nothing may act between convergence_diff and solve_loop: no extension
-        (miditer), no converger object, no time limit, no per-solve timing."""
+        (miditer), no converger object, no per-solve timing.  (A time limit is checked before the
+        solve is enqueued, see :meth:`iterk_loop`.)"""
         o = self.options
-        return (self.extobject is None and self.ph_converger is None and o.get("time_limit") is None
+        return (self.extobject is None and self.ph_converger is None
                 and not o.get("display_timing", False) and o.get("pdhg_pipeline", True))
 
-    def update_and_solve(self, verbose=False):
-        """One PH iteration k >= 1 -- Compute_Xbar, Update_W, convergence_diff and, unless
-        conv < convthresh, solve_loop (``phbase.py:990-1035``) -- with one host synchronisation that
-        overlaps the solve: conv is computed on the device, the solve is enqueued gated on it
-        (``phg_opts.skip_if_conv_below``: a no-op when PH has converged, exactly the reference's
-        break before solve_loop), and only then does the host wait for conv.  Returns conv."""
-        self.Compute_Xbar(verbose)
-        self.Update_W(verbose)
-        if self.engine.exchange is not None:
-            self.mpicomm.allreduce_sum_(self.engine.exchange[1])
-        self.engine.conv_start()
-        pending = getattr(self, "_status_pending", None)
+    def update_and_solve(self, verbose=False, first=False):
+        """One pipelined PH iteration k with ONE all-reduce (include/phg.h, phg_ph_head).
+
+        The device runs: node sums of x_{k-1} into the packed exchange buffer; one SUM across GPUs
+        of [node sums | partials of update k-1]; conv_{k-1} from those partials; and, unless
+        conv_{k-1} < convthresh, Compute_Xbar / Update_W of iteration k and its partials; then
+        solve_loop k, gated on conv_{k-1} too.  The host waits for conv_{k-1} only, while update k
+        and solve k run.  So the solve is speculative by one iteration: conv_{k-1} < convthresh
+        means the reference broke at iteration k-1 BEFORE solve k-1 (``phbase.py:1008-1010``);
+        the device has skipped update k and solve k, and with the double-buffered solve state
+        (a gated solve writes nothing) the state is the one before solve k-1.
+
+        Returns conv_{k-1} (+inf when ``first``: no update precedes iteration 1)."""
+        eng = self.engine
         thr = float(self.options["convthresh"])
+        eng.node_sums()
+        if eng.exchange is not None:
+            self.mpicomm.allreduce_sum_(eng.exchange)
+        eng.ph_head(thr, first)
         self.solve_loop(solver_options=self.current_solver_options, gripe=verbose, verbose=verbose,
                         skip_below=thr if thr > 0 else 0.0)
-        launched = self._status_pending
-        self._status_pending = pending
-        conv = self.engine.conv_wait()
-        self._check_status_summary()          # statuses of the PREVIOUS solve, as convergence_diff
-        if conv < thr:                        # the gated solve did nothing on the device
-            self.solve_count -= self.engine.S
-            self._status_pending = None
-        else:
-            self._status_pending = launched
+        self._spec_pending = True
+        conv = eng.conv_wait()
+        if not first:
+            # statuses of the solve that preceded update k-1 (they ride with its partials)
+            n_bad, n_nan = eng.solve_summary()
+            if verbose and n_bad and self.cylinder_rank == 0:
+                print(f"[{self.__class__.__name__}] {n_bad} subproblem(s) did not reach the KKT tolerance")
+            if n_nan:
+                raise RuntimeError(f"PDHG numerical failure (NaN) in {n_nan} subproblem(s)")
+        if conv < thr:
+            # solve k did nothing and solve k-1 is undone (its state swap is reverted by solve k's)
+            self.solve_count -= 2 * eng.S
+            self._spec_pending = False
         return conv
+
+    def _drain_speculation(self):
+        """Finish the pipeline: conv of the last pipelined update (the partials not yet exchanged)
+        and, if PH had converged before the solve that followed it, undo that solve.  Returns
+        (conv, undone)."""
+        eng = self.engine
+        if eng.exchange is not None:
+            self.mpicomm.allreduce_sum_(eng.convpart_view)
+        conv = eng.conv_finish()
+        self._spec_pending = False
+        if eng.solve_summary()[1]:
+            raise RuntimeError(f"PDHG numerical failure (NaN) in {eng.solve_summary()[1]} subproblem(s)")
+        if conv < float(self.options["convthresh"]):
+            eng.solve_undo()
+            self.solve_count -= eng.S
+            self._status_pending = (False, True)    # the front solve state changed: refetch statuses
+            return conv, True
+        return conv, False
+
+    def _time_over(self):
+        if self.options["time_limit"] is None:
+            return False
+        over = (time.perf_counter() - self.start_time) >= self.options["time_limit"]
+        if self.n_proc > 1:
+            over = self.mpicomm.allreduce_scalar(float(over)) > 0
+        return over
 
     # ------------------------------------------------------------------------------- expectations
     def _rank_fsum(self, vals):
         local = math.fsum(vals)
         return self.mpicomm.allreduce_scalar(local) if self.n_proc > 1 else local
 
-    def Ebound(self, verbose=False, extra_sum_terms=None):
-        """``spopt.py:377-422`` (outer bound = the solver's dual bound)."""
+    def _valid_bounds(self):
+        """Per-scenario outer bounds of the last solve, model sense.  The PDHG dual objective is a
+        valid bound only at a KKT-optimal point (status 0): at an iteration-limited or failed
+        scenario the dual iterate may be infeasible on infinite-bound columns, so its bound is
+        replaced by the trivial one (-inf when minimising, +inf when maximising), as a solver that
+        reports no Lower_bound would leave it (spopt.py:225-230)."""
         b = self.engine.get(_lib.F_BOUND)
+        self._statuses()
+        bad = self._status != 0
+        if bad.any():
+            b = b.copy()
+            b[bad] = -math.inf if self.is_minimizing else math.inf
+        return b
+
+    def Ebound(self, verbose=False, extra_sum_terms=None):
+        """``spopt.py:377-422`` (outer bound = the solver's dual bound, see :meth:`_valid_bounds`)."""
+        b = self._valid_bounds()
         p = self.engine.batch.prob
         vals = [p[k] * b[k] for k in range(len(b))]
         if extra_sum_terms is None:
@@ -336,8 +389,8 @@ class PHBase(SPBase):
         self.E1 = self._rank_fsum(list(self.engine.batch.prob))
 
     def _statuses(self):
-        if getattr(self, "_status_pending", None) is not None:
-            self._check_status_now(*self._status_pending)
+        if getattr(self, "_status_pending", None) is not None or not hasattr(self, "_status"):
+            self._check_status_now(*(getattr(self, "_status_pending", None) or (False, True)))
         return self._feasible
 
     def feas_prob(self):
@@ -444,35 +497,52 @@ class PHBase(SPBase):
         self.engine.set(_lib.F_RHO, rho.ravel())
 
     def iterk_loop(self):
-        """``phbase.py:949-1061``."""
+        """``phbase.py:949-1061``.  With :meth:`_can_pipeline`, iteration k runs as
+        :meth:`update_and_solve` (one host synchronisation, one all-reduce, the solve speculative
+        by one iteration; every break leaves exactly the reference's state: see
+        :meth:`_drain_speculation`), otherwise statement by statement."""
         verbose = self.options["verbose"]
         dprogress = self.options["display_progress"]
+        thr = self.options["convthresh"]
         self.conv = None
         max_iterations = int(self.options["PHIterLimit"])
         self.conv_history = []
         pipelined = self._can_pipeline()
+        self._spec_pending = False
         for self._PHIter in range(1, max_iterations + 1):
             iteration_start_time = time.time()
-            if pipelined:   # same statements, the solve already enqueued (gated on conv)
-                self.conv = self.update_and_solve(verbose)
+            if pipelined and self.options["time_limit"] is not None and self._time_over():
+                # leave the pipeline before enqueueing: settle the previous iteration first, then
+                # run this one statement by statement (its own time check breaks below)
+                if self._spec_pending:
+                    c, undone = self._drain_speculation()
+                    if undone:
+                        self._PHIter -= 1
+                        self.conv = c
+                        self.conv_history.append(c)
+                        break
+                pipelined = False
+            if pipelined:
+                c = self.update_and_solve(verbose, first=self._PHIter == 1)
+                if self._PHIter > 1:
+                    self.conv = c
+                    self.conv_history.append(c)
+                    if c < thr:
+                        self._PHIter -= 1       # the reference broke at the previous iteration
+                        break
             else:
                 self.Compute_Xbar(verbose)
                 self.Update_W(verbose)
                 self.conv = self.convergence_diff()
-            self.conv_history.append(self.conv)
-            if self.extobject is not None:
-                self.extobject.miditer()
-            if self.ph_converger is not None and self.convobject.is_converged():
-                break
-            if self.conv is not None and self.conv < self.options["convthresh"]:
-                break
-            if self.options["time_limit"] is not None:
-                over = (time.perf_counter() - self.start_time) >= self.options["time_limit"]
-                if self.n_proc > 1:
-                    over = self.mpicomm.allreduce_scalar(float(over)) > 0
-                if over:
+                self.conv_history.append(self.conv)
+                if self.extobject is not None:
+                    self.extobject.miditer()
+                if self.ph_converger is not None and self.convobject.is_converged():
                     break
-            if not pipelined:
+                if self.conv is not None and self.conv < thr:
+                    break
+                if self._time_over():
+                    break
                 self.solve_loop(solver_options=self.current_solver_options, dtiming=self.options["display_timing"],
                                 gripe=verbose, verbose=verbose)
             if self.extobject is not None:
@@ -491,6 +561,10 @@ class PHBase(SPBase):
                 print("Elapsed time:   %6.2f" % (time.perf_counter() - self.start_time))
         else:
             self.mpicomm.Barrier()
+        if self._spec_pending:      # PHIterLimit or the hub ended a pipelined loop
+            c, _undone = self._drain_speculation()
+            self.conv = c
+            self.conv_history.append(c)
 
     def post_loops(self, extensions=None):
         """``phbase.py:1064-1119``."""

@@ -162,9 +162,23 @@ class SPBase:
             for nd in s._mpisppy_node_list:
                 v = np.full(s._mpisppy_data.nlens[nd.name], 0.0) + s._mpisppy_data.prob_coeff[nd.name]
                 sums[nd.name] = sums.get(nd.name, 0.0) + v
-        for ndn in sorted(sums):
-            tot = np.asarray(self.mpicomm.allreduce_array(np.asarray(sums[ndn], dtype="d"))) \
-                if self.n_proc > 1 else sums[ndn]
+        # ranks own different nodes of a multistage tree: ONE reduction over a vector laid out over
+        # the union of every rank's nodes (the reference has one communicator per node instead),
+        # so every rank makes the same collective call with the same length
+        lens = {k: len(v) for k, v in sums.items()}
+        if self.n_proc > 1:
+            for d in self.mpicomm.allgather_object(lens):
+                lens.update(d)
+        names = sorted(lens)
+        off = np.concatenate([[0], np.cumsum([lens[k] for k in names])]).astype(int)
+        flat = np.zeros(int(off[-1]))
+        for i, k in enumerate(names):
+            if k in sums:
+                flat[off[i]:off[i + 1]] = sums[k]
+        if self.n_proc > 1:
+            flat = np.asarray(self.mpicomm.allreduce_array(flat))
+        for i, ndn in enumerate(names):
+            tot = flat[off[i]:off[i + 1]]
             if not np.allclose(tot, 1.0, atol=self.E1_tolerance):
                 bad = np.nonzero(~np.isclose(tot, 1.0, atol=self.E1_tolerance))[0]
                 raise RuntimeError(f"Node {ndn}, variables indexed {bad.tolist()} have unconditional "

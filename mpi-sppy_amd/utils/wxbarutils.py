@@ -98,7 +98,11 @@ def _check_W(w_val_dict, PHB, rank):
             print("Removing unknown variables:", ", ".join(sorted(extra)))
             for v in extra:
                 provided.pop(v, None)
-    names = sorted(set().union(*[_nonant_names(s) for s in PHB.local_scenarios.values()]))
+    names = set().union(*[_nonant_names(s) for s in PHB.local_scenarios.values()])
+    if PHB.n_proc > 1:   # multistage ranks see different nonant names: reduce over their union
+        for other in PHB.comms["ROOT"].allgather_object(sorted(names)):
+            names.update(other)
+    names = sorted(names)
     local = np.array([sum(s._mpisppy_probability * w_val_dict[sn].get(v, 0.0)
                           for sn, s in PHB.local_scenarios.items()) for v in names])
     dual = PHB.comms["ROOT"].allreduce_array(local) if PHB.n_proc > 1 else local

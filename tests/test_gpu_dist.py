@@ -1,5 +1,5 @@
-"""Multi-rank bench path on the one-GPU box: ``bench.py`` under ``torch.distributed.run`` with two
-ranks sharing cuda:0 over the gloo backend (the device exchange buffers are all-reduced through
+"""Multi-rank bench path on the one-GPU box: ``bench.py --gpus 2`` (which starts
+``torch.distributed.run`` on itself) with two ranks sharing cuda:0 over the gloo backend (the device exchange buffers are all-reduced through
 host staging; the 8-GPU RCCL run is the driver's).  The 2-rank run shards 2x500 farmer scenarios
 with the reference's slicing; its PH trajectory must match a 1-rank run of the same 1000 scenarios
 (conv to 1e-9 relative: only the node-sum summation order differs)."""
@@ -31,10 +31,10 @@ def _run(cmd, env):
 def test_two_ranks_match_one_rank():
     env = dict(os.environ, PHG_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     one = _run([sys.executable, "bench.py", "--scen", "1000"] + ARGS, env)
-    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                "--master-addr", "127.0.0.1", "--master-port", "29531", "bench.py", "--gpus", "2",
-                "--scen", "500"] + ARGS, env)
+    # bench.py starts torch.distributed.run on itself for --gpus 2 (the driver's N-GPU command)
+    two = _run([sys.executable, "bench.py", "--gpus", "2", "--scen", "500"] + ARGS, env)
     assert two["n_gpus"] == 2 and two["config"]["scenarios"] == 1000
+    assert len(two["per_rank"]["pdhg_ms_per_step"]) == 2
     assert one["config"]["scenarios"] == 1000
     assert two["value"] > 0
     c1, c2 = one["conv_at_end"], two["conv_at_end"]

@@ -1,0 +1,89 @@
+"""The north-star target on the GPU: "farmer with 10k scenarios reaches PH convergence < 1e-4 with
+objective within 1e-6 of the reference" (BASELINE.json).
+
+The reference's answer for the instance is its extensive-form optimum (``create_EF``,
+``mpisppy/utils/sputils.py:143-357``; the farmer EF objective -108390 of ``doc/src/examples.rst:382``
+is the cm=1 S=3 case, pinned in ``tests/test_oracle_pins.py``).  The EF optima of farmer
+crops_multiplier=10 with 30 / 1 000 / 10 000 scenarios are committed fixtures
+(``tests/golden/make_ef_fixtures.py``: the oracle's restated scenario LPs stacked into the EF and
+solved by HiGHS 1.8 IPM + crossover).  The product runs PH (eps 1e-9 prox-QP solves, rho = 1, the
+bench's options) to conv < 1e-4 through the C ABI, then:
+
+* E[objective] with W and prox on (``ph_main``'s Eobj, ``opt/ph.py:76``) within 1e-6 relative of
+  the EF optimum;
+* the converged root xbar fixed in every scenario (the xhat evaluation, ``xhat_eval.py:102-170``)
+  gives an inner bound >= EF - 1e-7 relative (first-order solves at eps 1e-9) and within 1e-6;
+* the Lagrangian bound with the converged W (``lagrangian_bounder.py:21-44``) <= EF + 1e-7
+  relative and within 1e-6 (outer <= EF <= inner: the gap closes);
+* the converged xbar against the EF's first-stage solution (reported; asserted loosely: the EF
+  optimum's first stage need not be unique).
+
+And against the oracle's own PH to convergence on S = 30 (``oracle_ph_farmer_cm10_S30.json``):
+E[obj] within 1e-6 relative.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from mpisppy_amd import cylinders  # noqa: E402
+from mpisppy_amd.examples import farmer  # noqa: E402
+from mpisppy_amd.ph import PH  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _fixture(name):
+    fn = os.path.join(GOLD, name)
+    if not os.path.exists(fn):
+        pytest.skip(f"fixture {name} not generated (tests/golden/make_ef_fixtures.py)")
+    return json.load(open(fn))
+
+
+def _converged_ph(S, cm=10):
+    opts = {"solver_name": "phg", "PHIterLimit": 20000, "defaultPHrho": 1.0, "convthresh": 1e-4,
+            "verbose": False, "display_progress": False,
+            "iter0_solver_options": {"pdhg_eps": 1e-9}, "iterk_solver_options": {"pdhg_eps": 1e-9}}
+    ph = PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator,
+            scenario_creator_kwargs={"crops_multiplier": cm, "num_scens": S})
+    conv, eobj, tb = ph.ph_main()
+    return ph, conv, eobj, tb
+
+
+@pytest.mark.parametrize("S", [30, 1000, 10000])
+def test_farmer_converged_ph_vs_ef(S):
+    ef = _fixture(f"farmer_cm10_ef_S{S}.json")
+    assert ef["status"] == "Optimal"
+    ph, conv, eobj, tb = _converged_ph(S)
+    efo = ef["objective"]
+    assert conv < 1e-4 and ph._PHIter < 20000
+    rel = abs(eobj - efo) / abs(efo)
+    xhat = ph.xbars()[:30]
+    inner = cylinders.evaluate_xhat(ph, xhat)
+    outer = cylinders.evaluate_lagrangian(ph)
+    dx = float(np.max(np.abs(xhat - np.array(ef["root_nonants"]))))
+    print(f"\nS={S}: PH iters {ph._PHIter}, conv {conv:.3e}, Eobj {eobj:.6f}, EF {efo:.6f} (rel {rel:.2e}), "
+          f"inner {inner} ({(inner - efo) / abs(efo):.2e}), outer {outer} ({(outer - efo) / abs(efo):.2e}), "
+          f"max |xbar - x_EF| {dx:.3e}")
+    assert rel <= 1e-6
+    assert tb <= efo                                   # the trivial bound is an outer bound
+    assert inner is not None and -1e-7 <= (inner - efo) / abs(efo) <= 1e-6
+    assert outer is not None and -1e-6 <= (outer - efo) / abs(efo) <= 1e-7
+    assert dx <= 1.0                                    # acres; reported above at full precision
+
+
+def test_farmer_converged_ph_vs_oracle_ph():
+    """Against the oracle's PH to conv < 1e-4 on the same instance (farmer cm=10, S=30)."""
+    ref = _fixture("oracle_ph_farmer_cm10_S30.json")
+    ph, conv, eobj, tb = _converged_ph(30)
+    assert conv < 1e-4 and ref["conv"] < 1e-4
+    assert abs(eobj - ref["Eobj"]) <= 1e-6 * abs(ref["Eobj"]), (eobj, ref["Eobj"])
+    assert abs(tb - ref["trivial_bound"]) <= 1e-6 * abs(ref["trivial_bound"])
+    np.testing.assert_allclose(ph.xbars()[:30], ref["xbar"], atol=0.5)

@@ -149,6 +149,44 @@ def test_prox_qp_solves_vs_oracle(S, cm, layout):
         np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6)
 
 
+@pytest.mark.parametrize("layout", ["gather", "block"])
+@pytest.mark.parametrize("tree", ["bf33", (2, 1, 4), (5, 15, 30)])
+def test_hydro_prox_qp_solves_vs_oracle(tree, layout):
+    """Multistage prox-QPs with identical W and per-NODE xbar in both solvers (the xbar slot of each
+    nonant comes from its scenario's node at that stage, xidx): strictly convex in x_N, so the
+    nonants are unique -- 1e-6 -- and so are the objectives (1e-6).  Covers the uniform 3x3 tree of
+    the reference (hydro.py) and non-uniform synthetic trees."""
+    if tree == "bf33":
+        bf = [3, 3]
+        names, nodenames = hydro.scenario_names_creator(9), create_nodenames_from_branching_factors(bf)
+        ph = PH(_opts(pdhg_layout=layout), names, hydro.scenario_creator, all_nodenames=nodenames,
+                scenario_creator_kwargs={"branching_factors": bf})
+        o = oph.OraclePH(_opts(PHIterLimit=3), om.hydro_names(9), om.hydro, {})
+    else:
+        S = sum(tree)
+        kw = {"fanouts": tree}
+        nodenames = hydro.synthetic_nodenames(tree)
+        ph = PH(_opts(pdhg_layout=layout), hydro.scenario_names_creator(S), hydro.synthetic_scenario_creator,
+                all_nodenames=nodenames, scenario_creator_kwargs=kw)
+        o = oph.OraclePH(_opts(PHIterLimit=3), om.hydro_names(S), om.hydro_tree, kw)
+    ph.PH_Prep()
+    ph.Iter0()
+    o.Iter0()
+    S = o.S
+    for it in range(3):
+        o.Compute_Xbar()
+        o.Update_W()
+        ph.engine.set(_lib.F_W, o.W.ravel())
+        ph.engine.set(_lib.F_XBAR, np.concatenate([o.node_xbar[nd] for nd in nodenames]))
+        ph.solve_loop()
+        o.solve_loop()
+        assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+        xg = ph.nonants()
+        xo = np.array([o.nonants(k) for k in range(S)])
+        np.testing.assert_allclose(xg, xo, rtol=1e-6, atol=1e-6 * max(1.0, np.abs(xo).max()))
+        np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6, atol=1e-6)
+
+
 # ----------------------------------------------------------------------------- full PH vs fixtures
 def test_w_and_xbar_fixtures_farmer3():
     """Reference fixture: W / xbar after 5 PH iterations (test_w_writer.py:83-112)."""
