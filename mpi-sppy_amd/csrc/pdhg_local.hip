@@ -14,6 +14,8 @@
 //
 // So one PDHG iteration is ~100 fp64 VALU instructions and one short DPP chain per wave, with no
 // memory traffic at all between the prologue (load the scenario) and the epilogue (store x, y).
+#include <algorithm>
+
 #include "phg_internal.h"
 #include "wave_ops.h"
 
@@ -40,7 +42,20 @@ struct Cold {
     static_assert(N == cold_items(CPL, RPL, D), "cold layout");
 };
 
-template <int LPS, int CPL, int RPL, int D>
+// PERSIST: a persistent grid (as many waves as are resident) in which every lane group takes its
+// next scenario from a device work queue (a.queue, in launch order: heaviest first) as soon as its
+// current one has terminated -- so the two scenarios sharing a wave no longer run until the slower
+// of them finishes, and there is no tail of late-starting waves.  A group reloads at a check
+// boundary (the other group of its wave waits for that prologue: a few global loads).  !PERSIST:
+// one work item per group, grid = items / G (the round-1 kernel).
+//
+// MB / MC: the block slots (bit r*CPL + k) and coupling slots (bit d*CPL + k) that hold an entry in
+// at least one lane (computed on the host from the layout; all ones = the generic kernel).  A slot
+// empty in every lane is dropped at compile time -- its register and its multiply-by-zero FMA in
+// A x, A^T y and the check's products (farmer: 8 of 24 per iteration; every crop's lane has the
+// same 4-column / 2-row block pattern and one coupling entry).  The sums are bit-identical to the
+// generic kernel's (the dropped terms are fma(0, v, acc) = acc).
+template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC>
 __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
     constexpr int G = 64 / LPS;                    // scenarios per wave
@@ -50,138 +65,80 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
     const int lane = threadIdx.x;
     auto CS = [&](int item) -> double& { return cold[item * 64 + lane]; };
     const int gl = lane % LPS;                     // lane inside the scenario's group
-    const int w_raw = blockIdx.x * G + lane / LPS;  // work item
-    const bool valid = w_raw < a.S;
-    const int w = valid ? w_raw : a.S - 1;         // a tail group mirrors the last item, writes nothing
-    const int s = a.order ? a.order[w] : w;        // scenario of this work item
+    const int grp = lane / LPS;
     const LocalLayout& L = a.loc;
     const int* col_nonant = a.lay.col_nonant;
-
-    // ------------------------------------------------------------------ columns of this lane
-    int cj[CPL];
     // the primal step is x+ = clamp(x ip + A^T y tip - ctip) with ip = 1 / (1 + tau q),
     // tip = tau ip, ctip = c tip (re-derived whenever tau changes; c itself is read from LDS):
     // 2 instead of 3 fp64 ops per column, for 2 more registers per column -- only where they
     // fit (the widest variants would spill; they keep x+ = clamp((x + tau (A^T y - c)) ip))
     constexpr bool FOLD = RPL * CPL + D * CPL <= 12;
+
+    // ------------------------------------------------------------------ per-group state
+    int s = 0;                                     // scenario of the group's current work item
+    int cj[CPL];
     double x[CPL], aty[CPL], c[CPL], lo[CPL], hi[CPL], ip[CPL], tip[CPL], ctip[CPL], xsum[CPL];
-    double prox_const = 0.0, c2 = 0.0;
-    {
-        const long sn = (long)s * a.n, sN = (long)s * a.N;
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-            seq();
-            const int j = L.col_of[gl * CPL + k];
-            cj[k] = j;
-            x[k] = aty[k] = c[k] = lo[k] = hi[k] = xsum[k] = 0.0;
-            double qs = 0.0;
-            CS(CI::IDC + k) = 1.0;
-            if (j >= 0) {
-                const long b = sn + j;
-                const double d = a.dc[b];
-                double cc = a.c[b], qq = 0.0;
-                double lo_ = a.cl[b], hi_ = a.cu[b];
-                const int kk = col_nonant[j];
-                if (kk >= 0) {
-                    const long t = sN + kk;
-                    ph_terms(a, t, cc, qq, prox_const);
-                    if (a.fix_nonants) fixed_box(a, t, d, lo_, hi_);
-                }
-                c2 += cc * cc;
-                CS(CI::IDC + k) = 1.0 / d;
-                c[k] = cc * d;
-                qs = qq * d * d;
-                lo[k] = lo_;
-                hi[k] = hi_;
-                x[k] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
-            }
-            CS(CI::XR + k) = x[k];
-            CS(CI::Q + k) = qs;
-        }
-    }
-    // ------------------------------------------------------------------ local rows + block
     double y[RPL], ax[RPL], rlo[RPL], rhi[RPL], ysum[RPL];
     double blk[RPL][CPL];
-    double b2 = 0.0;
-    {
-        const long sm = (long)s * a.m, snz = (long)s * a.nnz;
-#pragma unroll
-        for (int r = 0; r < RPL; ++r) {
-            seq();
-            const int i = L.row_of[gl * RPL + r];
-            y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
-            CS(CI::IDR + r) = 0.0;
-            if (i >= 0) {
-                const long b = sm + i;
-                CS(CI::IDR + r) = 1.0 / a.dr[b];
-                rlo[r] = a.rl[b];
-                rhi[r] = a.ru[b];
-                double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
-                if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
-                if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];
-                y[r] = yy;
-            }
-            CS(CI::YR + r) = y[r];
-            CS(CI::BLO + r) = rlo[r];
-            CS(CI::BHI + r) = rhi[r];
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-                const int p = L.blk_p[(gl * RPL + r) * CPL + k];
-                blk[r][k] = p >= 0 ? a.vals[snz + p] : 0.0;
-            }
-        }
-    }
-    // ------------------------------------------------------------------ coupling rows (replicated)
     double yd[DD], axd[DD], dlo[DD], dhi[DD], ydsum[DD];
     double cf[DD][CPL];
-    double b2d = 0.0;
-    {
-        const long sm = (long)s * a.m, snz = (long)s * a.nnz;
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            seq();
-            const int i = L.cpl_row[d];
-            yd[d] = axd[d] = dlo[d] = dhi[d] = ydsum[d] = 0.0;
-            CS(CI::IDRD + d) = 0.0;
-            if (i >= 0) {
-                const long b = sm + i;
-                CS(CI::IDRD + d) = 1.0 / a.dr[b];
-                dlo[d] = a.rl[b];
-                dhi[d] = a.ru[b];
-                double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
-                if (!fin(dlo[d])) yy = fmin(yy, 0.0); else b2d += dlo[d] * dlo[d];
-                if (!fin(dhi[d])) yy = fmax(yy, 0.0); else b2d += dhi[d] * dhi[d];
-                yd[d] = yy;
-            }
-            CS(CI::YDR + d) = yd[d];
-            CS(CI::DLO + d) = dlo[d];
-            CS(CI::DHI + d) = dhi[d];
+    for (int k = 0; k < CPL; ++k) { cj[k] = -1; x[k] = aty[k] = c[k] = lo[k] = hi[k] = ip[k] = tip[k] = ctip[k] = xsum[k] = 0.0; }
 #pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-                const int p = L.cpl_p[(d * LPS + gl) * CPL + k];
-                cf[d][k] = p >= 0 ? a.vals[snz + p] : 0.0;
-            }
-        }
+    for (int r = 0; r < RPL; ++r) {
+        y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) blk[r][k] = 0.0;
     }
+#pragma unroll
+    for (int d = 0; d < DD; ++d) {
+        yd[d] = axd[d] = dlo[d] = dhi[d] = ydsum[d] = 0.0;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) cf[d][k] = 0.0;
+    }
+    double omega = 1.0, tau = 0.0, sig = 0.0;
+    int it = 0, since = 0, cnt = 0;
 
     // ------------------------------------------------------------------ products
+    // (loops fully unrolled: the mask tests fold to constants)
+    auto bon = [](int r, int k) { return ((MB >> (r * CPL + k)) & 1u) != 0u; };
+    auto con = [](int d, int k) { return ((MC >> (d * CPL + k)) & 1u) != 0u; };
+    // row r of the block times a column vector f(k) (first term a product, then FMAs)
+    auto brow = [&](int r, auto f) {
+        double acc = 0.0;
+        bool first = true;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if (bon(r, k)) { acc = first ? blk[r][k] * f(k) : fma(blk[r][k], f(k), acc); first = false; }
+        return acc;
+    };
+    auto crow = [&](int d, auto f) {
+        double acc = 0.0;
+        bool first = true;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if (con(d, k)) { acc = first ? cf[d][k] * f(k) : fma(cf[d][k], f(k), acc); first = false; }
+        return acc;
+    };
+    // column k of [block; coupling]^T times (row vector g(r), coupling vector h(d))
+    auto bcol = [&](int k, auto g, auto h) {
+        double acc = 0.0;
+        bool first = true;
+#pragma unroll
+        for (int r = 0; r < RPL; ++r)
+            if (bon(r, k)) { acc = first ? blk[r][k] * g(r) : fma(blk[r][k], g(r), acc); first = false; }
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            if (con(d, k)) { acc = first ? cf[d][k] * h(d) : fma(cf[d][k], h(d), acc); first = false; }
+        return acc;
+    };
     auto mv_ax = [&](const double (&xx)[CPL], double (&o)[RPL], double (&od)[DD]) {
 #pragma unroll
-        for (int r = 0; r < RPL; ++r) {
-            double acc = blk[r][0] * xx[0];
-#pragma unroll
-            for (int k = 1; k < CPL; ++k) acc = fma(blk[r][k], xx[k], acc);
-            o[r] = acc;
-        }
+        for (int r = 0; r < RPL; ++r) o[r] = brow(r, [&](int k) { return xx[k]; });
         if constexpr (D > 0) {
             double t[D];
 #pragma unroll
-            for (int d = 0; d < D; ++d) {
-                double acc = cf[d][0] * xx[0];
-#pragma unroll
-                for (int k = 1; k < CPL; ++k) acc = fma(cf[d][k], xx[k], acc);
-                t[d] = acc;
-            }
+            for (int d = 0; d < D; ++d) t[d] = crow(d, [&](int k) { return xx[k]; });
             gsum_many<LPS, D>(t);
 #pragma unroll
             for (int d = 0; d < D; ++d) od[d] = t[d];
@@ -189,41 +146,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
     };
     auto mv_aty = [&](const double (&yy)[RPL], const double (&yyd)[DD], double (&o)[CPL]) {
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-            double acc = blk[0][k] * yy[0];
-#pragma unroll
-            for (int r = 1; r < RPL; ++r) acc = fma(blk[r][k], yy[r], acc);
-#pragma unroll
-            for (int d = 0; d < D; ++d) acc = fma(cf[d][k], yyd[d], acc);
-            o[k] = acc;
-        }
+        for (int k = 0; k < CPL; ++k) o[k] = bcol(k, [&](int r) { return yy[r]; }, [&](int d) { return yyd[d]; });
     };
-
-    // ------------------------------------------------------------------ scalars
-    // ||c'|| (unscaled, incl. PH terms), prox constant, initial primal weight ||c_hat||/||b_hat||
-    double omega;
-    {
-        double rr[4] = {c2, prox_const, 0.0, b2};
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
-        gsum_many<LPS, 4>(rr);
-        rr[3] += b2d;
-        CS(CI::SC + CI::CNORM) = sqrt(rr[0]);
-        CS(CI::SC + CI::PROX) = rr[1];
-        const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
-        omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
-        if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
-        else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);   // blend
-    }
-    const double eta = a.eta[s];
-    CS(CI::SC + CI::BNORM) = a.bnorm[s];
-    CS(CI::SC + CI::ETA) = eta;
-    {
-        const double tp = a.eps * (1.0 + a.bnorm[s]), td = a.eps * (1.0 + CS(CI::SC + CI::CNORM));
-        CS(CI::SC + CI::TP) = tp * tp;
-        CS(CI::SC + CI::TD) = td * td;
-    }
-    double tau = eta / omega, sig = eta * omega;
     // row bounds are held pre-multiplied by -sig (the dual step; re-derived from the LDS copy at
     // restarts), so the dual projection is one v_max_f64 + one v_min_f64 without modifiers
     auto rescale_bounds = [&]() {
@@ -232,7 +156,6 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
 #pragma unroll
         for (int d = 0; d < D; ++d) { dlo[d] = -sig * CS(CI::DLO + d); dhi[d] = -sig * CS(CI::DHI + d); }
     };
-    rescale_bounds();
     auto step_coefs = [&]() {
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
@@ -243,12 +166,6 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             }
         }
     };
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) CS(CI::C + k) = c[k];
-    step_coefs();
-
-    mv_ax(x, ax, axd);
-    mv_aty(y, yd, aty);
 
     // KKT pieces of an iterate over the scenario (group): [0] omega^2 ||pr||^2 + ||dres||^2 /
     // omega^2 on the scaled problem (PDLP's restart metric without the gap term), [1] unused,
@@ -323,26 +240,11 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         if (avg) {
             kkt_part([&](int k) { return xsum[k] * inv; },
                      [&](int k) {
-                         double acc = blk[0][k] * ysum[0];
-#pragma unroll
-                         for (int r = 1; r < RPL; ++r) acc = fma(blk[r][k], ysum[r], acc);
-#pragma unroll
-                         for (int d = 0; d < D; ++d) acc = fma(cf[d][k], ydsum[d], acc);
-                         return acc * inv;
+                         return bcol(k, [&](int r) { return ysum[r]; }, [&](int d) { return ydsum[d]; }) * inv;
                      },
                      [&](int r) { return ysum[r] * inv; },
-                     [&](int r) {
-                         double acc = blk[r][0] * xsum[0];
-#pragma unroll
-                         for (int k = 1; k < CPL; ++k) acc = fma(blk[r][k], xsum[k], acc);
-                         return acc * inv;
-                     },
-                     [&](int d) {
-                         double acc = cf[d][0] * xsum[0];
-#pragma unroll
-                         for (int k = 1; k < CPL; ++k) acc = fma(cf[d][k], xsum[k], acc);
-                         return acc;
-                     },
+                     [&](int r) { return brow(r, [&](int k) { return xsum[k]; }) * inv; },
+                     [&](int d) { return crow(d, [&](int k) { return xsum[k]; }); },
                      t + KT);
             gsum_many<LPS, 2 * KT>(t);
         } else {
@@ -375,22 +277,146 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         return fma(g, g, o[0]);
     };
 
-    CS(CI::SC + CI::OMEGA) = omega;
-    CS(CI::SC + CI::W2) = omega * omega;
-    CS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
-    {
-        double o[6];
-        kkt_both(false, 0.0, o, o);
-        CS(CI::SC + CI::KRST) = wkkt2_of(o);
-        CS(CI::SC + CI::KPREV) = INFINITY;
-    }
-    int it = 0, since = 0, cnt = 0;
-    bool live = true;
-    const int chk = a.check_every;
+    // ------------------------------------------------------------------ load one scenario
+    // (the group's lanes only; everything the iteration and the checks read is (re)initialised)
+    auto load = [&](int sc) {
+        s = sc;
+        const long sn = (long)s * a.n, sN = (long)s * a.N;
+        double prox_const = 0.0, c2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            seq();
+            const int j = L.col_of[gl * CPL + k];
+            cj[k] = j;
+            x[k] = aty[k] = c[k] = lo[k] = hi[k] = xsum[k] = 0.0;
+            double qs = 0.0;
+            CS(CI::IDC + k) = 1.0;
+            if (j >= 0) {
+                const long b = sn + j;
+                const double dd = a.dc[b];
+                double cc = a.c[b], qq = 0.0;
+                double lo_ = a.cl[b], hi_ = a.cu[b];
+                const int kk = col_nonant[j];
+                if (kk >= 0) {
+                    const long t = sN + kk;
+                    ph_terms(a, t, cc, qq, prox_const);
+                    if (a.fix_nonants) fixed_box(a, t, dd, lo_, hi_);
+                }
+                c2 += cc * cc;
+                CS(CI::IDC + k) = 1.0 / dd;
+                c[k] = cc * dd;
+                qs = qq * dd * dd;
+                lo[k] = lo_;
+                hi[k] = hi_;
+                x[k] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
+            }
+            CS(CI::XR + k) = x[k];
+            CS(CI::Q + k) = qs;
+        }
+        double b2 = 0.0;
+        {
+            const long sm = (long)s * a.m, snz = (long)s * a.nnz;
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+                seq();
+                const int i = L.row_of[gl * RPL + r];
+                y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
+                CS(CI::IDR + r) = 0.0;
+                if (i >= 0) {
+                    const long b = sm + i;
+                    CS(CI::IDR + r) = 1.0 / a.dr[b];
+                    rlo[r] = a.rl[b];
+                    rhi[r] = a.ru[b];
+                    double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
+                    if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
+                    if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];
+                    y[r] = yy;
+                }
+                CS(CI::YR + r) = y[r];
+                CS(CI::BLO + r) = rlo[r];
+                CS(CI::BHI + r) = rhi[r];
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const int p = L.blk_p[(gl * RPL + r) * CPL + k];
+                    blk[r][k] = p >= 0 ? a.vals[snz + p] : 0.0;
+                }
+            }
+        }
+        double b2d = 0.0;
+        {
+            const long sm = (long)s * a.m, snz = (long)s * a.nnz;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                seq();
+                const int i = L.cpl_row[d];
+                yd[d] = axd[d] = dlo[d] = dhi[d] = ydsum[d] = 0.0;
+                CS(CI::IDRD + d) = 0.0;
+                if (i >= 0) {
+                    const long b = sm + i;
+                    CS(CI::IDRD + d) = 1.0 / a.dr[b];
+                    dlo[d] = a.rl[b];
+                    dhi[d] = a.ru[b];
+                    double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
+                    if (!fin(dlo[d])) yy = fmin(yy, 0.0); else b2d += dlo[d] * dlo[d];
+                    if (!fin(dhi[d])) yy = fmax(yy, 0.0); else b2d += dhi[d] * dhi[d];
+                    yd[d] = yy;
+                }
+                CS(CI::YDR + d) = yd[d];
+                CS(CI::DLO + d) = dlo[d];
+                CS(CI::DHI + d) = dhi[d];
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    const int p = L.cpl_p[(d * LPS + gl) * CPL + k];
+                    cf[d][k] = p >= 0 ? a.vals[snz + p] : 0.0;
+                }
+            }
+        }
+        // ||c'|| (unscaled, incl. PH terms), prox constant, initial primal weight ||c_hat||/||b_hat||
+        {
+            double rr[4] = {c2, prox_const, 0.0, b2};
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
+            gsum_many<LPS, 4>(rr);
+            rr[3] += b2d;
+            CS(CI::SC + CI::CNORM) = sqrt(rr[0]);
+            CS(CI::SC + CI::PROX) = rr[1];
+            const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
+            omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
+            if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
+            else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);   // blend
+        }
+        const double eta = a.eta[s];
+        CS(CI::SC + CI::BNORM) = a.bnorm[s];
+        CS(CI::SC + CI::ETA) = eta;
+        {
+            const double tp = a.eps * (1.0 + a.bnorm[s]), td = a.eps * (1.0 + CS(CI::SC + CI::CNORM));
+            CS(CI::SC + CI::TP) = tp * tp;
+            CS(CI::SC + CI::TD) = td * td;
+        }
+        tau = eta / omega;
+        sig = eta * omega;
+        rescale_bounds();
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) CS(CI::C + k) = c[k];
+        step_coefs();
+        mv_ax(x, ax, axd);
+        mv_aty(y, yd, aty);
+        CS(CI::SC + CI::OMEGA) = omega;
+        CS(CI::SC + CI::W2) = omega * omega;
+        CS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
+        {
+            double o[6];
+            kkt_both(false, 0.0, o, o);
+            CS(CI::SC + CI::KRST) = wkkt2_of(o);
+            CS(CI::SC + CI::KPREV) = INFINITY;
+        }
+        it = 0;
+        since = 0;
+        cnt = 0;
+    };
 
-    // epilogue for a group that has terminated (st 0 optimal, 1 iteration limit, 2 NaN)
+    // epilogue of a group that has terminated (st 0 optimal, 1 iteration limit, 2 NaN)
     auto finish = [&](bool use_avg, double inv, double rel, double pobj, double dobj, int st) {
-        if (!valid) return;
         const int sl = launder(s);
         const long sn = (long)sl * a.n, sm = (long)sl * a.m, sN = (long)sl * a.N;
 #pragma unroll
@@ -440,7 +466,35 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         }
     };
 
-    while (wave_any(live)) {
+    // next work item of this group (group-uniform): the queue in PERSIST mode, else the group's
+    // one item of this workgroup (and nothing after it)
+    int taken = 0;
+    auto fetch = [&]() -> int {
+        if constexpr (PERSIST) {
+            int w = 0;
+            if (gl == 0) w = (int)__hip_atomic_fetch_add(a.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return __shfl(w, grp * LPS, 64);
+        } else {
+            return taken++ ? a.S : (int)blockIdx.x * G + grp;
+        }
+    };
+
+    bool valid = true, live = false;   // valid: the group may still receive work
+    const int chk = a.check_every;
+    for (;;) {
+        const bool need = valid && !live;
+        if (wave_any(need)) {
+            if (need) {
+                const int w = fetch();
+                if (w < a.S) {
+                    load(a.order ? a.order[w] : w);
+                    live = true;
+                } else {
+                    valid = false;
+                }
+            }
+        }
+        if (!wave_any(live)) break;
         // two PDHG iterations per trip (check_every is even): the A x / A x+ hand-over is a
         // register rename instead of copies
         auto step = [&]() {
@@ -498,7 +552,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                    nan ? 2 : (term ? 0 : 1));
             live = false;
         }
-        if (!wave_any(live)) break;
+        if (!wave_any(live)) continue;   // (refill or exit at the top)
 
         const double k_cur = wkkt2_of(oc), k_avg = wkkt2_of(oa);
         const bool use_avg = k_avg < k_cur;
@@ -507,7 +561,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         const bool restart = live && ((cand <= a.beta_suf * a.beta_suf * krst) ||
                                       (cand <= a.beta_nec * a.beta_nec * krst && cand > CS(CI::SC + CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
-        CS(CI::SC + CI::KPREV) = cand;
+        if (live) CS(CI::SC + CI::KPREV) = cand;
         if (wave_any(restart)) {
             const bool ra = restart && use_avg;
             if (wave_any(ra)) {
@@ -521,7 +575,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 mv_ax(x, ax, axd);
                 mv_aty(y, yd, aty);
             }
-            // primal weight update (theta = 0.5) from the movement since the last restart
+            // primal weight update from the movement since the last restart
             double mv[2] = {0.0, 0.0};
 #pragma unroll
             for (int k = 0; k < CPL; ++k) { const double t = x[k] - CS(CI::XR + k); mv[0] += t * t; }
@@ -530,14 +584,13 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             gsum_many<LPS, 2>(mv);
 #pragma unroll
             for (int d = 0; d < D; ++d) { const double t = yd[d] - CS(CI::YDR + d); mv[1] += t * t; }
-            omega = CS(CI::SC + CI::OMEGA);
-            if (restart) omega = primal_weight(omega, mv[0], mv[1], a.theta);
-            const double et = CS(CI::SC + CI::ETA);
-            tau = et / omega;
-            sig = et * omega;
-            rescale_bounds();
-            step_coefs();
             if (restart) {
+                omega = primal_weight(CS(CI::SC + CI::OMEGA), mv[0], mv[1], a.theta);
+                const double et = CS(CI::SC + CI::ETA);
+                tau = et / omega;
+                sig = et * omega;
+                rescale_bounds();
+                step_coefs();
 #pragma unroll
                 for (int k = 0; k < CPL; ++k) { CS(CI::XR + k) = x[k]; xsum[k] = 0.0; }
 #pragma unroll
@@ -554,16 +607,33 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             }
         }
     }
+    if constexpr (PERSIST) {
+        // the last wave out re-arms the queue for the next (stream-ordered) launch: every wave
+        // has stopped fetching by then (a fetch past the end only happens once the queue is dry)
+        if (lane == 0) {
+            const unsigned prev = __hip_atomic_fetch_add(a.queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev == gridDim.x - 1) {
+                __hip_atomic_store(a.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------- dispatch
 struct LocalVariant {
     int LPS, CPL, RPL, D;
+    unsigned MB, MC;           // compiled-in block / coupling slot masks (all ones: generic)
     void (*fn)(PdhgArgs);
+    void (*fn_persist)(PdhgArgs);
 };
 
-#define PHG_L(a_, b_, c_, d_) {a_, b_, c_, d_, pdhg_local_kernel<a_, b_, c_, d_>}
-// ordered by preference: fewest lanes per scenario first, then smallest register footprint
+#define PHG_LM(a_, b_, c_, d_, mb_, mc_)                                                        \
+    {a_, b_, c_, d_, mb_, mc_, pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_>,                \
+     pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_>}
+#define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u)
+// shapes ordered by preference: fewest lanes per scenario first, then smallest register footprint;
+// the generic kernel of every shape first, then pattern-specialised ones
 static const LocalVariant kLocalVariants[] = {
     PHG_L(16, 4, 2, 1),
     PHG_L(16, 4, 3, 1),
@@ -574,10 +644,39 @@ static const LocalVariant kLocalVariants[] = {
     PHG_L(64, 4, 2, 1),
     PHG_L(64, 4, 3, 1),
     PHG_L(64, 4, 4, 2),
+    // farmer (examples/farmer/farmer.py:157-203): per crop lane, columns DevotedAcreage, SubQuota,
+    // SuperQuota, Purchased; rows cattle feed (all four) and limit sold (no Purchased); the
+    // total-acreage coupling row on DevotedAcreage only
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u),
 };
 #undef PHG_L
+#undef PHG_LM
+constexpr int kLocalShapes = 9;   // the generic entries; the planner walks these
 
-int pdhg_local_num_variants() { return (int)(sizeof(kLocalVariants) / sizeof(kLocalVariants[0])); }
+int pdhg_local_num_variants() { return kLocalShapes; }
+
+// the variant to run for shape v and the layout's slot masks: the specialised entry of that shape
+// with the fewest slots that still covers every occupied one, else the generic kernel
+int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc) {
+    const LocalVariant& S0 = kLocalVariants[v];
+    int best = v, bits = __builtin_popcount(S0.MB) + __builtin_popcount(S0.MC);
+    const int total = (int)(sizeof(kLocalVariants) / sizeof(kLocalVariants[0]));
+    for (int u = kLocalShapes; u < total; ++u) {
+        const LocalVariant& V = kLocalVariants[u];
+        if (V.LPS != S0.LPS || V.CPL != S0.CPL || V.RPL != S0.RPL || V.D != S0.D) continue;
+        if ((mb & ~V.MB) || (mc & ~V.MC)) continue;
+        const int b = __builtin_popcount(V.MB) + __builtin_popcount(V.MC);
+        if (b < bits) { best = u; bits = b; }
+    }
+    return best;
+}
+
+void pdhg_local_variant_masks(int v, unsigned* out2) {
+    out2[0] = kLocalVariants[v].MB;
+    out2[1] = kLocalVariants[v].MC;
+}
 
 void pdhg_local_variant_shape(int v, int* out4) {
     const LocalVariant& V = kLocalVariants[v];
@@ -591,10 +690,28 @@ size_t pdhg_local_lds_bytes(int v) {
     return (size_t)cold_items(V.CPL, V.RPL, V.D) * 64 * sizeof(double);
 }
 
+// PERSIST (a.queue set): a grid of as many waves as fit on the device at once (occupancy x CUs,
+// queried once per variant); more would only find the queue dry, fewer would leave SIMDs idle
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream) {
-    const int G = 64 / kLocalVariants[v].LPS;
-    hipLaunchKernelGGL(kLocalVariants[v].fn, dim3((a.S + G - 1) / G), dim3(64), pdhg_local_lds_bytes(v),
-                       stream, a);
+    const LocalVariant& V = kLocalVariants[v];
+    const int G = 64 / V.LPS;
+    const size_t lds = pdhg_local_lds_bytes(v);
+    int grid = (a.S + G - 1) / G;
+    if (a.queue) {
+        static int resident[32] = {0};
+        if (!resident[v]) {
+            int dev = 0, cus = 0, per = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, V.fn_persist, 64, lds);
+            if (e != hipSuccess) return e;
+            resident[v] = std::max(1, per) * std::max(1, cus);
+        }
+        grid = std::min(grid, resident[v]);
+        hipLaunchKernelGGL(V.fn_persist, dim3(grid), dim3(64), lds, stream, a);
+    } else {
+        hipLaunchKernelGGL(V.fn, dim3(grid), dim3(64), lds, stream, a);
+    }
     return hipGetLastError();
 }
 

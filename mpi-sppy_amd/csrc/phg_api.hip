@@ -26,6 +26,8 @@ hipError_t prep_launch(const PrepArgs& a, hipStream_t stream);
 hipError_t schedule_launch(const int* iters, int S, int unit, int* order, hipStream_t st);
 int pdhg_local_num_variants();
 void pdhg_local_variant_shape(int v, int* out4);
+int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc);
+void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_block_num_variants();
 void pdhg_block_variant_shape(int v, int* out5);
@@ -82,6 +84,7 @@ struct phg_handle {
     int layout_policy = PHG_LAYOUT_AUTO;
     int vshape[6] = {0};
     int lshape[4] = {0};
+    unsigned local_masks[2] = {0, 0};   // occupied block / coupling slots of the lane-local layout
     std::vector<void*> allocs;
     // device arrays
     double *vals = nullptr, *c = nullptr, *cl = nullptr, *cu = nullptr, *rl = nullptr, *ru = nullptr;
@@ -104,6 +107,8 @@ struct phg_handle {
     } back{};
     int swaps = 0;             // solves since load (parity of the front copy; phg_solve_undo)
     int* order = nullptr;      // launch schedule (schedule.hip)
+    unsigned* queue = nullptr; // work queue of the persistent lane-local kernel
+    bool persist = false;      // PHG_LOCAL_PERSIST=1 selects the persistent work-queue grid (measured slower)
     bool have_order = false;
     double* pinned = nullptr;  // page-locked readback buffer (convergence partials)
     int summary[2] = {0, 0};   // scenarios not optimal / NaN, as of the last phg_conv_finish
@@ -208,6 +213,7 @@ int phg_create(int device, phg_handle** out) {
     CK(hipSetDevice(device));
     phg_handle* h = new phg_handle();
     h->device = device;
+    if (const char* ev = std::getenv("PHG_LOCAL_PERSIST")) h->persist = std::atoi(ev) != 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return fail("phg_create: hipStreamCreate failed");
@@ -547,7 +553,22 @@ static int build_local_layout(phg_handle* h, const phg_batch* b) {
         const int r = plan_local(b, sh[0], sh[1], sh[2], sh[3], plan);
         if (r < 0) return -1;
         if (r > 0) continue;
-        h->local_variant = v;
+        // slots occupied in at least one lane -> the pattern-specialised kernel of this shape
+        const int LPS = sh[0], CPL = sh[1], RPL = sh[2], D = sh[3];
+        unsigned mb = 0, mc = 0;
+        for (int l = 0; l < LPS; ++l) {
+            for (int rr = 0; rr < RPL; ++rr)
+                for (int k = 0; k < CPL; ++k)
+                    if (plan.blk_p[(l * RPL + rr) * CPL + k] >= 0) mb |= 1u << (rr * CPL + k);
+            for (int d = 0; d < D; ++d)
+                for (int k = 0; k < CPL; ++k)
+                    if (plan.cpl_p[(d * LPS + l) * CPL + k] >= 0) mc |= 1u << (d * CPL + k);
+        }
+        // PHG_LOCAL_GENERIC=1 keeps the generic kernel (A/B of the specialisation)
+        const char* gen = std::getenv("PHG_LOCAL_GENERIC");
+        h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc);
+        h->local_masks[0] = mb;
+        h->local_masks[1] = mc;
         std::memcpy(h->lshape, sh, sizeof sh);
         int* p;
         if (dput(h, &p, plan.col_of.data(), plan.col_of.size())) return -1; h->loc.col_of = p;
@@ -1102,6 +1123,7 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     if (dalloc(h, &h->status, S)) return -1;
     if (dalloc(h, &h->iters_acc, S)) return -1;
     if (dalloc(h, &h->order, S)) return -1;
+    if (dalloc(h, &h->queue, 2)) return -1;
     h->nonant_col_h.assign(b->nonant_col, b->nonant_col + N);
     if (dput(h, &h->nonant_col_d, b->nonant_col, N)) return -1;
     if (build_ph_tables(h, b)) return -1;
@@ -1248,6 +1270,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.blk = h->blk;
     a.gate = o->skip_if_conv_below > 0 ? h->gate : nullptr;
     a.gate_below = o->skip_if_conv_below;
+    a.queue = h->persist ? h->queue : nullptr;
     if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));

@@ -115,6 +115,9 @@ struct PdhgArgs {
     // before it has read conv back
     const double* gate;
     double gate_below;
+    // work queue of the persistent lane-local kernel ([0] next item, [1] waves done; both 0
+    // between launches), or nullptr: one work item per lane group
+    unsigned* queue;
 };
 
 struct PrepArgs {

@@ -97,6 +97,13 @@ def solve(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=None, o
     obj = float(h.getInfo().objective_function_value)
     rd = np.array(sol.row_dual, dtype=np.float64) if sol.dual_valid else None
     cd = np.array(sol.col_dual, dtype=np.float64) if sol.dual_valid else None
+    if qdiag is not None and np.any(np.asarray(qdiag) != 0) and st != "Optimal" and do_polish and time_limit is None:
+        # HiGHS 1.8's QP solver occasionally ends in "Solve error" on a prox-QP that is plainly
+        # feasible and bounded (farmer cm=10 deep in a PH run): the interior-point oracle certifies it
+        from . import ipm
+        r = ipm.solve_qp(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=qdiag, offset=offset)
+        if r.ok:
+            return SolveResult("Optimal", r.x, r.obj)
     if qdiag is not None and st == "Optimal" and do_polish:
         # 1. HiGHS's own point, when its duals certify it (relative KKT <= 1e-9);
         # 2. else the exact active-set polish (small subproblems: dense KKT solves);
