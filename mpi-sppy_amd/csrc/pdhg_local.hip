@@ -23,24 +23,29 @@ namespace phg {
 
 // Per-lane "cold" state (read only at the every-`check_every` restart/termination test) lives in
 // LDS as [item][lane] doubles -- conflict-free ds_read_b64 -- so the registers hold only what the
-// PDHG iteration itself touches.
-// cold items per lane: XR/YR/YDR restart point, Q diagonal, C scaled cost, IDC/IDR/IDRD inverse scalings (unscaled
-// residuals), BLO/BHI/DLO/DHI the scaled row bounds (the registers hold them times -sigma), then
-// per-group scalars (CNORM, BNORM, ... replicated in every lane of the group)
-constexpr int cold_items(int CPL, int RPL, int D) { return 4 * CPL + 4 * RPL + 4 * (D > 0 ? D : 1) + 11; }
-
+// PDHG iteration itself touches.  Lane items: XR / YR restart point, Q diagonal, C scaled cost,
+// IDC / IDR inverse scalings (unscaled residuals), BLO / BHI the scaled row bounds (the registers
+// hold them times -sigma).  Group items (the same value in every lane of a scenario's group, stored
+// once per group and read as an LDS broadcast): the coupling rows' restart point, inverse scaling
+// and bounds, and the scalars (CNORM, BNORM, ...).  12.5 KB per wave (farmer).
 template <int CPL, int RPL, int D>
 struct Cold {
     static constexpr int DD = D > 0 ? D : 1;
+    // lane items
     static constexpr int XR = 0, Q = CPL, IDC = 2 * CPL, C = 3 * CPL, YR = 4 * CPL, IDR = YR + RPL, BLO = IDR + RPL,
-                         BHI = BLO + RPL, YDR = BHI + RPL, IDRD = YDR + DD, DLO = IDRD + DD, DHI = DLO + DD,
-                         SC = DHI + DD;
+                         BHI = BLO + RPL, NL = BHI + RPL;
+    // group items
+    static constexpr int YDR = 0, IDRD = DD, DLO = 2 * DD, DHI = 3 * DD, SC = 4 * DD;
     // KRST / KPREV hold SQUARED weighted KKT errors; TP / TD the squared termination thresholds
     // (eps (1 + ||b||))^2, (eps (1 + ||c||))^2; W2 / IW2 = omega^2, 1 / omega^2
     enum { CNORM = 0, BNORM, ETA, PROX, OMEGA, KRST, KPREV, TP, TD, W2, IW2, NSC };
-    static constexpr int N = SC + NSC;
-    static_assert(N == cold_items(CPL, RPL, D), "cold layout");
+    static constexpr int NG = SC + NSC;
 };
+template <int LPS, int CPL, int RPL, int D>
+constexpr size_t local_lds_bytes() {
+    using CI = Cold<CPL, RPL, D>;
+    return (size_t)(CI::NL * 64 + (64 / LPS) * CI::NG) * sizeof(double);
+}
 
 // PERSIST: a persistent grid (as many waves as are resident) in which every lane group takes its
 // next scenario from a device work queue (a.queue, in launch order: heaviest first) as soon as its
@@ -55,17 +60,25 @@ struct Cold {
 // A x, A^T y and the check's products (farmer: 8 of 24 per iteration; every crop's lane has the
 // same 4-column / 2-row block pattern and one coupling entry).  The sums are bit-identical to the
 // generic kernel's (the dropped terms are fma(0, v, acc) = acc).
+// Waves per SIMD.  Three fit the LDS (12.5 KB per wave on farmer) and, with the step
+// coefficients re-derived after every check instead of held across it, 168 registers with a few
+// prologue spills -- but measured on MI355X that is 0.345-0.350 ms per farmer-10k launch against
+// 0.342 ms at two waves (the kernel is VALU-issue-bound, not latency-bound), so two it is.
+template <int LPS, int CPL, int RPL, int D>
+constexpr int local_waves() { return 2; }
+
 template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC>
-__global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
+__global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
     constexpr int G = 64 / LPS;                    // scenarios per wave
     constexpr int DD = D > 0 ? D : 1;
     using CI = Cold<CPL, RPL, D>;
     extern __shared__ double cold[];
     const int lane = threadIdx.x;
-    auto CS = [&](int item) -> double& { return cold[item * 64 + lane]; };
     const int gl = lane % LPS;                     // lane inside the scenario's group
     const int grp = lane / LPS;
+    auto CS = [&](int item) -> double& { return cold[item * 64 + lane]; };
+    auto GS = [&](int item) -> double& { return cold[CI::NL * 64 + grp * CI::NG + item]; };
     const LocalLayout& L = a.loc;
     const int* col_nonant = a.lay.col_nonant;
     // the primal step is x+ = clamp(x ip + A^T y tip - ctip) with ip = 1 / (1 + tau q),
@@ -154,7 +167,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
 #pragma unroll
         for (int r = 0; r < RPL; ++r) { rlo[r] = -sig * CS(CI::BLO + r); rhi[r] = -sig * CS(CI::BHI + r); }
 #pragma unroll
-        for (int d = 0; d < D; ++d) { dlo[d] = -sig * CS(CI::DLO + d); dhi[d] = -sig * CS(CI::DHI + d); }
+        for (int d = 0; d < D; ++d) { dlo[d] = -sig * GS(CI::DLO + d); dhi[d] = -sig * GS(CI::DHI + d); }
     };
     auto step_coefs = [&]() {
 #pragma unroll
@@ -212,7 +225,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             if (fin(hi[k])) t[5] += hi[k] * fmin(rc_, 0.0);
             t[5] -= hq;
         }
-        t[0] = fma(CS(CI::SC + CI::W2), pr2, dr2 * CS(CI::SC + CI::IW2));
+        t[0] = fma(GS(CI::SC + CI::W2), pr2, dr2 * GS(CI::SC + CI::IW2));
 #pragma unroll
         for (int d = 0; d < D; ++d) t[cslot(d)] = axdp(d);
     };
@@ -222,10 +235,10 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         for (int d = 0; d < D; ++d) {
             seq();
             const double axx = t[cslot(d)] * scale, yy = ydf(d);
-            const double bl = CS(CI::DLO + d), bu = CS(CI::DHI + d);
+            const double bl = GS(CI::DLO + d), bu = GS(CI::DHI + d);
             const double pr = axx - clampd(axx, bl, bu);
-            t[0] = fma(CS(CI::SC + CI::W2), pr * pr, t[0]);
-            const double pu = pr * CS(CI::IDRD + d);
+            t[0] = fma(GS(CI::SC + CI::W2), pr * pr, t[0]);
+            const double pu = pr * GS(CI::IDRD + d);
             t[2] += pu * pu;
             if (fin(bl)) t[5] += bl * fmax(yy, 0.0);
             if (fin(bu)) t[5] += bu * fmin(yy, 0.0);
@@ -261,14 +274,14 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
     };
     // relative KKT error (reported in the epilogue only)
     auto rel_of = [&](const double* o) {
-        const double p = sqrt(o[2]) / (1.0 + CS(CI::SC + CI::BNORM));
-        const double d = sqrt(o[3]) / (1.0 + CS(CI::SC + CI::CNORM));
+        const double p = sqrt(o[2]) / (1.0 + GS(CI::SC + CI::BNORM));
+        const double d = sqrt(o[3]) / (1.0 + GS(CI::SC + CI::CNORM));
         const double g = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
         return fmax(fmax(p, d), g);
     };
     // rel_of(o) <= eps without square roots or divisions
     auto converged = [&](const double* o) {
-        return o[2] <= CS(CI::SC + CI::TP) && o[3] <= CS(CI::SC + CI::TD) &&
+        return o[2] <= GS(CI::SC + CI::TP) && o[3] <= GS(CI::SC + CI::TD) &&
                fabs(o[4] - o[5]) <= a.eps * (1.0 + fabs(o[4]) + fabs(o[5]));
     };
     // squared primal-weighted KKT error (PDLP's restart metric)
@@ -350,10 +363,10 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                 seq();
                 const int i = L.cpl_row[d];
                 yd[d] = axd[d] = dlo[d] = dhi[d] = ydsum[d] = 0.0;
-                CS(CI::IDRD + d) = 0.0;
+                GS(CI::IDRD + d) = 0.0;
                 if (i >= 0) {
                     const long b = sm + i;
-                    CS(CI::IDRD + d) = 1.0 / a.dr[b];
+                    GS(CI::IDRD + d) = 1.0 / a.dr[b];
                     dlo[d] = a.rl[b];
                     dhi[d] = a.ru[b];
                     double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
@@ -361,9 +374,9 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                     if (!fin(dhi[d])) yy = fmax(yy, 0.0); else b2d += dhi[d] * dhi[d];
                     yd[d] = yy;
                 }
-                CS(CI::YDR + d) = yd[d];
-                CS(CI::DLO + d) = dlo[d];
-                CS(CI::DHI + d) = dhi[d];
+                GS(CI::YDR + d) = yd[d];
+                GS(CI::DLO + d) = dlo[d];
+                GS(CI::DHI + d) = dhi[d];
 #pragma unroll
                 for (int k = 0; k < CPL; ++k) {
                     const int p = L.cpl_p[(d * LPS + gl) * CPL + k];
@@ -378,20 +391,20 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
             gsum_many<LPS, 4>(rr);
             rr[3] += b2d;
-            CS(CI::SC + CI::CNORM) = sqrt(rr[0]);
-            CS(CI::SC + CI::PROX) = rr[1];
+            GS(CI::SC + CI::CNORM) = sqrt(rr[0]);
+            GS(CI::SC + CI::PROX) = rr[1];
             const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
             omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
             if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
             else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);   // blend
         }
         const double eta = a.eta[s];
-        CS(CI::SC + CI::BNORM) = a.bnorm[s];
-        CS(CI::SC + CI::ETA) = eta;
+        GS(CI::SC + CI::BNORM) = a.bnorm[s];
+        GS(CI::SC + CI::ETA) = eta;
         {
-            const double tp = a.eps * (1.0 + a.bnorm[s]), td = a.eps * (1.0 + CS(CI::SC + CI::CNORM));
-            CS(CI::SC + CI::TP) = tp * tp;
-            CS(CI::SC + CI::TD) = td * td;
+            const double tp = a.eps * (1.0 + a.bnorm[s]), td = a.eps * (1.0 + GS(CI::SC + CI::CNORM));
+            GS(CI::SC + CI::TP) = tp * tp;
+            GS(CI::SC + CI::TD) = td * td;
         }
         tau = eta / omega;
         sig = eta * omega;
@@ -401,14 +414,14 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         step_coefs();
         mv_ax(x, ax, axd);
         mv_aty(y, yd, aty);
-        CS(CI::SC + CI::OMEGA) = omega;
-        CS(CI::SC + CI::W2) = omega * omega;
-        CS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
+        GS(CI::SC + CI::OMEGA) = omega;
+        GS(CI::SC + CI::W2) = omega * omega;
+        GS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
         {
             double o[6];
             kkt_both(false, 0.0, o, o);
-            CS(CI::SC + CI::KRST) = wkkt2_of(o);
-            CS(CI::SC + CI::KPREV) = INFINITY;
+            GS(CI::SC + CI::KRST) = wkkt2_of(o);
+            GS(CI::SC + CI::KPREV) = INFINITY;
         }
         it = 0;
         since = 0;
@@ -455,8 +468,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
                     if (a.y_out) a.y_out[b] = yv * a.dr[b];
                 }
             }
-            const double offs = a.obj_off[sl] + (a.prox_on ? CS(CI::SC + CI::PROX) : 0.0);
-            a.omega[sl] = CS(CI::SC + CI::OMEGA);
+            const double offs = a.obj_off[sl] + (a.prox_on ? GS(CI::SC + CI::PROX) : 0.0);
+            a.omega[sl] = GS(CI::SC + CI::OMEGA);
             a.obj[sl] = a.sense * (pobj + offs);
             a.bound[sl] = a.sense * (dobj + offs);
             a.kkt[sl] = rel;
@@ -557,11 +570,11 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
         const double k_cur = wkkt2_of(oc), k_avg = wkkt2_of(oa);
         const bool use_avg = k_avg < k_cur;
         const double cand = use_avg ? k_avg : k_cur;
-        const double krst = CS(CI::SC + CI::KRST);
+        const double krst = GS(CI::SC + CI::KRST);
         const bool restart = live && ((cand <= a.beta_suf * a.beta_suf * krst) ||
-                                      (cand <= a.beta_nec * a.beta_nec * krst && cand > CS(CI::SC + CI::KPREV)) ||
+                                      (cand <= a.beta_nec * a.beta_nec * krst && cand > GS(CI::SC + CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
-        if (live) CS(CI::SC + CI::KPREV) = cand;
+        if (live) GS(CI::SC + CI::KPREV) = cand;
         if (wave_any(restart)) {
             const bool ra = restart && use_avg;
             if (wave_any(ra)) {
@@ -583,10 +596,10 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
             for (int r = 0; r < RPL; ++r) { const double t = y[r] - CS(CI::YR + r); mv[1] += t * t; }
             gsum_many<LPS, 2>(mv);
 #pragma unroll
-            for (int d = 0; d < D; ++d) { const double t = yd[d] - CS(CI::YDR + d); mv[1] += t * t; }
+            for (int d = 0; d < D; ++d) { const double t = yd[d] - GS(CI::YDR + d); mv[1] += t * t; }
             if (restart) {
-                omega = primal_weight(CS(CI::SC + CI::OMEGA), mv[0], mv[1], a.theta);
-                const double et = CS(CI::SC + CI::ETA);
+                omega = primal_weight(GS(CI::SC + CI::OMEGA), mv[0], mv[1], a.theta);
+                const double et = GS(CI::SC + CI::ETA);
                 tau = et / omega;
                 sig = et * omega;
                 rescale_bounds();
@@ -596,12 +609,12 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
 #pragma unroll
                 for (int r = 0; r < RPL; ++r) { CS(CI::YR + r) = y[r]; ysum[r] = 0.0; }
 #pragma unroll
-                for (int d = 0; d < D; ++d) { CS(CI::YDR + d) = yd[d]; ydsum[d] = 0.0; }
-                CS(CI::SC + CI::OMEGA) = omega;
-                CS(CI::SC + CI::W2) = omega * omega;
-                CS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
-                CS(CI::SC + CI::KRST) = cand;
-                CS(CI::SC + CI::KPREV) = INFINITY;
+                for (int d = 0; d < D; ++d) { GS(CI::YDR + d) = yd[d]; ydsum[d] = 0.0; }
+                GS(CI::SC + CI::OMEGA) = omega;
+                GS(CI::SC + CI::W2) = omega * omega;
+                GS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
+                GS(CI::SC + CI::KRST) = cand;
+                GS(CI::SC + CI::KPREV) = INFINITY;
                 cnt = 0;
                 since = 0;
             }
@@ -624,12 +637,14 @@ __global__ __launch_bounds__(64, 2) void pdhg_local_kernel(PdhgArgs a) {
 struct LocalVariant {
     int LPS, CPL, RPL, D;
     unsigned MB, MC;           // compiled-in block / coupling slot masks (all ones: generic)
+    size_t lds;                // dynamic LDS per wave (Cold layout)
     void (*fn)(PdhgArgs);
     void (*fn_persist)(PdhgArgs);
 };
 
 #define PHG_LM(a_, b_, c_, d_, mb_, mc_)                                                        \
-    {a_, b_, c_, d_, mb_, mc_, pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_>,                \
+    {a_, b_, c_, d_, mb_, mc_, local_lds_bytes<a_, b_, c_, d_>(),                                \
+     pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_>,                                         \
      pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_>}
 #define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u)
 // shapes ordered by preference: fewest lanes per scenario first, then smallest register footprint;
@@ -683,12 +698,7 @@ void pdhg_local_variant_shape(int v, int* out4) {
     out4[0] = V.LPS; out4[1] = V.CPL; out4[2] = V.RPL; out4[3] = V.D;
 }
 
-size_t pdhg_local_lds_bytes(int v) {
-    const LocalVariant& V = kLocalVariants[v];
-    const int DD = V.D > 0 ? V.D : 1;
-    (void)DD;
-    return (size_t)cold_items(V.CPL, V.RPL, V.D) * 64 * sizeof(double);
-}
+size_t pdhg_local_lds_bytes(int v) { return kLocalVariants[v].lds; }
 
 // PERSIST (a.queue set): a grid of as many waves as fit on the device at once (occupancy x CUs,
 // queried once per variant); more would only find the queue dry, fewer would leave SIMDs idle
