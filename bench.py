@@ -50,7 +50,7 @@ def parse():
                          "case, i.e. farmer 10k = the BASELINE headline, sharded over the N GPUs: strong "
                          "scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0: skip)")
-    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local"],
+    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local", "block", "mfma"],
                     help="PDHG data layout (include/phg.h: phg_set_layout)")
     ap.add_argument("--no-schedule", action="store_true", help="launch scenarios in index order")
     ap.add_argument("--check-every", type=int, default=32, help="PDHG restart/termination check interval")
@@ -284,6 +284,22 @@ def main():
     ph_bytes = 8 * S_loc * b.N * 4 + 8 * S_loc + 16 * b.N_tot
     ph_gbs = ph_bytes / (upd_ms / args.steps / 1e3) / 1e9
     valu = eng.layout in ("local", "gather")
+    # shared-matrix MFMA layout: SURVEY 8(d)2 F = 4 m n flops per scenario per PDHG iteration (A x and
+    # A^T y as dense GEMM) and the flops the matrix cores actually execute (16 x 16 x 4 fragments:
+    # 2048 flops per 16 scenarios each, the all-zero ones skipped)
+    mfma_rf = None
+    if eng.layout == "mfma":
+        dense = 4 * b.n * m_run
+        frag = eng.mfma_fragments()
+        exe = 128 * frag
+        mfma_rf = {"bound": "mfma", "achieved": round(dense * pdhg_iters / args.steps / avg_launch_s / 1e12, 4),
+                   "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                   "frac": round(dense * pdhg_iters / args.steps / avg_launch_s / 1e12 / FP64_PEAK_TFLOPS, 5),
+                   "flops_dense_per_pdhg_iter_per_scen": dense, "mfma_fragments_per_pdhg_iter": frag,
+                   "mfma_flops_executed_per_pdhg_iter_per_scen": exe,
+                   "executed_tflops": round(exe * pdhg_iters / args.steps / avg_launch_s / 1e12, 4),
+                   "flops_sparse_per_pdhg_iter_per_scen": f_it,
+                   "sparse_tflops": round(achieved_tf, 4)}
 
     out = {
         "metric": "scenario-QP solves/sec (PH iteration: batched prox-QP solve of every scenario + fused xbar/W/conv)",
@@ -311,7 +327,8 @@ def main():
                    "presolve_rows_folded": eng.rows_folded},
         # fp64 VALU-bound kernels (lane-local / gather): flops against the fp64 peak; the streaming
         # block kernel: algorithmic bytes against HBM
-        "roofline": ({"bound": "valu", "achieved": round(achieved_tf, 4), "peak": FP64_PEAK_TFLOPS,
+        "roofline": (mfma_rf if mfma_rf is not None else
+                     {"bound": "valu", "achieved": round(achieved_tf, 4), "peak": FP64_PEAK_TFLOPS,
                       "unit": "TFLOP/s", "frac": round(achieved_tf / FP64_PEAK_TFLOPS, 5)}
                      if valu else
                      {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -321,7 +338,8 @@ def main():
                      "traffic": traffic,
                      "kernel": {"local": "pdhg_local_kernel (lane-local, fp64 VALU)",
                                 "gather": "pdhg_kernel (wave LDS-gather, fp64 VALU)",
-                                "block": "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)"}[eng.layout],
+                                "block": "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)",
+                                "mfma": "pdhg_mfma_kernel (shared matrix, v_mfma_f64_16x16x4_f64, 16 scenarios per wave)"}[eng.layout],
                      "flops_per_pdhg_iter_per_scen": f_it,
                      "pdhg_iters_per_scen_per_step": round(pdhg_iters / args.steps / S_loc, 2),
                      "max_pdhg_iters": max_iters,

@@ -143,12 +143,17 @@ int  phg_set_stream(phg_handle* h, void* hip_stream);
 int  phg_sync(phg_handle* h);
 
 /* PDHG data layout, chosen at phg_load_batch (call before it):
- *   AUTO   : the lane-local register layout (pdhg_local.hip) when the pattern splits into blocks
- *            that fit a lane plus <= a few coupling rows, else the wave LDS-gather layout
+ *   AUTO   : when every scenario has the same constraint matrix and it fits the MFMA tiles
+ *            (n, m <= 16: one 16 x 16 tile) densely enough (nnz >= 1/16 of the padded
+ *            tile) and the batch holds >= 4096 scenarios (one 16-scenario wave per CU), the
+ *            shared-matrix fp64 MFMA layout (pdhg_mfma.hip, 16 scenarios per wave);
+ *            else the lane-local register layout (pdhg_local.hip) when the pattern splits into
+ *            blocks that fit a lane plus <= a few coupling rows, else the wave LDS-gather layout
  *            (pdhg.hip, n, m <= 256), else the workgroup-per-scenario streaming layout
  *            (pdhg_block.hip, n, m up to 4096)
- *   GATHER / LOCAL / BLOCK : that layout or fail                                                */
-enum { PHG_LAYOUT_AUTO = 0, PHG_LAYOUT_GATHER = 1, PHG_LAYOUT_LOCAL = 2, PHG_LAYOUT_BLOCK = 3 };
+ *   GATHER / LOCAL / BLOCK / MFMA : that layout or fail (MFMA: shared matrix only)              */
+enum { PHG_LAYOUT_AUTO = 0, PHG_LAYOUT_GATHER = 1, PHG_LAYOUT_LOCAL = 2, PHG_LAYOUT_BLOCK = 3,
+       PHG_LAYOUT_MFMA = 4 };
 int  phg_set_layout(phg_handle* h, int32_t policy);
 /* host-only dry run of the lane-local planner (no device needed): out8 = {local variant or -1,
  * lanes per scenario, columns per lane, rows per lane, coupling-row slots, coupling rows used,
@@ -165,8 +170,12 @@ int  phg_load_batch(phg_handle* h, const phg_batch* b);
 int  phg_set(phg_handle* h, int32_t field, const double* host_in);
 int  phg_get(phg_handle* h, int32_t field, double* host_out);
 int  phg_get_i32(phg_handle* h, int32_t field, int32_t* host_out);
+/* shared-matrix MFMA layout: out4 = {row tiles, column tiles, 16x4 fragments with a nonzero in
+ * A x, in A^T y} (each is one v_mfma_f64_16x16x4_f64 per PDHG iteration per 16 scenarios)       */
+int  phg_mfma_info(phg_handle* h, int32_t* out4);
 int  phg_info(phg_handle* h, int32_t* out8);   /* S, n, m, nnz, N, N_tot, kernel variant
-                                                  (>= 100: lane-local, >= 200: workgroup),
+                                                  (>= 100: lane-local, >= 200: workgroup,
+                                                  >= 300: shared-matrix MFMA),
                                                   lanes (threads) per scenario             */
 
 /* Solve every scenario's subproblem (solve_loop):

@@ -33,6 +33,9 @@ int pdhg_block_num_variants();
 void pdhg_block_variant_shape(int v, int* out5);
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad);
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
+int pdhg_mfma_num_variants();
+void pdhg_mfma_variant_shape(int v, int* out2);
+hipError_t pdhg_mfma_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t piece_gather_launch(const double* vals, int nnz, const int* perm, int E, int S, double* out,
                                hipStream_t st);
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
@@ -78,6 +81,9 @@ struct phg_handle {
     int variant = -1;          // gather kernel variant (pdhg.hip), or
     int local_variant = -1;    // lane-local kernel variant (pdhg_local.hip); preferred when >= 0
     int block_variant = -1;    // workgroup-per-scenario kernel variant (pdhg_block.hip)
+    int mfma_variant = -1;     // shared-matrix MFMA kernel variant (pdhg_mfma.hip)
+    int mshape[2] = {0, 0};
+    MfmaLayout mf{};
     int bshape[5] = {0};
     std::vector<int> block_rperm, block_cperm;   // piece layout -> CSR position (host copies)
     bool vals_shared = false;
@@ -313,7 +319,7 @@ int phg_set_smoothing(phg_handle* h, int32_t on) {
 int phg_set_layout(phg_handle* h, int32_t policy) {
     if (!h) return fail("null handle");
     if (h->loaded) return fail("phg_set_layout: must be called before phg_load_batch");
-    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_BLOCK) return fail("phg_set_layout: bad policy");
+    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_MFMA) return fail("phg_set_layout: bad policy");
     h->layout_policy = policy;
     return 0;
 }
@@ -854,6 +860,67 @@ static int build_block_values(phg_handle* h) {
     return 0;
 }
 
+// Shared-matrix MFMA layout (pdhg_mfma.hip).  Planner: the smallest tile grid (16 TM rows x 16 TN
+// columns) holding the matrix; used by AUTO when the matrix is the same in every scenario and
+// fills at least 1/16 of the padded tiles (below that the dense products waste more than 15 of 16
+// MFMA lanes and the sparse layouts win).  Returns 0 (chosen), 1 (does not fit / not chosen).
+static constexpr int kMfmaMinScenarios = 4096;
+
+static int pick_mfma_variant(const phg_batch* b, bool shared, bool forced, int* shape) {
+    if (!shared) return -1;
+    for (int v = 0; v < pdhg_mfma_num_variants(); ++v) {
+        int sh[2];
+        pdhg_mfma_variant_shape(v, sh);
+        if (b->m > 16 * sh[0] || b->n > 16 * sh[1]) continue;
+        if (!forced && 16L * b->nnz < 256L * sh[0] * sh[1]) return -1;   // density rule
+        // size rule: 16 scenarios per wave means S / 16 waves; below ~one wave per CU the
+        // one-scenario-per-wave kernels finish sooner (their PDHG iteration is shorter and they
+        // spread over more SIMDs).  Measured on hydro trees (MI355X): S = 2 000 gather 0.240 ms vs
+        // MFMA 0.368 ms per launch; S = 20 000 gather 1.018 ms vs MFMA 0.426 ms
+        if (!forced && b->S < kMfmaMinScenarios) return -1;
+        shape[0] = sh[0];
+        shape[1] = sh[1];
+        return v;
+    }
+    return -1;
+}
+
+// Fragments of the SCALED shared matrix (scenario 0's values after prep: every scenario's are the
+// same, prep being deterministic on identical input) in the order pdhg_mfma_kernel reads them.
+static int build_mfma_fragments(phg_handle* h, const phg_batch* b) {
+    const int TM = h->mshape[0], TN = h->mshape[1], NF = 4 * TM * TN;
+    const int M = 16 * TM, N = 16 * TN;
+    std::vector<double> v0(b->nnz);
+    CK(hipMemcpyAsync(v0.data(), h->vals, b->nnz * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    std::vector<double> A((size_t)M * N, 0.0);
+    for (int i = 0; i < b->m; ++i)
+        for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) A[(size_t)i * N + b->colidx[p]] = v0[p];
+    std::vector<double> fr((size_t)2 * NF * 64, 0.0);
+    unsigned long long nza = 0, nzb = 0;
+    for (int t = 0; t < TM; ++t)
+        for (int u = 0; u < TN; ++u)
+            for (int j = 0; j < 4; ++j) {
+                const int fa = (t * TN + u) * 4 + j, fb = (u * TM + t) * 4 + j;
+                for (int l = 0; l < 64; ++l) {
+                    // A x: A[16 t + (l & 15)][16 u + 4 j + (l >> 4)]
+                    const double va = A[(size_t)(16 * t + (l & 15)) * N + 16 * u + 4 * j + (l >> 4)];
+                    // A^T y: A[16 t + 4 j + (l >> 4)][16 u + (l & 15)]
+                    const double vb = A[(size_t)(16 * t + 4 * j + (l >> 4)) * N + 16 * u + (l & 15)];
+                    fr[(size_t)fa * 64 + l] = va;
+                    fr[(size_t)(NF + fb) * 64 + l] = vb;
+                    if (va != 0.0) nza |= 1ull << fa;
+                    if (vb != 0.0) nzb |= 1ull << fb;
+                }
+            }
+    double* d;
+    if (dput(h, &d, fr.data(), fr.size())) return -1;
+    h->mf.frag = d;
+    h->mf.nz_ax = nza;
+    h->mf.nz_aty = nzb;
+    return 0;
+}
+
 // ----------------------------------------------------------------------------- presolve
 // Singleton rows (PDLP-style presolve): a row  lo <= a x_j <= hi  with ONE nonzero, on a column
 // that is not a nonant, is the column bound  lo/a <= x_j <= hi/a  (swapped for a < 0).  The LP is
@@ -1051,24 +1118,8 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
         if (dput(h, &p, col_nonant.data(), col_nonant.size())) return -1;
         h->lay.col_nonant = p;
     }
-    // layout: lane-local (block-structured patterns) > wave gather (n, m <= 256) > workgroup block
-    int lr = 1, gr = 1, br = 1;
-    const int pol = h->layout_policy;
-    if (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_LOCAL) {
-        lr = build_local_layout(h, b);
-        if (lr < 0) return -1;
-        if (lr > 0 && pol == PHG_LAYOUT_LOCAL) return -1;
-    }
-    if (lr != 0 && (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_GATHER)) {
-        gr = build_layout(h, b, colptr, csc_row, csc_p);
-        if (gr < 0 || (gr > 0 && pol == PHG_LAYOUT_GATHER)) return -1;
-    }
-    if (lr != 0 && gr != 0) {
-        br = build_block_layout(h, b, colptr, csc_row, csc_p);
-        if (br != 0) return -1;
-        h->variant = -1;
-    }
-    // one matrix for all scenarios? (then the block kernel streams a single copy)
+    // one matrix for all scenarios? (then the block kernel streams a single copy, and the MFMA
+    // layout applies)
     {
         bool same = true;
         const size_t nz = (size_t)b->nnz;
@@ -1076,6 +1127,32 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
             same = std::memcmp(b->vals, b->vals + s2 * nz, nz * sizeof(double)) == 0;
         h->vals_shared = same;
     }
+    // layout: shared-matrix MFMA > lane-local (block-structured patterns) > wave gather
+    // (n, m <= 256) > workgroup block
+    int lr = 1, gr = 1, br = 1;
+    const int pol = h->layout_policy;
+    if (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_MFMA) {
+        h->mfma_variant = pick_mfma_variant(b, h->vals_shared, pol == PHG_LAYOUT_MFMA, h->mshape);
+        if (h->mfma_variant < 0 && pol == PHG_LAYOUT_MFMA)
+            return fail(h->vals_shared ? "phg_load_batch: the matrix does not fit the MFMA tile (n, m <= 16)"
+                                       : "phg_load_batch: the MFMA layout needs one matrix shared by all scenarios");
+        if (h->mfma_variant >= 0) lr = gr = br = 0;
+    }
+    if (h->mfma_variant < 0 && (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_LOCAL)) {
+        lr = build_local_layout(h, b);
+        if (lr < 0) return -1;
+        if (lr > 0 && pol == PHG_LAYOUT_LOCAL) return -1;
+    }
+    if (h->mfma_variant < 0 && lr != 0 && (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_GATHER)) {
+        gr = build_layout(h, b, colptr, csc_row, csc_p);
+        if (gr < 0 || (gr > 0 && pol == PHG_LAYOUT_GATHER)) return -1;
+    }
+    if (h->mfma_variant < 0 && lr != 0 && gr != 0) {
+        br = build_block_layout(h, b, colptr, csc_row, csc_p);
+        if (br != 0) return -1;
+        h->variant = -1;
+    }
+    if (h->mfma_variant >= 0) h->variant = -1;
     // min-form objective
     std::vector<double> cmin((size_t)S * n), off((size_t)S, 0.0);
     for (size_t e = 0; e < cmin.size(); ++e) cmin[e] = h->sense * b->c[e];
@@ -1146,15 +1223,27 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     pa.ru = h->ru; pa.eta = h->eta; pa.bnorm = h->bnorm; pa.scratch = scratch;
     CK(prep_launch(pa, h->stream));
     if (h->block_variant >= 0 && build_block_values(h)) return -1;
+    if (h->mfma_variant >= 0 && build_mfma_fragments(h, b)) return -1;
     CK(hipStreamSynchronize(h->stream));
     h->loaded = true;
+    return 0;
+}
+
+int phg_mfma_info(phg_handle* h, int32_t* o) {
+    if (!h || !h->loaded || !o) return fail("phg_mfma_info: no batch loaded");
+    if (h->mfma_variant < 0) return fail("phg_mfma_info: the batch does not use the MFMA layout");
+    o[0] = h->mshape[0];
+    o[1] = h->mshape[1];
+    o[2] = __builtin_popcountll(h->mf.nz_ax);
+    o[3] = __builtin_popcountll(h->mf.nz_aty);
     return 0;
 }
 
 int phg_info(phg_handle* h, int32_t* o) {
     if (!h || !h->loaded) return fail("phg_info: no batch loaded");
     o[0] = h->S; o[1] = h->n; o[2] = h->m_orig; o[3] = h->nnz; o[4] = h->N; o[5] = h->N_tot;
-    if (h->local_variant >= 0) { o[6] = 100 + h->local_variant; o[7] = h->lshape[0]; }
+    if (h->mfma_variant >= 0) { o[6] = 300 + h->mfma_variant; o[7] = 4; }
+    else if (h->local_variant >= 0) { o[6] = 100 + h->local_variant; o[7] = h->lshape[0]; }
     else if (h->block_variant >= 0) { o[6] = 200 + h->block_variant; o[7] = h->bshape[0]; }
     else { o[6] = h->variant; o[7] = 64; }
     return 0;
@@ -1264,14 +1353,16 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.beta_nec = o->beta_necessary > 0 ? o->beta_necessary : 0.8;
     a.beta_art = o->beta_artificial > 0 ? o->beta_artificial : 0.25;
     a.theta = o->primal_weight_theta > 0 && o->primal_weight_theta <= 1 ? o->primal_weight_theta : 0.8;
-    if (h->local_variant >= 0) a.check_every = (a.check_every + 1) & ~1;   // 2 iterations per trip
+    if (h->local_variant >= 0 || h->mfma_variant >= 0) a.check_every = (a.check_every + 1) & ~1;   // 2 iterations per trip
     if (timing_event(h, 0, 0)) return -1;
     a.loc = h->loc;
     a.blk = h->blk;
+    a.mf = h->mf;
     a.gate = o->skip_if_conv_below > 0 ? h->gate : nullptr;
     a.gate_below = o->skip_if_conv_below;
     a.queue = h->persist ? h->queue : nullptr;
-    if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
+    if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
+    else if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
     if (timing_event(h, 0, 1)) return -1;

@@ -59,11 +59,21 @@ struct BlockLayout {
     long vstride_r, vstride_c;   // per-scenario strides (0: one matrix shared by all scenarios)
 };
 
+// Shared-matrix MFMA layout (pdhg_mfma.hip): the A operands of v_mfma_f64_16x16x4_f64 for A x
+// (fragment (t, u, j): lane l holds A_hat[16 t + (l & 15)][16 u + 4 j + (l >> 4)]) and for A^T y
+// (fragment (u, t, j): lane l holds A_hat[16 t + 4 j + (l >> 4)][16 u + (l & 15)]), [fragment][64],
+// and which fragments hold a nonzero
+struct MfmaLayout {
+    const double* frag;     // [2 * 4 TM TN][64]
+    unsigned long long nz_ax, nz_aty;
+};
+
 struct PdhgArgs {
     int S, n, m, nnz, N, n_pad;
     Layout lay;
     LocalLayout loc;
     BlockLayout blk;
+    MfmaLayout mf;
     // scenario data (scaled where noted)
     const double* vals;     // [S*nnz] scaled values
     const double* c;        // [S*n]   min-form objective, UNscaled

@@ -133,6 +133,10 @@ class OraclePH:
         self.solve_count += 1
         if not r.ok:
             self.feasible[k] = False
+            import os
+            if os.environ.get("ORACLE_DUMP"):
+                np.savez(os.environ["ORACLE_DUMP"], c=c, q=q if q is not None else np.zeros(0), off=off,
+                         **{kk: np.asarray(v) for kk, v in a.items()})
             raise RuntimeError(f"[oracle] Solve failed for scenario {self.names[k]}: {r.status}")
         self.feasible[k] = True
         self.x[k] = r.x

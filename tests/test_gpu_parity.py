@@ -149,7 +149,7 @@ def test_prox_qp_solves_vs_oracle(S, cm, layout):
         np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6)
 
 
-@pytest.mark.parametrize("layout", ["gather", "block"])
+@pytest.mark.parametrize("layout", ["gather", "block", "mfma"])
 @pytest.mark.parametrize("tree", ["bf33", (2, 1, 4), (5, 15, 30)])
 def test_hydro_prox_qp_solves_vs_oracle(tree, layout):
     """Multistage prox-QPs with identical W and per-NODE xbar in both solvers (the xbar slot of each
