@@ -90,10 +90,11 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
         for (int t = 0; t < KRS; ++t) { rv[r][t] = 0.0; rc[r][t] = 0; }
         if (i >= 0) {
             const long b = sm + i;
-            rlo[r] = a.rl[b];
-            rhi[r] = a.ru[b];
+            row_bounds(a, i, b, rlo[r], rhi[r]);
             drs[r] = a.dr[b];
             y[r] = (a.warm & 1) ? a.ys_in[b] : 0.0;
+            if (!fin(rlo[r])) y[r] = fmin(y[r], 0.0);   // a warm dual must fit the row's bounds
+            if (!fin(rhi[r])) y[r] = fmax(y[r], 0.0);
 #pragma unroll
             for (int t = 0; t < KRS; ++t) {
                 const int idx = (l * RPL + r) * KRS + t;

@@ -105,8 +105,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
         if (i >= 0) {
             const long b = sm + i;
-            rlo[r] = a.rl[b];
-            rhi[r] = a.ru[b];
+            row_bounds(a, i, b, rlo[r], rhi[r]);
             double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
             if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
             if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];

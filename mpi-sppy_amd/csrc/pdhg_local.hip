@@ -338,8 +338,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                 if (i >= 0) {
                     const long b = sm + i;
                     CS(CI::IDR + r) = 1.0 / a.dr[b];
-                    rlo[r] = a.rl[b];
-                    rhi[r] = a.ru[b];
+                    row_bounds(a, i, b, rlo[r], rhi[r]);
                     double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
                     if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
                     if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];
@@ -367,8 +366,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                 if (i >= 0) {
                     const long b = sm + i;
                     GS(CI::IDRD + d) = 1.0 / a.dr[b];
-                    dlo[d] = a.rl[b];
-                    dhi[d] = a.ru[b];
+                    row_bounds(a, i, b, dlo[d], dhi[d]);
                     double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
                     if (!fin(dlo[d])) yy = fmin(yy, 0.0); else b2d += dlo[d] * dlo[d];
                     if (!fin(dhi[d])) yy = fmax(yy, 0.0); else b2d += dhi[d] * dhi[d];

@@ -125,8 +125,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
             if (i < a.m) {
                 const long b = sm + i;
                 CS(CI::IDR + r) = 1.0 / a.dr[b];
-                rlo[r] = a.rl[b];
-                rhi[r] = a.ru[b];
+                row_bounds(a, i, b, rlo[r], rhi[r]);
                 double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
                 if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
                 if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];

@@ -119,6 +119,7 @@ struct phg_handle {
     double* pinned = nullptr;  // page-locked readback buffer (convergence partials)
     int summary[2] = {0, 0};   // scenarios not optimal / NaN, as of the last phg_conv_finish
     int* nonant_col_d = nullptr;
+    unsigned char* row_fixed = nullptr;   // [m] every column of the (kept) row is a nonant
     Layout lay{};
     LocalLayout loc{};
     BlockLayout blk{};
@@ -1202,6 +1203,17 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     if (dalloc(h, &h->order, S)) return -1;
     if (dalloc(h, &h->queue, 2)) return -1;
     h->nonant_col_h.assign(b->nonant_col, b->nonant_col + N);
+    {   // rows made constant by fixing the nonants (row_bounds in phg_internal.h)
+        std::vector<char> isn(n, 0);
+        for (int k = 0; k < N; ++k) isn[b->nonant_col[k]] = 1;
+        std::vector<unsigned char> rf(m, 0);
+        for (int i = 0; i < m; ++i) {
+            bool all = b->rowptr[i + 1] > b->rowptr[i];
+            for (int p = b->rowptr[i]; p < b->rowptr[i + 1] && all; ++p) all = isn[b->colidx[p]] != 0;
+            rf[i] = all ? 1 : 0;
+        }
+        if (dput(h, &h->row_fixed, rf.data(), rf.size())) return -1;
+    }
     if (dput(h, &h->nonant_col_d, b->nonant_col, N)) return -1;
     if (build_ph_tables(h, b)) return -1;
     h->ph.status = h->status;
@@ -1347,6 +1359,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.order = (o->schedule && h->have_order) ? h->order : nullptr;
     a.iters_acc = h->iters_acc;
     a.w_on = w_on; a.prox_on = prox_on; a.fix_nonants = o->fix_nonants; a.fix_tol = o->fix_tol > 0 ? o->fix_tol : 0.0;
+    a.row_fixed = h->row_fixed;
     a.warm = o->warm_start;
     a.max_iter = o->max_iter; a.check_every = o->check_every; a.eps = o->eps_rel; a.sense = h->sense;
     a.beta_suf = o->beta_sufficient > 0 ? o->beta_sufficient : 0.2;

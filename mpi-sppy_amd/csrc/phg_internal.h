@@ -116,6 +116,7 @@ struct PdhgArgs {
     long long* iters_acc;   // [S] PDHG iterations accumulated over solves (phg_timing_reset zeroes)
     int w_on, prox_on, fix_nonants, warm, max_iter, check_every;
     double fix_tol;                        // fixed nonants: box of half-width fix_tol max(1, |v|)
+    const unsigned char* row_fixed;        // [m] 1: every column of the row is a nonant
     double eps, sense;
     double beta_suf, beta_nec, beta_art;   // restart rule
     double theta;                          // primal weight smoothing (1: no smoothing)
@@ -222,6 +223,17 @@ __device__ __forceinline__ void fixed_box(const PdhgArgs& a, long t, double d, d
     const double w = a.fix_tol * fmax(1.0, fabs(v));
     lo = (v - w) / d;
     hi = (v + w) / d;
+}
+
+// scaled bounds of row i (b = s*m + i): with the nonants fixed (xhat evaluation), a row all of whose
+// columns are nonants is a constant -- a CPU solver's presolve drops it (or declares the candidate
+// infeasible when it is violated beyond its feasibility tolerance; the caller checks that on the
+// host, cylinders.evaluate_xhat).  Kept as a row with a first-order solver it would be an equality
+// between constants that round-off makes infeasible, sending the dual iterates off along the ray.
+__device__ __forceinline__ void row_bounds(const PdhgArgs& a, int i, long b, double& lo, double& hi) {
+    if (a.fix_nonants && a.row_fixed && a.row_fixed[i]) { lo = -INFINITY; hi = INFINITY; return; }
+    lo = a.rl[b];
+    hi = a.ru[b];
 }
 
 // PDLP primal weight update at a restart: omega <- (dy/dx)^theta omega^(1-theta), from the squared

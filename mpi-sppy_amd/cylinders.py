@@ -156,9 +156,9 @@ class XhatShuffleInnerBound(_BoundSpoke):
         self.best_X = None           # local scenarios x n: the incumbent's full solution
         # an infeasible fixing would run PDHG to its cap: tries use a smaller one
         self.max_iter = int(self.options.get("xhat_max_iter", 20000))
-        # fixed values get a box of half-width xhat_fix_tol * max(1, |v|) (phg_opts.fix_tol): the
-        # CPU solver's feasibility tolerance of the reference's exact fixing
-        self.fix_tol = float(self.options.get("xhat_fix_tol", 1e-9))
+        # fixed values may get a box of half-width xhat_fix_tol * max(1, |v|) (phg_opts.fix_tol);
+        # first-stage rows are dropped by the kernels while the nonants are fixed (row_bounds)
+        self.fix_tol = float(self.options.get("xhat_fix_tol", 0.0))
 
     def _candidate_row(self, gidx):
         """Nonants of global scenario gidx from the hub (host vector; summed over ranks)."""
@@ -205,14 +205,51 @@ class XhatShuffleInnerBound(_BoundSpoke):
         return val
 
 
-def evaluate_xhat(opt, xhat, eps=None, max_iter=200000, fix_tol=1e-9):
+def fixed_rows_violation(batch, xhat):
+    """Largest violation, relative to max(1, |bound|), of the rows whose columns are all nonants
+    (first-stage rows) by the candidate ``xhat`` over the batch's scenarios.  With the nonants fixed
+    these rows are constants, which the kernels drop (phg_internal.h: row_bounds) -- as a CPU
+    solver's presolve does -- so the candidate's feasibility for them is decided here."""
+    cols = np.asarray(batch.nonant_col)
+    pos = {int(c): k for k, c in enumerate(cols)}
+    worst = 0.0
+    for i in range(batch.m):
+        p0, p1 = int(batch.rowptr[i]), int(batch.rowptr[i + 1])
+        cj = batch.colidx[p0:p1]
+        if p1 == p0 or any(int(c) not in pos for c in cj):
+            continue
+        xv = np.array([xhat[pos[int(c)]] for c in cj])
+        ax = batch.vals[:, p0:p1] @ xv
+        lo, hi = batch.rl[:, i], batch.ru[:, i]
+        with np.errstate(invalid="ignore"):
+            v = np.maximum(np.where(np.isfinite(lo), (lo - ax) / np.maximum(1.0, np.abs(lo)), 0.0),
+                           np.where(np.isfinite(hi), (ax - hi) / np.maximum(1.0, np.abs(hi)), 0.0))
+        worst = max(worst, float(np.max(v)))
+    return worst
+
+
+def evaluate_xhat(opt, xhat, eps=None, max_iter=200000, fix_tol=0.0, feas_tol=1e-7):
     """Inner bound of a two-stage candidate (``xhat_eval.py:102-170`` / ``xhatbase.py:42-235``):
     every local scenario's nonants fixed to ``xhat`` (one vector, node order), W and prox off, one
     batched solve on a temporary handle holding ``opt``'s batch; sum_s p_s obj_s (math.fsum per
-    rank, SUM across ranks) if every scenario reached the KKT tolerance, else None."""
+    rank, SUM across ranks) if every scenario reached the KKT tolerance, else None.
+
+    First-stage rows (every column a nonant) are checked here against ``feas_tol`` relative to
+    max(1, |bound|) -- the part the CPU solver's feasibility tolerance plays in the reference -- and
+    dropped from the device solves (they are constants once the nonants are fixed).  A candidate
+    assembled from first-order solves at relative KKT 1e-9 meets such a row only to
+    eps (1 + ||b||): on farmer cm=10 (quota bounds of 1e5 in b) up to ~5e-4 acres on the
+    5 000-acre total-acreage row, hence 1e-7.  ``fix_tol`` (phg_opts.fix_tol) additionally lets each
+    fixed value move by fix_tol * max(1, |v|) (0: exact)."""
     he = opt.engine
     if he.batch.L != 1:
         raise NotImplementedError("evaluate_xhat: two-stage batches")
+    viol = fixed_rows_violation(he.batch, np.asarray(xhat, np.float64))
+    if opt.n_proc > 1:
+        viol = opt.mpicomm.allreduce_scalar(viol)   # sum over ranks >= the largest (conservative)
+    evaluate_xhat.last_violation = viol
+    if viol > feas_tol:
+        return None
     dev = 0
     try:
         import torch
@@ -242,7 +279,7 @@ def evaluate_xhat(opt, xhat, eps=None, max_iter=200000, fix_tol=1e-9):
         eng.close()
 
 
-def evaluate_lagrangian(opt, eps=None, max_iter=200000):
+def evaluate_lagrangian(opt, eps=None, max_iter=1000000):
     """Lagrangian outer bound with ``opt``'s current W (``lagrangian_bounder.py:21-44``): every
     local scenario with W on and prox off, one batched solve on a temporary handle; sum_s p_s
     bound_s (the PDHG dual objective, valid at KKT-optimal points), or None if any scenario did
@@ -263,7 +300,9 @@ def evaluate_lagrangian(opt, eps=None, max_iter=200000):
         eng.solve(1, 0, eps=eps or o["pdhg_eps"], max_iter=max_iter, check_every=o["pdhg_check_every"],
                   warm_start=0, schedule=False)
         eng.sync()
-        bad = float((eng.get_i32(_lib.I_STATUS) != 0).sum())
+        st = eng.get_i32(_lib.I_STATUS)
+        evaluate_lagrangian.last_status_counts = np.bincount(st, minlength=3).tolist()
+        bad = float((st != 0).sum())
         if opt.n_proc > 1:
             bad = opt.mpicomm.allreduce_scalar(bad)
         if bad:

@@ -99,7 +99,19 @@ def solve(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=None, o
     cd = np.array(sol.col_dual, dtype=np.float64) if sol.dual_valid else None
     if qdiag is not None and np.any(np.asarray(qdiag) != 0) and st != "Optimal" and do_polish and time_limit is None:
         # HiGHS 1.8's QP solver occasionally ends in "Solve error" on a prox-QP that is plainly
-        # feasible and bounded (farmer cm=10 deep in a PH run): the interior-point oracle certifies it
+        # feasible and bounded (farmer cm=10 deep in a PH run, LP part solved by the same HiGHS):
+        # retry with the infinite column bounds capped far outside the data (the cap must be
+        # inactive at the solution), then the usual certify / polish / IPM chain; else the IPM alone
+        cu = np.asarray(col_hi, dtype=np.float64)
+        if not np.all(np.isfinite(cu)):
+            fin_ = np.abs(np.concatenate([np.asarray(v, float)[np.isfinite(v)] for v in
+                                          (col_lo, col_hi, row_lo, row_hi)] + [np.zeros(1)]))
+            cap = 1e3 * max(1.0, float(fin_.max()))
+            r = solve(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, np.where(np.isfinite(cu), cu, cap),
+                      qdiag=qdiag, offset=offset, threads=threads, tol=tol, presolve=presolve,
+                      do_polish=do_polish)
+            if r.ok and np.all(np.abs(r.x[~np.isfinite(cu)]) < 0.5 * cap):
+                return r
         from . import ipm
         r = ipm.solve_qp(c, rowptr, colidx, vals, row_lo, row_hi, col_lo, col_hi, qdiag=qdiag, offset=offset)
         if r.ok:

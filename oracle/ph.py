@@ -135,7 +135,7 @@ class OraclePH:
             self.feasible[k] = False
             import os
             if os.environ.get("ORACLE_DUMP"):
-                np.savez(os.environ["ORACLE_DUMP"], c=c, q=q if q is not None else np.zeros(0), off=off,
+                np.savez(os.environ["ORACLE_DUMP"], cost=c, q=q if q is not None else np.zeros(0), off=off,
                          **{kk: np.asarray(v) for kk, v in a.items()})
             raise RuntimeError(f"[oracle] Solve failed for scenario {self.names[k]}: {r.status}")
         self.feasible[k] = True

@@ -99,3 +99,29 @@ def test_hydro_ef():
     obj, xs = ph.ef_solve(sc)
     np.testing.assert_allclose(xs[0][:4], [30.0, 60.0, 0.0, 54.432], atol=1e-6)
     assert round_pos_sig(xs[6][4], 1) == 60      # Scen7.Pgt[2]
+
+
+def test_farmer_ef_fixture_generators_agree():
+    """The EF fixtures of the north-star test (tests/golden/make_ef_fixtures.py): the exact
+    separable solution (used at S = 10 000, where the 1.2M-column LP is out of reach of HiGHS here)
+    equals the HiGHS LP extensive form on the same restated scenario LPs (S = 30), objective and
+    first-stage solution; and the committed fixtures hold those values."""
+    import json
+    import os
+    import sys
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    sys.path.insert(0, gold)
+    import make_ef_fixtures as mk
+    obj, root = mk.farmer_ef_separable(30)
+    c, A, rlo, rhi, clo, chi, cols, n, _ = mk.farmer_ef(30)
+    st, x, lp_obj, _, _ = mk.solve_lp(c, A, rlo, rhi, clo, chi, threads=1)
+    assert st == "Optimal"
+    assert abs(obj - lp_obj) <= 1e-12 * abs(lp_obj)
+    np.testing.assert_allclose(root, x[cols], atol=1e-8)
+    for S in (30, 1000, 10000):
+        d = json.load(open(os.path.join(gold, f"farmer_cm10_ef_S{S}.json")))
+        assert d["status"] == "Optimal" and d["S"] == S
+        if S == 30:
+            assert abs(d["objective"] - obj) <= 1e-12 * abs(obj)
+        if "lp_ef_objective" in d:
+            assert d["rel_diff_vs_lp_ef"] <= 1e-10
