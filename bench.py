@@ -32,12 +32,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--case", default="farmer", choices=["farmer", "sslp", "netdes", "hydro"],
+    ap.add_argument("--case", default="farmer", choices=["farmer", "sslp", "netdes", "hydro", "uc"],
                     help="workload: farmer (the BASELINE.json headline, configs[1]), sslp_15_45_10 or "
-                         "netdes network-50-30-H-01 LP relaxations (configs[2], configs[4]), or a "
-                         "non-uniform 3-stage hydro tree (configs[3], SURVEY 8(d) M3)")
+                         "netdes network-50-30-H-01 LP relaxations (configs[2], configs[4]), a "
+                         "non-uniform 3-stage hydro tree (configs[3], SURVEY 8(d) M3), or the synthetic "
+                         "UC-shaped LP relaxation (configs[4], SURVEY 8(d) M5)")
     ap.add_argument("--scen", type=int, default=None,
-                    help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes, 2000 hydro")
+                    help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes, 2000 hydro, 64 uc")
     ap.add_argument("--cm", type=int, default=10)
     ap.add_argument("--rho", type=float, default=1.0)
     ap.add_argument("--eps", type=float, default=1e-9)
@@ -50,7 +51,7 @@ def parse():
                          "case, i.e. farmer 10k = the BASELINE headline, sharded over the N GPUs: strong "
                          "scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0: skip)")
-    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local", "block", "mfma"],
+    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local", "block", "mfma", "stream"],
                     help="PDHG data layout (include/phg.h: phg_set_layout)")
     ap.add_argument("--no-schedule", action="store_true", help="launch scenarios in index order")
     ap.add_argument("--check-every", type=int, default=32, help="PDHG restart/termination check interval")
@@ -106,7 +107,7 @@ def _cpu_share():
     return max(1, min(share, vis)), vis, why
 
 
-def _case_setup(args, S, farmer, hydro, netdes, sslp):
+def _case_setup(args, S, farmer, hydro, netdes, sslp, uc=None):
     nodenames = None
     if args.case == "farmer":
         names, creator = farmer.scenario_names_creator(S), farmer.scenario_creator
@@ -120,6 +121,9 @@ def _case_setup(args, S, farmer, hydro, netdes, sslp):
         names, creator, ckw = hydro.scenario_names_creator(S), hydro.synthetic_scenario_creator, {"fanouts": fan}
         nodenames = hydro.synthetic_nodenames(fan)
         desc = f"hydro 3-stage non-uniform tree, stage-2 fan-outs {list(fan)}"
+    elif args.case == "uc":
+        names, creator, ckw = uc.scenario_names_creator(S), uc.scenario_creator, {"num_scens": S}
+        desc = "synthetic UC-shaped LP relaxation (85 generators x 48 periods, N = 4080)"
     else:
         names, creator, ckw = netdes.scenario_names_creator(S), netdes.scenario_creator, {"num_scens": S}
         desc = "netdes network-50-30-H-01 LP relaxation"
@@ -166,16 +170,16 @@ def main():
     from mpisppy_amd import _lib
     from mpisppy_amd import cylinders
     from mpisppy_amd.comm import TorchComm
-    from mpisppy_amd.examples import farmer, hydro, netdes, sslp
+    from mpisppy_amd.examples import farmer, hydro, netdes, sslp, uc
     from mpisppy_amd.ph import PH
     if world > 1:
         comm = TorchComm()
 
-    default_scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024, "hydro": 2000}[args.case]
+    default_scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024, "hydro": 2000, "uc": 64}[args.case]
     if args.scen is None:
         args.scen = default_scen
     S = args.scen * world
-    names, creator, ckw, nodenames, desc = _case_setup(args, S, farmer, hydro, netdes, sslp)
+    names, creator, ckw, nodenames, desc = _case_setup(args, S, farmer, hydro, netdes, sslp, uc)
     opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
             "convthresh": 1e-4, "verbose": False, "display_progress": False, "pdhg_layout": args.layout,
             "pdhg_schedule": not args.no_schedule, "pdhg_check_every": args.check_every,
@@ -318,6 +322,8 @@ def main():
                  "netdes": "network-50-30-H-01 data (30 scenarios) + seeded synthetic cost/capacity noise beyond 30",
                  "hydro": "hydro model of examples/hydro/hydro.py, synthetic inflows A2~U[10,90] per node, "
                           "A3~U[40,60] per leaf (default_rng(1134))",
+                 "uc": "synthetic UC-shaped LP (examples/uc.py; egret, which the reference's uc needs, is absent): "
+                       "seeded generator data, per-scenario demand and unit derates",
                  }[args.case],
         "config": {"workload": f"{desc}, {S} scenarios ({args.scen} per GPU), PH rho={args.rho}, "
                                f"PDHG eps_rel={args.eps}",
@@ -339,7 +345,9 @@ def main():
                      "kernel": {"local": "pdhg_local_kernel (lane-local, fp64 VALU)",
                                 "gather": "pdhg_kernel (wave LDS-gather, fp64 VALU)",
                                 "block": "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)",
-                                "mfma": "pdhg_mfma_kernel (shared matrix, v_mfma_f64_16x16x4_f64, 16 scenarios per wave)"}[eng.layout],
+                                "mfma": "pdhg_mfma_kernel (shared matrix, v_mfma_f64_16x16x4_f64, 16 scenarios per wave)",
+                                "stream": f"pdhg_stream_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
+                                          "iterates and values streamed)"}[eng.layout],
                      "flops_per_pdhg_iter_per_scen": f_it,
                      "pdhg_iters_per_scen_per_step": round(pdhg_iters / args.steps / S_loc, 2),
                      "max_pdhg_iters": max_iters,
@@ -372,7 +380,7 @@ def main():
         S_c = args.conv_scen or default_scen
         if S_c % world:
             S_c -= S_c % world
-        names_c, creator_c, ckw_c, nodenames_c, _ = _case_setup(args, S_c, farmer, hydro, netdes, sslp)
+        names_c, creator_c, ckw_c, nodenames_c, _ = _case_setup(args, S_c, farmer, hydro, netdes, sslp, uc)
         copts = dict(opts, PHIterLimit=args.conv_iters, convthresh=1e-4,
                      time_limit=None if args.case == "farmer" else args.conv_time)
         ph2 = PH(copts, names_c, creator_c, mpicomm=comm, scenario_creator_kwargs=ckw_c, all_nodenames=nodenames_c)
@@ -429,7 +437,7 @@ def _cpu_worker(payload):
     from oracle import highs
     from oracle import models as om
     case, names, kw, W, xbar, rho, budget = payload
-    build = {"farmer": om.farmer, "sslp": om.sslp, "netdes": om.netdes, "hydro": om.hydro_tree}[case]
+    build = {"farmer": om.farmer, "sslp": om.sslp, "netdes": om.netdes, "hydro": om.hydro_tree, "uc": om.uc}[case]
     cnt = 0
     t0 = _t.perf_counter()
     for k, nm in enumerate(names):

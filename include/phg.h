@@ -150,10 +150,11 @@ int  phg_sync(phg_handle* h);
  *            else the lane-local register layout (pdhg_local.hip) when the pattern splits into
  *            blocks that fit a lane plus <= a few coupling rows, else the wave LDS-gather layout
  *            (pdhg.hip, n, m <= 256), else the workgroup-per-scenario streaming layout
- *            (pdhg_block.hip, n, m up to 4096)
- *   GATHER / LOCAL / BLOCK / MFMA : that layout or fail (MFMA: shared matrix only)              */
+ *            (pdhg_block.hip, n, m up to 4096), else the multi-workgroup streaming layout
+ *            (pdhg_stream.hip, any size: K workgroups per scenario, everything streamed)
+ *   GATHER / LOCAL / BLOCK / MFMA / STREAM : that layout or fail (MFMA: shared matrix only)     */
 enum { PHG_LAYOUT_AUTO = 0, PHG_LAYOUT_GATHER = 1, PHG_LAYOUT_LOCAL = 2, PHG_LAYOUT_BLOCK = 3,
-       PHG_LAYOUT_MFMA = 4 };
+       PHG_LAYOUT_MFMA = 4, PHG_LAYOUT_STREAM = 5 };
 int  phg_set_layout(phg_handle* h, int32_t policy);
 /* host-only dry run of the lane-local planner (no device needed): out8 = {local variant or -1,
  * lanes per scenario, columns per lane, rows per lane, coupling-row slots, coupling rows used,
@@ -175,7 +176,8 @@ int  phg_get_i32(phg_handle* h, int32_t field, int32_t* host_out);
 int  phg_mfma_info(phg_handle* h, int32_t* out4);
 int  phg_info(phg_handle* h, int32_t* out8);   /* S, n, m, nnz, N, N_tot, kernel variant
                                                   (>= 100: lane-local, >= 200: workgroup,
-                                                  >= 300: shared-matrix MFMA),
+                                                  >= 300: shared-matrix MFMA, 400 + K:
+                                                  streaming, K workgroups per scenario),
                                                   lanes (threads) per scenario             */
 
 /* Solve every scenario's subproblem (solve_loop):

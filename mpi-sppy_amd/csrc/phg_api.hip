@@ -33,6 +33,8 @@ int pdhg_block_num_variants();
 void pdhg_block_variant_shape(int v, int* out5);
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad);
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
+hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream);
+hipError_t pdhg_stream_capacity(int* out);
 int pdhg_mfma_num_variants();
 void pdhg_mfma_variant_shape(int v, int* out2);
 hipError_t pdhg_mfma_launch(int v, const PdhgArgs& a, hipStream_t stream);
@@ -82,6 +84,9 @@ struct phg_handle {
     int local_variant = -1;    // lane-local kernel variant (pdhg_local.hip); preferred when >= 0
     int block_variant = -1;    // workgroup-per-scenario kernel variant (pdhg_block.hip)
     int mfma_variant = -1;     // shared-matrix MFMA kernel variant (pdhg_mfma.hip)
+    bool stream_layout = false;   // multi-workgroup streaming kernel (pdhg_stream.hip)
+    StreamLayout st{};
+    std::vector<int> stream_cperm;   // CSC entry -> CSR position (values gathered after prep)
     int mshape[2] = {0, 0};
     MfmaLayout mf{};
     int bshape[5] = {0};
@@ -320,7 +325,7 @@ int phg_set_smoothing(phg_handle* h, int32_t on) {
 int phg_set_layout(phg_handle* h, int32_t policy) {
     if (!h) return fail("null handle");
     if (h->loaded) return fail("phg_set_layout: must be called before phg_load_batch");
-    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_MFMA) return fail("phg_set_layout: bad policy");
+    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_STREAM) return fail("phg_set_layout: bad policy");
     h->layout_policy = policy;
     return 0;
 }
@@ -922,6 +927,77 @@ static int build_mfma_fragments(phg_handle* h, const phg_batch* b) {
     return 0;
 }
 
+// Streaming layout (pdhg_stream.hip).  K workgroups per scenario so that S K workgroups fill the
+// chip (at most what can be resident -- one 1024-thread workgroup per CU; the K of a scenario must
+// be co-resident for their barriers, which the cooperative launch enforces -- and at most 16); rows
+// and columns are split into K contiguous ranges of about equal nonzeros.
+static int build_stream_layout(phg_handle* h, const phg_batch* b, const std::vector<int>& colptr,
+                               const std::vector<int>& csc_row, const std::vector<int>& csc_p) {
+    int cap = 0;
+    CK(pdhg_stream_capacity(&cap));
+    int K = 1;
+    if (const char* ev = std::getenv("PHG_STREAM_K")) K = std::max(1, std::atoi(ev));
+    else K = std::max(1, std::min(16, cap / std::max(1, b->S)));
+    if (K > 1 && (long)K * b->S > cap) K = std::max(1, cap / b->S);
+    const int n = b->n, m = b->m, nnz = b->nnz;
+    auto split = [&](const int* ptr, int cnt, std::vector<int>& first) {
+        first.assign(K + 1, cnt);
+        first[0] = 0;
+        int q = 1;
+        for (int i = 0; i < cnt && q < K; ++i)
+            if ((long)ptr[i] * K >= (long)q * ptr[cnt]) first[q++] = i;
+        for (; q < K; ++q) first[q] = cnt;
+        for (int k = 1; k <= K; ++k) first[k] = std::max(first[k], first[k - 1]);
+    };
+    std::vector<int> rf, cf;
+    split(b->rowptr, m, rf);
+    split(colptr.data(), n, cf);
+    StreamLayout& L = h->st;
+    L.K = K;
+    int* p;
+    if (dput(h, &p, rf.data(), rf.size())) return -1; L.row_first = p;
+    if (dput(h, &p, cf.data(), cf.size())) return -1; L.col_first = p;
+    if (dput(h, &p, b->rowptr, m + 1)) return -1; L.rowptr = p;
+    if (dput(h, &p, b->colidx, nnz)) return -1; L.colidx = p;
+    if (dput(h, &p, colptr.data(), n + 1)) return -1; L.colptr = p;
+    if (dput(h, &p, csc_row.data(), nnz)) return -1; L.rowidx = p;
+    h->stream_cperm = csc_p;
+    const size_t Sn = (size_t)b->S * n, Sm = (size_t)b->S * m;
+    double* d;
+    if (dalloc(h, &d, Sn)) return -1; L.cs = d;
+    if (dalloc(h, &d, Sn)) return -1; L.qs = d;
+    if (dalloc(h, &d, Sn)) return -1; L.lo = d;
+    if (dalloc(h, &d, Sn)) return -1; L.hi = d;
+    if (dalloc(h, &d, Sn)) return -1; L.xsum = d;
+    if (dalloc(h, &d, Sn)) return -1; L.aty = d;
+    if (dalloc(h, &d, Sn)) return -1; L.xr = d;
+    if (dalloc(h, &d, Sm)) return -1; L.ysum = d;
+    if (dalloc(h, &d, Sm)) return -1; L.axo = d;
+    if (dalloc(h, &d, Sm)) return -1; L.yr = d;
+    if (dalloc(h, &d, (size_t)b->S * K * 16)) return -1; L.part = d;
+    unsigned* u;
+    if (dalloc(h, &u, 2 * (size_t)b->S)) return -1; L.bar = u;
+    int* e;
+    if (dalloc(h, &e, 1)) return -1; L.err = e;
+    h->stream_layout = true;
+    return 0;
+}
+
+// scaled values in CSR order are the handle's own array; the CSC copy is gathered after prep
+static int build_stream_values(phg_handle* h) {
+    StreamLayout& L = h->st;
+    const int Sv = h->vals_shared ? 1 : h->S;
+    int* perm;
+    double* cv;
+    if (dput(h, &perm, h->stream_cperm.data(), h->stream_cperm.size())) return -1;
+    if (dalloc(h, &cv, (size_t)Sv * h->nnz)) return -1;
+    CK(piece_gather_launch(h->vals, h->nnz, perm, h->nnz, Sv, cv, h->stream));
+    L.rvals = h->vals;
+    L.cvals = cv;
+    L.vstride = h->vals_shared ? 0 : h->nnz;
+    return 0;
+}
+
 // ----------------------------------------------------------------------------- presolve
 // Singleton rows (PDLP-style presolve): a row  lo <= a x_j <= hi  with ONE nonzero, on a column
 // that is not a nonant, is the column bound  lo/a <= x_j <= hi/a  (swapped for a < 0).  The LP is
@@ -1148,9 +1224,13 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
         gr = build_layout(h, b, colptr, csc_row, csc_p);
         if (gr < 0 || (gr > 0 && pol == PHG_LAYOUT_GATHER)) return -1;
     }
-    if (h->mfma_variant < 0 && lr != 0 && gr != 0) {
+    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && pol != PHG_LAYOUT_STREAM) {
         br = build_block_layout(h, b, colptr, csc_row, csc_p);
-        if (br != 0) return -1;
+        if (br < 0 || (br > 0 && pol == PHG_LAYOUT_BLOCK)) return -1;
+        h->variant = -1;
+    }
+    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && br != 0) {
+        if (build_stream_layout(h, b, colptr, csc_row, csc_p)) return -1;
         h->variant = -1;
     }
     if (h->mfma_variant >= 0) h->variant = -1;
@@ -1236,6 +1316,7 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     CK(prep_launch(pa, h->stream));
     if (h->block_variant >= 0 && build_block_values(h)) return -1;
     if (h->mfma_variant >= 0 && build_mfma_fragments(h, b)) return -1;
+    if (h->stream_layout && build_stream_values(h)) return -1;
     CK(hipStreamSynchronize(h->stream));
     h->loaded = true;
     return 0;
@@ -1254,7 +1335,8 @@ int phg_mfma_info(phg_handle* h, int32_t* o) {
 int phg_info(phg_handle* h, int32_t* o) {
     if (!h || !h->loaded) return fail("phg_info: no batch loaded");
     o[0] = h->S; o[1] = h->n; o[2] = h->m_orig; o[3] = h->nnz; o[4] = h->N; o[5] = h->N_tot;
-    if (h->mfma_variant >= 0) { o[6] = 300 + h->mfma_variant; o[7] = 4; }
+    if (h->stream_layout) { o[6] = 400 + h->st.K; o[7] = 256; }
+    else if (h->mfma_variant >= 0) { o[6] = 300 + h->mfma_variant; o[7] = 4; }
     else if (h->local_variant >= 0) { o[6] = 100 + h->local_variant; o[7] = h->lshape[0]; }
     else if (h->block_variant >= 0) { o[6] = 200 + h->block_variant; o[7] = h->bshape[0]; }
     else { o[6] = h->variant; o[7] = 64; }
@@ -1371,10 +1453,12 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.loc = h->loc;
     a.blk = h->blk;
     a.mf = h->mf;
+    a.st = h->st;
     a.gate = o->skip_if_conv_below > 0 ? h->gate : nullptr;
     a.gate_below = o->skip_if_conv_below;
     a.queue = h->persist ? h->queue : nullptr;
-    if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
+    if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));
+    else if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
     else if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));

@@ -68,12 +68,34 @@ struct MfmaLayout {
     unsigned long long nz_ax, nz_aty;
 };
 
+// Streaming layout (pdhg_stream.hip): K workgroups per scenario, each owning a row range and a
+// column range; the shared pattern in CSR and CSC, the scaled values in both orders, and the
+// per-scenario work arrays every PDHG iteration streams
+struct StreamLayout {
+    int K;
+    const int* row_first;   // [K+1]
+    const int* col_first;   // [K+1]
+    const int* rowptr;      // [m+1]
+    const int* colidx;      // [nnz]
+    const int* colptr;      // [n+1]
+    const int* rowidx;      // [nnz] CSC row indices
+    const double* rvals;    // [S or 1][nnz] scaled values, CSR order
+    const double* cvals;    // [S or 1][nnz] scaled values, CSC order
+    long vstride;           // nnz, or 0 when every scenario has the same matrix
+    double *cs, *qs, *lo, *hi, *xsum, *aty, *xr;   // [S*n]
+    double *ysum, *axo, *yr;                        // [S*m]
+    double* part;           // [S*K*16] per-workgroup partial sums
+    unsigned* bar;          // [2*S] barrier arrivals, workgroups done (0 between launches)
+    int* err;               // [1] a barrier wait ran past its bound
+};
+
 struct PdhgArgs {
     int S, n, m, nnz, N, n_pad;
     Layout lay;
     LocalLayout loc;
     BlockLayout blk;
     MfmaLayout mf;
+    StreamLayout st;
     // scenario data (scaled where noted)
     const double* vals;     // [S*nnz] scaled values
     const double* c;        // [S*n]   min-form objective, UNscaled

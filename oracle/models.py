@@ -305,3 +305,59 @@ def netdes(scenario_name, num_scens=None):
 
 def netdes_names(num_scens, start=0):
     return [f"Scenario{i}" for i in range(start, start + num_scens)]
+
+
+# ------------------------------------------------------------------------------------------------
+# uc: synthetic UC-shaped LP relaxation (the reference's examples/uc needs egret,
+# absent) -- restated independently of mpi-sppy_amd/examples/uc.py from the same formulas
+# ------------------------------------------------------------------------------------------------
+def uc(scenario_name, num_gens=85, num_periods=48, num_scens=None):
+    k = extract_num(scenario_name)
+    G, T = int(num_gens), int(num_periods)
+    rng = np.random.default_rng(1134)
+    pmax = rng.uniform(50.0, 400.0, G)
+    mc = rng.uniform(10.0, 60.0, G)
+    sc = rng.uniform(200.0, 2000.0, G)
+    u0 = (np.arange(G) % 2 == 0).astype(float)
+    tt = np.arange(T)
+    dbase = 0.6 * pmax.sum() * (0.8 + 0.2 * np.sin(2.0 * np.pi * tt / T))
+    srng = np.random.default_rng([1134, k])
+    dem = dbase * (1.0 + 0.05 * srng.standard_normal(T))
+    avail = np.where(srng.random((G, T)) < 0.05, 0.8, 1.0)
+    pmin, ramp, nl = 0.3 * pmax, 0.5 * pmax, 0.1 * mc * pmax
+    s = OScen(scenario_name)
+    idx = [(g, t) for g in range(G) for t in range(T)]
+    u = {gt: s.var(f"UnitOn[{gt}]", 0.0, 1.0, nl[gt[0]]) for gt in idx}
+    p = {gt: s.var(f"PowerGenerated[{gt}]", 0.0, INF, mc[gt[0]]) for gt in idx}
+    su = {gt: s.var(f"StartUp[{gt}]", 0.0, 1.0, sc[gt[0]]) for gt in idx}
+    sd = {gt: s.var(f"ShutDown[{gt}]", 0.0, 1.0, 0.0) for gt in idx}
+    r = {gt: s.var(f"Reserve[{gt}]", 0.0, INF, 0.0) for gt in idx}
+    for g, t in idx:
+        s.row({p[(g, t)]: 1.0, r[(g, t)]: 1.0, u[(g, t)]: -avail[g, t] * pmax[g]}, -INF, 0.0)
+    for g, t in idx:
+        s.row({p[(g, t)]: 1.0, u[(g, t)]: -pmin[g]}, 0.0, INF)
+    for g, t in idx:
+        co = {u[(g, t)]: 1.0, su[(g, t)]: -1.0, sd[(g, t)]: 1.0}
+        if t > 0:
+            co[u[(g, t - 1)]] = -1.0
+            s.row(co, 0.0, 0.0)
+        else:
+            s.row(co, u0[g], u0[g])
+    for g, t in idx:
+        if t > 0:
+            s.row({p[(g, t)]: 1.0, p[(g, t - 1)]: -1.0}, -INF, ramp[g])
+    for g, t in idx:
+        if t > 0:
+            s.row({p[(g, t - 1)]: 1.0, p[(g, t)]: -1.0}, -INF, ramp[g])
+    for t in range(T):
+        s.row({p[(g, t)]: 1.0 for g in range(G)}, dem[t], dem[t])
+    for t in range(T):
+        s.row({r[(g, t)]: 1.0 for g in range(G)}, 0.03 * dem[t], INF)
+    s.nodes = [dict(name="ROOT", cond_prob=1.0, stage=1, cols=[u[k2] for k2 in sorted(u)])]
+    if num_scens is not None:
+        s.prob = 1.0 / num_scens
+    return s
+
+
+def uc_names(num_scens, start=1):
+    return [f"Scenario{i}" for i in range(start, start + num_scens)]

@@ -13,7 +13,7 @@ if not torch.cuda.is_available():
     pytest.skip("needs a HIP device", allow_module_level=True)
 
 from mpisppy_amd import _lib  # noqa: E402
-from mpisppy_amd.examples import netdes, sslp  # noqa: E402
+from mpisppy_amd.examples import netdes, sslp, uc  # noqa: E402
 from mpisppy_amd.ph import PH  # noqa: E402
 from oracle import models as om  # noqa: E402
 from oracle import ph as oph  # noqa: E402
@@ -31,6 +31,10 @@ CASES = {
              lambda S: om.sslp_names(S), om.sslp, {}),
     "netdes": (lambda S: netdes.scenario_names_creator(S), netdes.scenario_creator, {"num_scens": 3},
                lambda S: om.netdes_names(S), om.netdes, {"num_scens": 3}),
+    # UC-shaped, a small instance of the same generator (6 units x 8 periods)
+    "uc_small": (lambda S: uc.scenario_names_creator(S), uc.scenario_creator,
+                 {"num_gens": 6, "num_periods": 8, "num_scens": 4},
+                 lambda S: om.uc_names(S), om.uc, {"num_gens": 6, "num_periods": 8, "num_scens": 4}),
 }
 
 
@@ -49,10 +53,13 @@ def test_iter0_lp_block_kernel(case, S):
     assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
 
 
-@pytest.mark.parametrize("case,S", [("sslp", 4), ("netdes", 3)])
-def test_prox_qp_block_kernel(case, S):
+@pytest.mark.parametrize("case,S,layout", [("sslp", 4, "auto"), ("netdes", 3, "auto"), ("sslp", 4, "stream"),
+                                           ("uc_small", 4, "stream")])
+def test_prox_qp_block_kernel(case, S, layout):
+    """layout "stream": the multi-workgroup streaming kernel (pdhg_stream.hip) with K > 1
+    workgroups per scenario (few scenarios: K = 16), its cross-workgroup barriers and sums."""
     pn, pc, pkw, on, oc, okw = CASES[case]
-    ph = PH(_opts(), pn(S), pc, scenario_creator_kwargs=pkw)
+    ph = PH(_opts(pdhg_layout=layout), pn(S), pc, scenario_creator_kwargs=pkw)
     ph.PH_Prep()
     ph.Iter0()
     o = oph.OraclePH(_opts(), on(S), oc, okw)
@@ -68,3 +75,28 @@ def test_prox_qp_block_kernel(case, S):
         xo = np.array([o.nonants(k) for k in range(S)])
         np.testing.assert_allclose(xg, xo, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(xo).max()))
         np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6)
+        assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+    if layout == "stream":
+        assert ph.engine.layout == "stream" and ph.engine.workgroups_per_scenario > 1
+
+
+@pytest.mark.parametrize("S", [2])
+def test_uc_fullsize_stream_vs_oracle(S):
+    """The UC-shaped LP at full size (n = 20 400, m = 20 326, N = 4 080) through the AUTO layout
+    (too large for a workgroup's LDS: the streaming kernel, K > 1 workgroups per scenario).  At this
+    size PDHG needs > 2e5 iterations for a 1e-9 relative KKT error, so the solve runs at
+    pdhg_eps = 1e-6 (the accuracy PDLP-class solvers default to): Iter0 LP objectives and dual
+    bounds against HiGHS at 1e-5 relative (LP optima may be non-unique: objectives only)."""
+    so = {"pdhg_eps": 1e-6}
+    ph = PH(_opts(iter0_solver_options=so, iterk_solver_options=so), uc.scenario_names_creator(S),
+            uc.scenario_creator, scenario_creator_kwargs={"num_scens": S})
+    ph.PH_Prep()
+    assert ph.engine.layout == "stream" and ph.engine.workgroups_per_scenario > 1
+    tb = ph.Iter0()
+    o = oph.OraclePH(_opts(), om.uc_names(S), om.uc, {"num_scens": S})
+    otb = o.Iter0()
+    assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+    assert (ph.engine.get(_lib.F_KKT) <= 1e-6).all()
+    assert abs(tb - otb) <= 1e-5 * abs(otb), (tb, otb)
+    np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-5)
+    np.testing.assert_allclose(ph.engine.get(_lib.F_BOUND), o.outer, rtol=1e-5)

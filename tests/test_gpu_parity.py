@@ -34,7 +34,7 @@ def _opts(**kw):
     return o
 
 
-LAYOUTS = ["gather", "local", "block"]
+LAYOUTS = ["gather", "local", "block", "stream"]
 
 
 def _farmer_ph(S, cm=1, virtual_nproc=None, layout="auto", **kw):

@@ -122,3 +122,24 @@ def test_hydro_synthetic_tree_bit_exact(fan):
     assert hydro.synthetic_fanouts(500) == (50, 150, 300) and hydro.synthetic_fanouts(2000) == (200, 600, 1200)
     p = [hydro.synthetic_scenario_creator(f"Scen{k}", fanouts=fan)._mpisppy_probability for k in range(1, S + 1)]
     assert abs(sum(p) - 1.0) < 1e-12
+
+
+@pytest.mark.parametrize("sn,kw", [("Scenario1", {}), ("Scenario7", {"num_scens": 64}),
+                                   ("Scenario3", {"num_gens": 6, "num_periods": 8, "num_scens": 4})])
+def test_uc_bit_exact(sn, kw):
+    """Synthetic UC-shaped LP: product generator == oracle restatement."""
+    from mpisppy_amd.examples import uc
+    mp = uc.scenario_creator(sn, **kw)
+    o = om.uc(sn, **kw)
+    _same(mp, o)
+    if "num_scens" in kw:
+        assert mp._mpisppy_probability == o.prob
+
+
+def test_uc_sizes():
+    from mpisppy_amd.examples import uc
+    m = uc.scenario_creator("Scenario2")
+    assert (m.n, m.m, len(m.pattern()[1]), len(m._mpisppy_node_list[0].nonant_vardata_list)) == (20400, 20326, 60775, 4080)
+    # scenarios differ in demand (right-hand side) and derates (matrix values)
+    a, b = m.arrays(), uc.scenario_creator("Scenario3").arrays()
+    assert not np.array_equal(a["row_lo"], b["row_lo"]) and not np.array_equal(a["vals"], b["vals"])
