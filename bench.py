@@ -41,7 +41,9 @@ def parse():
                     help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes, 2000 hydro, 64 uc")
     ap.add_argument("--cm", type=int, default=10)
     ap.add_argument("--rho", type=float, default=1.0)
-    ap.add_argument("--eps", type=float, default=1e-9)
+    ap.add_argument("--eps", type=float, default=None,
+                    help="PDHG relative KKT tolerance (default 1e-9; uc 1e-6: at n ~ 2e4 PDHG needs > 2e5 "
+                         "iterations per solve for 1e-9)")
     ap.add_argument("--conv-iters", type=int, default=20000, help="PH iteration cap for time-to-conv (0: skip)")
     ap.add_argument("--conv-time", type=float, default=120.0,
                     help="wall cap (s) for time-to-conv (PHBase time_limit; not set for farmer, whose "
@@ -51,7 +53,7 @@ def parse():
                          "case, i.e. farmer 10k = the BASELINE headline, sharded over the N GPUs: strong "
                          "scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0: skip)")
-    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local", "block", "mfma", "stream"],
+    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local", "block", "mfma", "stream", "border"],
                     help="PDHG data layout (include/phg.h: phg_set_layout)")
     ap.add_argument("--no-schedule", action="store_true", help="launch scenarios in index order")
     ap.add_argument("--check-every", type=int, default=32, help="PDHG restart/termination check interval")
@@ -178,6 +180,8 @@ def main():
     default_scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024, "hydro": 2000, "uc": 64}[args.case]
     if args.scen is None:
         args.scen = default_scen
+    if args.eps is None:
+        args.eps = 1e-6 if args.case == "uc" else 1e-9
     S = args.scen * world
     names, creator, ckw, nodenames, desc = _case_setup(args, S, farmer, hydro, netdes, sslp, uc)
     opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
@@ -347,7 +351,9 @@ def main():
                                 "block": "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)",
                                 "mfma": "pdhg_mfma_kernel (shared matrix, v_mfma_f64_16x16x4_f64, 16 scenarios per wave)",
                                 "stream": f"pdhg_stream_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
-                                          "iterates and values streamed)"}[eng.layout],
+                                          "range split, iterates and values streamed)",
+                                "border": f"pdhg_border_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
+                                          "bordered block-diagonal, slices in LDS, linking rows exchanged)"}[eng.layout],
                      "flops_per_pdhg_iter_per_scen": f_it,
                      "pdhg_iters_per_scen_per_step": round(pdhg_iters / args.steps / S_loc, 2),
                      "max_pdhg_iters": max_iters,

@@ -150,11 +150,14 @@ int  phg_sync(phg_handle* h);
  *            else the lane-local register layout (pdhg_local.hip) when the pattern splits into
  *            blocks that fit a lane plus <= a few coupling rows, else the wave LDS-gather layout
  *            (pdhg.hip, n, m <= 256), else the workgroup-per-scenario streaming layout
- *            (pdhg_block.hip, n, m up to 4096), else the multi-workgroup streaming layout
- *            (pdhg_stream.hip, any size: K workgroups per scenario, everything streamed)
- *   GATHER / LOCAL / BLOCK / MFMA / STREAM : that layout or fail (MFMA: shared matrix only)     */
+ *            (pdhg_block.hip, n, m up to 4096), else a multi-workgroup layout (K workgroups per
+ *            scenario): the bordered block-diagonal one (pdhg_border.hip: column blocks coupled by
+ *            <= 1024 linking rows, slices in LDS, one cross-workgroup exchange per iteration) when
+ *            the pattern has that structure, else the range-split one (pdhg_stream.hip, any size)
+ *   GATHER / LOCAL / BLOCK / MFMA / STREAM / BORDER : that layout or fail (MFMA: shared matrix
+ *            only; STREAM: the range-split kernel)                                             */
 enum { PHG_LAYOUT_AUTO = 0, PHG_LAYOUT_GATHER = 1, PHG_LAYOUT_LOCAL = 2, PHG_LAYOUT_BLOCK = 3,
-       PHG_LAYOUT_MFMA = 4, PHG_LAYOUT_STREAM = 5 };
+       PHG_LAYOUT_MFMA = 4, PHG_LAYOUT_STREAM = 5, PHG_LAYOUT_BORDER = 6 };
 int  phg_set_layout(phg_handle* h, int32_t policy);
 /* host-only dry run of the lane-local planner (no device needed): out8 = {local variant or -1,
  * lanes per scenario, columns per lane, rows per lane, coupling-row slots, coupling rows used,

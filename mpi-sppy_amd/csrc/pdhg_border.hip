@@ -1,0 +1,471 @@
+// pdhg_border.hip -- batched PDHG for scenario LPs / QPs too large for one workgroup whose
+// constraint matrix is bordered block-diagonal (block-angular): column blocks coupled only through
+// a few linking rows.  Unit commitment is the type (one block per generating unit,
+// demand and reserve rows coupling them); the host finds the blocks (phg_api.hip:
+// build_border_layout) and falls back to the range-split kernel (pdhg_stream.hip) when it finds
+// none.  Same algorithm, restart rule, termination test and outputs as the other PDHG kernels
+// (replaces SPOpt.solve_one, mpisppy/spopt.py:184-231, for every local scenario).  Mapping:
+//
+//   * a slot of K workgroups (one 1024-thread workgroup per CU) solves one scenario at a time,
+//     taking scenarios from a queue heaviest first; workgroup k owns a group of whole blocks -- its
+//     columns and every row whose columns it owns ("local rows") -- and keeps their CSR / CSC
+//     slices in LDS (values loaded per scenario);
+//   * the NL linking rows are replicated: every workgroup holds their y (thread l < NL, registers,
+//     and an LDS copy for A^T y); their A x is the one cross-workgroup step of a PDHG iteration --
+//     each workgroup publishes the partial sums over its columns (sc1 stores), ONE slot barrier,
+//     and every workgroup adds the K partials in workgroup order, so all hold the same bits and
+//     take the same decisions (a double-buffered exchange: no second barrier);
+//   * everything else (x, local y, A x, A^T y, running sums) is owned by one workgroup: plain
+//     loads and stores, ordered by workgroup barriers;
+//   * per-scenario sums (KKT norms, objectives, primal-weight movement) every check_every
+//     iterations through the same workgroup-partials pattern (linking rows counted by workgroup 0).
+//
+// Roofline: per PDHG iteration a workgroup moves its slice's vectors (x, y, sums, bounds: L2-
+// resident at these sizes), gathers from LDS, and exchanges NL doubles; the slot barrier sets the
+// floor (MI355X_MICROARCH.md: a few us per cross-CU barrier), so the time per iteration is
+// latency-bound and reported against HBM on the SURVEY 8(d)1 algorithmic bytes.
+#include "phg_internal.h"
+#include "wave_ops.h"
+#include "stream_sync.h"
+
+namespace phg {
+
+template <int NT>
+__global__ __launch_bounds__(NT) void pdhg_border_kernel(PdhgArgs a) {
+    if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
+    __shared__ double red[16 * (NT / 64)];
+    __shared__ int s_w;
+    extern __shared__ double dyn[];
+    const StreamLayout& L = a.st;
+    const BorderLayout& B = a.bd;
+    const int K = L.K;
+    const int slot = blockIdx.x / K, kw = blockIdx.x % K;
+    const int t = threadIdx.x;
+    const BorderGroup G = B.grp[kw];
+    const int NL = B.nlink;
+    const int nc = G.nc, nr = G.nr;
+    // ------------------------------------------------------------------ LDS slice (per launch)
+    double* lrv = dyn;                               // [nrz_max] local rows' values, CSR order
+    double* lkv = lrv + B.nrz_max;                   // [nlz_max] linking rows' values on owned columns
+    double* lcv = lkv + B.nlz_max;                   // [ncz_max] owned columns' values, CSC order
+    double* yl = lcv + B.ncz_max;                    // [NL] linking rows' y (current)
+    double* ylx = yl + NL;                           // [NL] linking rows' y running sums (checks)
+    int* lcol = reinterpret_cast<int*>(ylx + NL);    // [C_max] owned columns
+    int* lrow = lcol + B.C_max;                      // [R_max] local rows
+    int* lrp = lrow + B.R_max;                       // [R_max + 1]
+    int* lci = lrp + B.R_max + 1;                    // [nrz_max] column of each local-row entry
+    int* lkp = lci + B.nrz_max;                      // [NL + 1]
+    int* lkc = lkp + NL + 1;                         // [nlz_max] column of each linking-row entry
+    int* lcp = lkc + B.nlz_max;                      // [C_max + 1]
+    int* lri = lcp + B.C_max + 1;                    // [ncz_max] row: >= 0 local row, -(l + 1) linking row l
+    for (int q = t; q < nc; q += NT) lcol[q] = B.col_list[G.c0 + q];
+    for (int q = t; q < nr; q += NT) lrow[q] = B.row_list[G.r0 + q];
+    for (int q = t; q <= nr; q += NT) lrp[q] = B.rptr[G.rp0 + q];
+    for (int q = t; q < G.nrz; q += NT) lci[q] = B.rcol[G.rz0 + q];
+    for (int q = t; q <= NL; q += NT) lkp[q] = B.lptr[G.lp0 + q];
+    for (int q = t; q < G.nlz; q += NT) lkc[q] = B.lcol[G.lz0 + q];
+    for (int q = t; q <= nc; q += NT) lcp[q] = B.cptr[G.cp0 + q];
+    for (int q = t; q < G.ncz; q += NT) lri[q] = B.crow[G.cz0 + q];
+
+    double* part = L.part + (long)slot * K * 16;
+    unsigned* bar = L.ctrl + kCtrlBar + 2 * slot;
+    unsigned* mbox = L.ctrl + kCtrlBar + 2 * L.slots + slot;
+    unsigned nbar = 0, xc = 0;
+    bool alive = true;
+    auto barrier = [&]() {
+        if (K == 1) { __syncthreads(); return; }
+        ++nbar;
+        if (!scen_barrier(bar, nbar * (unsigned)K, L.err)) alive = false;
+    };
+    auto scen_sum = [&](auto& v) {
+        constexpr int V = sizeof(v) / sizeof(double);
+        wg_sum<NT, V>(v, red);
+        if (K == 1) return;
+        if (t < V) put(&part[kw * 16 + t], v[t]);
+        barrier();
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            double acc = get(&part[u]);
+            for (int q = 1; q < K; ++q) acc += get(&part[q * 16 + u]);
+            v[u] = acc;
+        }
+        barrier();   // the partials are reused by the next scen_sum
+    };
+    // linking-row partials (thread l < NL) -> the K-workgroup sum, same bits everywhere
+    auto exchange = [&](double v) {
+        if (K == 1) return v;
+        double* buf = B.plink + ((long)slot * 2 + (xc & 1u)) * K * NL;
+        ++xc;
+        if (t < NL) put(&buf[kw * NL + t], v);
+        barrier();
+        double acc = 0.0;
+        if (t < NL) {
+            acc = get(&buf[t]);
+            for (int q = 1; q < K; ++q) acc += get(&buf[q * NL + t]);
+        }
+        return acc;
+    };
+    bool vals_loaded = false;
+
+    while (true) {
+    // ------------------------------------------------------------------ next scenario of the slot
+    if (kw == 0 && t == 0) {
+        const unsigned w = __hip_atomic_fetch_add(L.ctrl + kCtrlHead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_w = (int)w;
+        if (K > 1) __hip_atomic_store(mbox, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (K > 1) {
+        barrier();
+        if (kw != 0 && t == 0) s_w = (int)__hip_atomic_load(mbox, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int wi = s_w;
+    if (!alive || wi >= a.S) break;
+    const int s = a.order ? a.order[wi] : wi;
+    const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
+    if (L.vstride != 0 || !vals_loaded) {
+        const double* rv = L.rvals + (long)s * L.vstride;
+        for (int q = t; q < G.nrz; q += NT) lrv[q] = rv[B.rperm[G.rz0 + q]];
+        for (int q = t; q < G.nlz; q += NT) lkv[q] = rv[B.lperm[G.lz0 + q]];
+        for (int q = t; q < G.ncz; q += NT) lcv[q] = rv[B.cperm[G.cz0 + q]];
+        vals_loaded = true;
+    }
+    double* X = a.xs + sn;            // owned columns only: plain accesses inside the workgroup
+    double* Y = a.ys + sm;
+    double* XS = L.xsum + sn;
+    double* YS = L.ysum + sm;
+    double* CS = L.cs + sn;
+    double* QS = L.qs + sn;
+    double* LO = L.lo + sn;
+    double* HI = L.hi + sn;
+    double* ATY = L.aty + sn;
+    double* XR = L.xr + sn;
+    double* AXO = L.axo + sm;
+    double* YR = L.yr + sm;
+    auto rowb = [&](int i, double& lo, double& hi) { row_bounds(a, i, sm + i, lo, hi); };
+    auto ax_loc = [&](const double* xv, int q) {
+        double acc = 0.0;
+        for (int p = lrp[q]; p < lrp[q + 1]; ++p) acc = fma(lrv[p], xv[lci[p]], acc);
+        return acc;
+    };
+    auto ax_link = [&](const double* xv) {
+        double acc = 0.0;
+        if (t < NL)
+            for (int p = lkp[t]; p < lkp[t + 1]; ++p) acc = fma(lkv[p], xv[lkc[p]], acc);
+        return acc;
+    };
+    auto aty_col = [&](const double* yv, const double* ylv, int q) {
+        double acc = 0.0;
+        for (int p = lcp[q]; p < lcp[q + 1]; ++p) {
+            const int r = lri[p];
+            acc = fma(lcv[p], r >= 0 ? yv[r] : ylv[-r - 1], acc);
+        }
+        return acc;
+    };
+
+    // ------------------------------------------------------------------ prologue
+    double c2 = 0.0, prox_const = 0.0, cs2 = 0.0, b2 = 0.0;
+    for (int q = t; q < nc; q += NT) {
+        const int j = lcol[q];
+        const long b = sn + j;
+        const double d = a.dc[b];
+        double cc = a.c[b], qq = 0.0;
+        double lo_ = a.cl[b], hi_ = a.cu[b];
+        const int kk = a.lay.col_nonant[j];
+        if (kk >= 0) {
+            ph_terms(a, sN + kk, cc, qq, prox_const);
+            if (a.fix_nonants) fixed_box(a, sN + kk, d, lo_, hi_);
+        }
+        c2 += cc * cc;
+        const double csj = cc * d;
+        cs2 += csj * csj;
+        CS[j] = csj;
+        QS[j] = qq * d * d;
+        LO[j] = lo_;
+        HI[j] = hi_;
+        const double x0 = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
+        X[j] = x0;
+        XR[j] = x0;
+        XS[j] = 0.0;
+    }
+    for (int q = t; q < nr; q += NT) {
+        const int i = lrow[q];
+        double lo_, hi_;
+        rowb(i, lo_, hi_);
+        double yy = (a.warm & 1) ? a.ys_in[sm + i] : 0.0;
+        if (!fin(lo_)) yy = fmin(yy, 0.0); else b2 += lo_ * lo_;
+        if (!fin(hi_)) yy = fmax(yy, 0.0); else b2 += hi_ * hi_;
+        Y[i] = yy;
+        YR[i] = yy;
+        YS[i] = 0.0;
+    }
+    // linking row t: replicated state in registers of thread t
+    double l_lo = 0.0, l_hi = 0.0, l_y = 0.0, l_ys = 0.0, l_yr = 0.0, l_ax = 0.0, l_dr = 1.0;
+    int l_i = 0;
+    if (t < NL) {
+        l_i = B.link_rows[t];
+        rowb(l_i, l_lo, l_hi);
+        l_dr = a.dr[sm + l_i];
+        double yy = (a.warm & 1) ? a.ys_in[sm + l_i] : 0.0;
+        if (!fin(l_lo)) yy = fmin(yy, 0.0); else if (kw == 0) b2 += l_lo * l_lo;
+        if (!fin(l_hi)) yy = fmax(yy, 0.0); else if (kw == 0) b2 += l_hi * l_hi;
+        l_y = l_yr = yy;
+        yl[t] = yy;
+    }
+    double omega, cnorm;
+    {
+        double rr[4] = {c2, prox_const, cs2, b2};
+        scen_sum(rr);   // (its workgroup barriers also order the prologue's stores)
+        cnorm = sqrt(rr[0]);
+        prox_const = rr[1];
+        const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
+        omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
+        if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
+        else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);
+    }
+    const double bnorm = a.bnorm[s], eta = a.eta[s];
+    double tau = eta / omega, sig = eta * omega;
+    auto products = [&]() {   // A x and A^T y at the current point (after a workgroup barrier)
+        for (int q = t; q < nr; q += NT) AXO[lrow[q]] = ax_loc(X, q);
+        l_ax = exchange(ax_link(X));
+        for (int q = t; q < nc; q += NT) ATY[lcol[q]] = aty_col(Y, yl, q);
+    };
+    products();
+
+    // KKT pieces of the current iterate (inv = 0) or of the average (inv = 1 / cnt), see
+    // pdhg_stream.hip: [0] ||pr||^2 scaled, [1] ||dres||^2 scaled, [2] ||pr||^2, [3] ||dres||^2
+    // unscaled, [4] pobj, [5] dobj; linking rows counted by workgroup 0
+    auto kkt_part = [&](bool avg, double inv, double l_axs, double* o) {
+        double v[6] = {0, 0, 0, 0, 0, 0};
+        auto row_terms = [&](double axx, double yy, double lo_, double hi_, double dr) {
+            const double pr = axx - clampd(axx, lo_, hi_);
+            v[0] += pr * pr;
+            const double pu = pr / dr;
+            v[2] += pu * pu;
+            if (fin(lo_)) v[5] += lo_ * fmax(yy, 0.0);
+            if (fin(hi_)) v[5] += hi_ * fmin(yy, 0.0);
+        };
+        for (int q = t; q < nr; q += NT) {
+            const int i = lrow[q];
+            double lo_, hi_;
+            rowb(i, lo_, hi_);
+            row_terms(avg ? ax_loc(XS, q) * inv : AXO[i], avg ? YS[i] * inv : Y[i], lo_, hi_, a.dr[sm + i]);
+        }
+        if (kw == 0 && t < NL) row_terms(avg ? l_axs * inv : l_ax, avg ? l_ys * inv : l_y, l_lo, l_hi, l_dr);
+        for (int q = t; q < nc; q += NT) {
+            const int j = lcol[q];
+            const double xx = avg ? XS[j] * inv : X[j];
+            const double at = avg ? aty_col(YS, ylx, q) * inv : ATY[j];
+            const double ck = CS[j], qk = QS[j], lo_ = LO[j], hi_ = HI[j];
+            const double rc_ = ck + qk * xx - at;
+            double dres = 0.0;
+            if (!fin(lo_) && rc_ > 0.0) dres += rc_;
+            if (!fin(hi_) && rc_ < 0.0) dres += rc_;
+            v[1] += dres * dres;
+            const double du = dres / a.dc[sn + j];
+            v[3] += du * du;
+            const double hq = 0.5 * qk * xx * xx;
+            v[4] += ck * xx + hq;
+            if (fin(lo_)) v[5] += lo_ * fmax(rc_, 0.0);
+            if (fin(hi_)) v[5] += hi_ * fmin(rc_, 0.0);
+            v[5] -= hq;
+        }
+#pragma unroll
+        for (int u = 0; u < 6; ++u) o[u] = v[u];
+    };
+    auto rel_of = [&](const double* o) {
+        const double p = sqrt(o[2]) / (1.0 + bnorm);
+        const double d = sqrt(o[3]) / (1.0 + cnorm);
+        const double g = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
+        return fmax(fmax(p, d), g);
+    };
+    auto wkkt_of = [&](const double* o, double w) {
+        const double g = o[4] - o[5];
+        return sqrt(w * w * o[0] + o[1] / (w * w) + g * g);
+    };
+    double kkt_restart, kkt_prev = INFINITY;
+    {
+        double o[6];
+        kkt_part(false, 0.0, 0.0, o);
+        scen_sum(o);
+        kkt_restart = wkkt_of(o, omega);
+    }
+    int it = 0, since = 0, cnt = 0, st = 1;
+    double rel_final = INFINITY, pobj = 0.0, dobj = 0.0;
+    bool use_avg_final = false;
+    const int chk = a.check_every;
+
+    while (alive) {
+        for (int kk = 0; kk < chk && alive; ++kk) {
+            for (int q = t; q < nc; q += NT) {
+                const int j = lcol[q];
+                const double ip = 1.0 / (1.0 + tau * QS[j]);
+                const double xn = clampd(fma(tau, ATY[j] - CS[j], X[j]) * ip, LO[j], HI[j]);
+                X[j] = xn;
+                XS[j] += xn;
+            }
+            __syncthreads();
+            // dual step: A (2 x+ - x) = 2 A x+ - A x
+            for (int q = t; q < nr; q += NT) {
+                const int i = lrow[q];
+                double lo_, hi_;
+                rowb(i, lo_, hi_);
+                const double axn = ax_loc(X, q);
+                const double g = Y[i] - sig * (2.0 * axn - AXO[i]);
+                const double yn = fmax(fma(sig, lo_, g), 0.0) + fmin(fma(sig, hi_, g), 0.0);
+                AXO[i] = axn;
+                Y[i] = yn;
+                YS[i] += yn;
+            }
+            const double axn_l = exchange(ax_link(X));   // the iteration's one slot barrier
+            if (t < NL) {
+                const double g = l_y - sig * (2.0 * axn_l - l_ax);
+                l_y = fmax(fma(sig, l_lo, g), 0.0) + fmin(fma(sig, l_hi, g), 0.0);
+                l_ax = axn_l;
+                l_ys += l_y;
+                yl[t] = l_y;
+            }
+            __syncthreads();
+            for (int q = t; q < nc; q += NT) ATY[lcol[q]] = aty_col(Y, yl, q);
+        }
+        if (!alive) break;
+        it += chk;
+        since += chk;
+        cnt += chk;
+
+        const double inv = 1.0 / (double)cnt;
+        const double l_axs = exchange(ax_link(XS));   // A x of the linking rows at the average
+        if (t < NL) ylx[t] = l_ys;
+        __syncthreads();
+        double oc[6], oa[6];
+        kkt_part(false, 0.0, 0.0, oc);
+        kkt_part(true, inv, l_axs, oa);
+        {
+            double both[12];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) { both[u] = oc[u]; both[6 + u] = oa[u]; }
+            scen_sum(both);
+#pragma unroll
+            for (int u = 0; u < 6; ++u) { oc[u] = both[u]; oa[u] = both[6 + u]; }
+        }
+        const double rel_cur = rel_of(oc), rel_avg = rel_of(oa);
+        const bool nan = !(rel_cur == rel_cur);
+        if (nan || rel_cur <= a.eps || rel_avg <= a.eps || it >= a.max_iter) {
+            use_avg_final = !nan && rel_avg < rel_cur;
+            rel_final = use_avg_final ? rel_avg : rel_cur;
+            pobj = use_avg_final ? oa[4] : oc[4];
+            dobj = use_avg_final ? oa[5] : oc[5];
+            st = nan ? 2 : ((rel_cur <= a.eps || rel_avg <= a.eps) ? 0 : 1);
+            break;
+        }
+        const double k_cur = wkkt_of(oc, omega), k_avg = wkkt_of(oa, omega);
+        const bool use_avg = k_avg < k_cur;
+        const double cand = use_avg ? k_avg : k_cur;
+        const bool restart = (cand <= a.beta_suf * kkt_restart) ||
+                             (cand <= a.beta_nec * kkt_restart && cand > kkt_prev) ||
+                             ((double)since >= a.beta_art * (double)it);
+        kkt_prev = cand;
+        if (restart) {
+            double mv[2] = {0.0, 0.0};
+            for (int q = t; q < nc; q += NT) {
+                const int j = lcol[q];
+                const double xv = use_avg ? XS[j] * inv : X[j];
+                const double d = xv - XR[j];
+                mv[0] += d * d;
+                XR[j] = xv;
+                X[j] = xv;
+                XS[j] = 0.0;
+            }
+            for (int q = t; q < nr; q += NT) {
+                const int i = lrow[q];
+                const double yv = use_avg ? YS[i] * inv : Y[i];
+                const double d = yv - YR[i];
+                mv[1] += d * d;
+                YR[i] = yv;
+                Y[i] = yv;
+                YS[i] = 0.0;
+            }
+            if (t < NL) {
+                const double yv = use_avg ? l_ys * inv : l_y;
+                const double d = yv - l_yr;
+                if (kw == 0) mv[1] += d * d;
+                l_yr = l_y = yv;
+                l_ys = 0.0;
+                yl[t] = yv;
+            }
+            scen_sum(mv);
+            omega = primal_weight(omega, mv[0], mv[1], a.theta);
+            tau = eta / omega;
+            sig = eta * omega;
+            cnt = 0;
+            since = 0;
+            kkt_restart = cand;
+            kkt_prev = INFINITY;
+            if (use_avg) products();   // exact products at the new point
+        }
+    }
+    if (!alive) { st = 2; rel_final = NAN; }
+
+    // ------------------------------------------------------------------ outputs
+    const double inv = cnt > 0 ? 1.0 / (double)cnt : 0.0;
+    for (int q = t; q < nc; q += NT) {
+        const int j = lcol[q];
+        const long b = sn + j;
+        const double xv = use_avg_final ? XS[j] * inv : X[j];
+        X[j] = xv;
+        const double xu = xv * a.dc[b];
+        if (a.x_out) a.x_out[b] = xu;
+        const int kk = a.lay.col_nonant[j];
+        if (kk >= 0) a.xN[sN + kk] = xu;
+    }
+    for (int q = t; q < nr; q += NT) {
+        const int i = lrow[q];
+        const long b = sm + i;
+        const double yv = use_avg_final ? YS[i] * inv : Y[i];
+        Y[i] = yv;
+        if (a.y_out) a.y_out[b] = yv * a.dr[b];
+    }
+    if (kw == 0 && t < NL) {
+        const long b = sm + l_i;
+        const double yv = use_avg_final ? l_ys * inv : l_y;
+        Y[l_i] = yv;
+        if (a.y_out) a.y_out[b] = yv * a.dr[b];
+    }
+    if (kw == 0 && t == 0) {
+        const double offs = a.obj_off[s] + (a.prox_on ? prox_const : 0.0);
+        a.omega[s] = omega;
+        a.obj[s] = a.sense * (pobj + offs);
+        a.bound[s] = a.sense * (dobj + offs);
+        a.kkt[s] = rel_final;
+        a.iters[s] = it;
+        a.iters_acc[s] += it;
+        a.status[s] = st;
+    }
+    if (!alive) break;
+    __syncthreads();   // the LDS values / linking copies are rewritten by the next scenario
+    }   // scenario queue
+}
+
+// ----------------------------------------------------------------------------- dispatch
+constexpr int kBorderNT = 1024;
+
+size_t pdhg_border_lds_bytes(const BorderLayout& B) {
+    return (size_t)(B.nrz_max + B.nlz_max + B.ncz_max + 2 * B.nlink) * sizeof(double) +
+           (size_t)(B.C_max + B.R_max + B.R_max + 1 + B.nrz_max + B.nlink + 1 + B.nlz_max + B.C_max + 1 + B.ncz_max) *
+               sizeof(int);
+}
+
+hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream) {
+    const StreamLayout& L = a.st;
+    hipError_t e = hipMemsetAsync(L.ctrl, 0, (size_t)(kCtrlBar + 3 * L.slots) * sizeof(unsigned), stream);
+    if (e != hipSuccess) return e;
+    const dim3 grid((unsigned)L.slots * (unsigned)L.K), block(kBorderNT);
+    const size_t lds = pdhg_border_lds_bytes(a.bd);
+    PdhgArgs copy = a;
+    void* args[] = {&copy};
+    const void* fn = (const void*)pdhg_border_kernel<kBorderNT>;
+    if (L.K == 1) return hipLaunchKernel(fn, grid, block, args, lds, stream);
+    return hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)lds, stream);
+}
+
+}  // namespace phg

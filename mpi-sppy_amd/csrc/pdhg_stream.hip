@@ -27,90 +27,40 @@
 //     over-subscribing).
 #include "phg_internal.h"
 #include "wave_ops.h"
+#include "stream_sync.h"
 
 namespace phg {
 
-// write-through (sc1) store and L1-bypassing (sc1) load of the values other workgroups read
-__device__ __forceinline__ void put(double* p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double get(const double* p) {
-    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// barrier of the K workgroups of one scenario: cnt[0] counts arrivals (monotonic within the
-// launch; re-armed by the last workgroup out, see the epilogue); target = (barrier number) * K
-__device__ __forceinline__ bool scen_barrier(unsigned* cnt, unsigned target, int* err) {
-    __shared__ int s_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 23)) {
-                ok = 0;
-                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        s_ok = ok;
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
-
-// workgroup sum of V values (V <= 16), same bits in every thread; fixed order
-template <int NT, int V>
-__device__ __forceinline__ void wg_sum(double (&v)[V], double* red) {
-    constexpr int NW = NT / 64;
-    gsum_many<64, V>(v);
-    const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0)
-#pragma unroll
-        for (int k = 0; k < V; ++k) red[k * NW + w] = v[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
-        double t = red[k * NW];
-#pragma unroll 1
-        for (int u = 1; u < NW; ++u) t += red[k * NW + u];
-        v[k] = t;
-    }
-    __syncthreads();
-}
-
-template <int NT>
+template <int NT, bool RES>
 __global__ __launch_bounds__(NT) void pdhg_stream_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     __shared__ double red[16 * (NT / 64)];
+    __shared__ int s_w;
+    extern __shared__ double dyn[];
     const StreamLayout& L = a.st;
     const int K = L.K;
-    const int wi = blockIdx.x / K, kw = blockIdx.x % K;
-    const int s = a.order ? a.order[wi] : wi;
+    const int slot = blockIdx.x / K, kw = blockIdx.x % K;
     const int t = threadIdx.x;
     const int r0 = L.row_first[kw], r1 = L.row_first[kw + 1];
     const int c0 = L.col_first[kw], c1 = L.col_first[kw + 1];
-    const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
-    const double* rv = L.rvals + (long)s * L.vstride;
-    const double* cv = L.cvals + (long)s * L.vstride;
-    double* X = a.xs + sn;            // current x (published), the solve's output copy
-    double* Y = a.ys + sm;
-    double* XS = L.xsum + sn;         // running sums since the last restart (published)
-    double* YS = L.ysum + sm;
-    double* CS = L.cs + sn;           // scaled cost with the PH terms
-    double* QS = L.qs + sn;           // scaled prox diagonal
-    double* LO = L.lo + sn;           // scaled column bounds (fixed nonants applied)
-    double* HI = L.hi + sn;
-    double* ATY = L.aty + sn;         // A^T y of the current y, owned columns
-    double* XR = L.xr + sn;           // restart point
-    double* AXO = L.axo + sm;         // A x of the current x, owned rows
-    double* YR = L.yr + sm;
-    double* part = L.part + (long)wi * K * 16;
-    unsigned* bar = L.bar + 2 * (long)wi;
+    const int p0 = L.rowptr[r0], q0 = L.colptr[c0];      // first nonzero of the owned rows / columns
+    const int nr = L.rowptr[r1] - p0, nc = L.colptr[c1] - q0;
+    // resident slice (RES): the owned rows' CSR and the owned columns' CSC, values per scenario
+    double* lrv = dyn;
+    double* lcv = lrv + L.nr_max;
+    int* lrp = reinterpret_cast<int*>(lcv + L.nc_max);
+    int* lci = lrp + L.R_max + 1;
+    int* lcp = lci + L.nr_max;
+    int* lri = lcp + L.C_max + 1;
+    if (RES) {
+        for (int i = t; i <= r1 - r0; i += NT) lrp[i] = L.rowptr[r0 + i] - p0;
+        for (int q = t; q < nr; q += NT) lci[q] = L.colidx[p0 + q];
+        for (int j = t; j <= c1 - c0; j += NT) lcp[j] = L.colptr[c0 + j] - q0;
+        for (int q = t; q < nc; q += NT) lri[q] = L.rowidx[q0 + q];
+    }
+    double* part = L.part + (long)slot * K * 16;
+    unsigned* bar = L.ctrl + kCtrlBar + 2 * slot;
+    unsigned* mbox = L.ctrl + kCtrlBar + 2 * L.slots + slot;
     unsigned nbar = 0;
     bool alive = true;
     auto barrier = [&]() {
@@ -133,6 +83,45 @@ __global__ __launch_bounds__(NT) void pdhg_stream_kernel(PdhgArgs a) {
         }
         barrier();   // the partials are reused by the next scen_sum
     };
+    bool vals_loaded = false;
+
+    // the slot's K workgroups take scenarios from one queue, heaviest first (a.order), until it is
+    // empty: workgroup 0 dequeues and publishes the index in the slot's mailbox
+    while (true) {
+    if (kw == 0 && t == 0) {
+        const unsigned w = __hip_atomic_fetch_add(L.ctrl + kCtrlHead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_w = (int)w;
+        if (K > 1) __hip_atomic_store(mbox, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (K > 1) {
+        barrier();   // the mailbox is published (its next write follows this scenario's barriers)
+        if (kw != 0 && t == 0) s_w = (int)__hip_atomic_load(mbox, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int wi = s_w;
+    if (!alive || wi >= a.S) break;
+    const int s = a.order ? a.order[wi] : wi;
+    const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
+    const double* rv = L.rvals + (long)s * L.vstride;
+    const double* cv = L.cvals + (long)s * L.vstride;
+    if (RES && (L.vstride != 0 || !vals_loaded)) {
+        for (int q = t; q < nr; q += NT) lrv[q] = rv[p0 + q];
+        for (int q = t; q < nc; q += NT) lcv[q] = cv[q0 + q];
+        vals_loaded = true;
+    }
+    __syncthreads();
+    double* X = a.xs + sn;            // current x (published), the solve's output copy
+    double* Y = a.ys + sm;
+    double* XS = L.xsum + sn;         // running sums since the last restart (published)
+    double* YS = L.ysum + sm;
+    double* CS = L.cs + sn;           // scaled cost with the PH terms
+    double* QS = L.qs + sn;           // scaled prox diagonal
+    double* LO = L.lo + sn;           // scaled column bounds (fixed nonants applied)
+    double* HI = L.hi + sn;
+    double* ATY = L.aty + sn;         // A^T y of the current y, owned columns
+    double* XR = L.xr + sn;           // restart point
+    double* AXO = L.axo + sm;         // A x of the current x, owned rows
+    double* YR = L.yr + sm;
     auto rowb = [&](int i, double& lo, double& hi) { row_bounds(a, i, sm + i, lo, hi); };
 
     // ------------------------------------------------------------------ prologue (owned elements)
@@ -186,12 +175,20 @@ __global__ __launch_bounds__(NT) void pdhg_stream_kernel(PdhgArgs a) {
     // products of the published x / y for the owned rows / columns
     auto ax_row = [&](const double* xv, int i) {
         double acc = 0.0;
-        for (int p = L.rowptr[i]; p < L.rowptr[i + 1]; ++p) acc = fma(rv[p], get(&xv[L.colidx[p]]), acc);
+        if (RES) {
+            for (int p = lrp[i - r0]; p < lrp[i - r0 + 1]; ++p) acc = fma(lrv[p], get(&xv[lci[p]]), acc);
+        } else {
+            for (int p = L.rowptr[i]; p < L.rowptr[i + 1]; ++p) acc = fma(rv[p], get(&xv[L.colidx[p]]), acc);
+        }
         return acc;
     };
     auto aty_col = [&](const double* yv, int j) {
         double acc = 0.0;
-        for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) acc = fma(cv[p], get(&yv[L.rowidx[p]]), acc);
+        if (RES) {
+            for (int p = lcp[j - c0]; p < lcp[j - c0 + 1]; ++p) acc = fma(lcv[p], get(&yv[lri[p]]), acc);
+        } else {
+            for (int p = L.colptr[j]; p < L.colptr[j + 1]; ++p) acc = fma(cv[p], get(&yv[L.rowidx[p]]), acc);
+        }
         return acc;
     };
     barrier();   // x, y published
@@ -355,7 +352,7 @@ __global__ __launch_bounds__(NT) void pdhg_stream_kernel(PdhgArgs a) {
     for (int j = c0 + t; j < c1; j += NT) {
         const long b = sn + j;
         const double xv = use_avg_final ? get(&XS[j]) * inv : get(&X[j]);
-        X[j] = xv;
+        put(&X[j], xv);
         const double xu = xv * a.dc[b];
         if (a.x_out) a.x_out[b] = xu;
         const int kk = a.lay.col_nonant[j];
@@ -364,7 +361,7 @@ __global__ __launch_bounds__(NT) void pdhg_stream_kernel(PdhgArgs a) {
     for (int i = r0 + t; i < r1; i += NT) {
         const long b = sm + i;
         const double yv = use_avg_final ? get(&YS[i]) * inv : get(&Y[i]);
-        Y[i] = yv;
+        put(&Y[i], yv);
         if (a.y_out) a.y_out[b] = yv * a.dr[b];
     }
     if (kw == 0 && t == 0) {
@@ -377,13 +374,8 @@ __global__ __launch_bounds__(NT) void pdhg_stream_kernel(PdhgArgs a) {
         a.iters_acc[s] += it;
         a.status[s] = st;
     }
-    // the last of the scenario's workgroups out re-arms its barrier counter for the next launch
-    if (K > 1 && t == 0) {
-        if (__hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)K - 1) {
-            __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    if (!alive) break;
+    }   // scenario queue
 }
 
 // ----------------------------------------------------------------------------- dispatch
@@ -391,12 +383,18 @@ constexpr int kStreamNT = 1024;
 
 int pdhg_stream_threads() { return kStreamNT; }
 
+size_t pdhg_stream_lds_bytes(const StreamLayout& L) {
+    if (!L.res) return 0;
+    return (size_t)(L.nr_max + L.nc_max) * sizeof(double) +
+           (size_t)(L.R_max + 1 + L.nr_max + L.C_max + 1 + L.nc_max) * sizeof(int);
+}
+
 // workgroups that can be resident at once (for the co-residency of a scenario's K workgroups)
 hipError_t pdhg_stream_capacity(int* out) {
     int dev = 0, cus = 0, per = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pdhg_stream_kernel<kStreamNT>, kStreamNT, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pdhg_stream_kernel<kStreamNT, false>, kStreamNT, 0);
     if (e != hipSuccess) return e;
     // a 1024-thread workgroup at <= 128 VGPRs fills a CU's 16 wave slots: one per CU, whatever the
     // occupancy API says (the barriers' hand-off protocol is measured for one per CU)
@@ -405,14 +403,17 @@ hipError_t pdhg_stream_capacity(int* out) {
 }
 
 hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream) {
-    const dim3 grid((unsigned)a.S * (unsigned)a.st.K), block(kStreamNT);
-    if (a.st.K == 1) {
-        hipLaunchKernelGGL(pdhg_stream_kernel<kStreamNT>, grid, block, 0, stream, a);
-        return hipGetLastError();
-    }
+    const StreamLayout& L = a.st;
+    // queue head, barrier counters and mailboxes start from zero every launch
+    hipError_t e = hipMemsetAsync(L.ctrl, 0, (size_t)(kCtrlBar + 3 * L.slots) * sizeof(unsigned), stream);
+    if (e != hipSuccess) return e;
+    const dim3 grid((unsigned)L.slots * (unsigned)L.K), block(kStreamNT);
+    const size_t lds = pdhg_stream_lds_bytes(L);
+    const void* fn = L.res ? (const void*)pdhg_stream_kernel<kStreamNT, true> : (const void*)pdhg_stream_kernel<kStreamNT, false>;
     PdhgArgs copy = a;
     void* args[] = {&copy};
-    return hipLaunchCooperativeKernel((const void*)pdhg_stream_kernel<kStreamNT>, grid, block, args, 0, stream);
+    if (L.K == 1) return hipLaunchKernel(fn, grid, block, args, lds, stream);
+    return hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)lds, stream);
 }
 
 }  // namespace phg

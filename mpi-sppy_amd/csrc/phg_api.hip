@@ -35,6 +35,9 @@ size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad);
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream);
 hipError_t pdhg_stream_capacity(int* out);
+size_t pdhg_stream_lds_bytes(const StreamLayout& L);
+hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream);
+size_t pdhg_border_lds_bytes(const BorderLayout& B);
 int pdhg_mfma_num_variants();
 void pdhg_mfma_variant_shape(int v, int* out2);
 hipError_t pdhg_mfma_launch(int v, const PdhgArgs& a, hipStream_t stream);
@@ -85,6 +88,8 @@ struct phg_handle {
     int block_variant = -1;    // workgroup-per-scenario kernel variant (pdhg_block.hip)
     int mfma_variant = -1;     // shared-matrix MFMA kernel variant (pdhg_mfma.hip)
     bool stream_layout = false;   // multi-workgroup streaming kernel (pdhg_stream.hip)
+    bool border_layout = false;   //   ... its bordered block-diagonal form (pdhg_border.hip)
+    BorderLayout bd{};
     StreamLayout st{};
     std::vector<int> stream_cperm;   // CSC entry -> CSR position (values gathered after prep)
     int mshape[2] = {0, 0};
@@ -325,7 +330,7 @@ int phg_set_smoothing(phg_handle* h, int32_t on) {
 int phg_set_layout(phg_handle* h, int32_t policy) {
     if (!h) return fail("null handle");
     if (h->loaded) return fail("phg_set_layout: must be called before phg_load_batch");
-    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_STREAM) return fail("phg_set_layout: bad policy");
+    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_BORDER) return fail("phg_set_layout: bad policy");
     h->layout_policy = policy;
     return 0;
 }
@@ -927,20 +932,215 @@ static int build_mfma_fragments(phg_handle* h, const phg_batch* b) {
     return 0;
 }
 
-// Streaming layout (pdhg_stream.hip).  K workgroups per scenario so that S K workgroups fill the
-// chip (at most what can be resident -- one 1024-thread workgroup per CU; the K of a scenario must
-// be co-resident for their barriers, which the cooperative launch enforces -- and at most 16); rows
-// and columns are split into K contiguous ranges of about equal nonzeros.
+// Bordered block-diagonal layout (pdhg_border.hip).  Columns linked by "sparse" rows (at most
+// max(16, 4 x the mean row length) nonzeros) form blocks (union-find); the blocks are packed,
+// heaviest first, into K groups of about equal nonzeros; rows inside one group are local to it, the
+// others are linking rows (at most 1024).  K: the smallest with every group's slice in LDS, raised
+// to fill the chip when there are few scenarios (at most 16).  Returns 1 (not applicable) when the
+// matrix has no such structure -- fewer than two blocks, a dominant block, too many linking rows or
+// no K that fits -- and the range-split streaming kernel is used instead.
+static int uf_find(std::vector<int>& p, int x) {
+    while (p[x] != x) { p[x] = p[p[x]]; x = p[x]; }
+    return x;
+}
+
+static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vector<int>& colptr,
+                               const std::vector<int>& csc_row, const std::vector<int>& csc_p, int cap) {
+    const int n = b->n, m = b->m, S = std::max(1, b->S);
+    const int* rp = b->rowptr;
+    const int* ci = b->colidx;
+    const int thr = std::max(16, (int)(4.0 * (double)b->nnz / std::max(1, m)));
+    std::vector<int> par(n);
+    for (int j = 0; j < n; ++j) par[j] = j;
+    for (int i = 0; i < m; ++i) {
+        if (rp[i + 1] - rp[i] > thr || rp[i + 1] == rp[i]) continue;
+        const int r0 = uf_find(par, ci[rp[i]]);
+        for (int p = rp[i] + 1; p < rp[i + 1]; ++p) {
+            const int r = uf_find(par, ci[p]);
+            if (r != r0) par[r] = r0;
+        }
+    }
+    std::vector<int> cid(n, -1), root_id(n, -1);
+    std::vector<long> wt;
+    for (int j = 0; j < n; ++j) {
+        const int r = uf_find(par, j);
+        if (root_id[r] < 0) { root_id[r] = (int)wt.size(); wt.push_back(0); }
+        cid[j] = root_id[r];
+        wt[cid[j]] += colptr[j + 1] - colptr[j] + 1;
+    }
+    const int ncomp = (int)wt.size();
+    if (ncomp < 2) return 1;
+    std::vector<int> by(ncomp);
+    for (int c = 0; c < ncomp; ++c) by[c] = c;
+    std::stable_sort(by.begin(), by.end(), [&](int x, int y) { return wt[x] > wt[y]; });
+    long total = 0;
+    for (long w : wt) total += w;
+
+    BorderLayout& B = h->bd;
+    std::vector<int> gof(n), rgrp(m), linkidx(m, -1);
+    std::vector<BorderGroup> groups;
+    std::vector<int> link_rows;
+    auto plan = [&](int K, long* gmax) -> size_t {
+        std::vector<long> load(K, 0);
+        std::vector<int> cg(ncomp);
+        for (int c : by) {
+            int k = 0;
+            for (int q = 1; q < K; ++q)
+                if (load[q] < load[k]) k = q;
+            cg[c] = k;
+            load[k] += wt[c];
+        }
+        *gmax = *std::max_element(load.begin(), load.end());
+        for (int j = 0; j < n; ++j) gof[j] = cg[cid[j]];
+        link_rows.clear();
+        std::fill(linkidx.begin(), linkidx.end(), -1);
+        for (int i = 0; i < m; ++i) {
+            int g = rp[i + 1] > rp[i] ? gof[ci[rp[i]]] : 0;
+            for (int p = rp[i]; p < rp[i + 1]; ++p)
+                if (gof[ci[p]] != g) { g = -1; break; }
+            rgrp[i] = g;
+            if (g < 0) { linkidx[i] = (int)link_rows.size(); link_rows.push_back(i); }
+        }
+        B.nlink = (int)link_rows.size();
+        if (B.nlink > 1024) return SIZE_MAX;
+        std::vector<int> nc(K, 0), nr(K, 0), nrz(K, 0), nlz(K, 0), ncz(K, 0);
+        for (int j = 0; j < n; ++j) { nc[gof[j]]++; ncz[gof[j]] += colptr[j + 1] - colptr[j]; }
+        for (int i = 0; i < m; ++i) {
+            if (rgrp[i] >= 0) { nr[rgrp[i]]++; nrz[rgrp[i]] += rp[i + 1] - rp[i]; }
+            else for (int p = rp[i]; p < rp[i + 1]; ++p) nlz[gof[ci[p]]]++;
+        }
+        B.C_max = *std::max_element(nc.begin(), nc.end());
+        B.R_max = *std::max_element(nr.begin(), nr.end());
+        B.nrz_max = *std::max_element(nrz.begin(), nrz.end());
+        B.nlz_max = *std::max_element(nlz.begin(), nlz.end());
+        B.ncz_max = *std::max_element(ncz.begin(), ncz.end());
+        return pdhg_border_lds_bytes(B);
+    };
+    const size_t budget = 156 * 1024;
+    long gmax = 0;
+    int K = 0;
+    if (const char* ek = std::getenv("PHG_STREAM_K")) {
+        K = std::max(1, std::min(cap, std::atoi(ek)));
+        if (plan(K, &gmax) > budget) return 1;
+    } else {
+        for (int k = 1; k <= 16 && K == 0; ++k)
+            if (plan(k, &gmax) <= budget) K = k;
+        if (K == 0) return 1;
+        const int fill = std::min(16, cap / S);
+        if (fill > K && plan(fill, &gmax) <= budget) K = fill;
+        else plan(K, &gmax);
+    }
+    // a dominant block leaves the other workgroups idle: not this layout's shape
+    if (K > 1 && (double)gmax > 2.0 * (double)total / K) return 1;
+
+    // concatenated per-group arrays
+    std::vector<int> col_list, row_list, rptr, rcol, rperm, lptr, lcol, lperm, cptr, crow, cperm;
+    groups.assign(K, BorderGroup{});
+    for (int k = 0; k < K; ++k) {
+        BorderGroup& G = groups[k];
+        G.c0 = (int)col_list.size();
+        for (int j = 0; j < n; ++j)
+            if (gof[j] == k) col_list.push_back(j);
+        G.nc = (int)col_list.size() - G.c0;
+        G.r0 = (int)row_list.size();
+        for (int i = 0; i < m; ++i)
+            if (rgrp[i] == k) row_list.push_back(i);
+        G.nr = (int)row_list.size() - G.r0;
+        G.rp0 = (int)rptr.size();
+        G.rz0 = (int)rcol.size();
+        for (int q = 0; q < G.nr; ++q) {
+            const int i = row_list[G.r0 + q];
+            rptr.push_back((int)rcol.size() - G.rz0);
+            for (int p = rp[i]; p < rp[i + 1]; ++p) { rcol.push_back(ci[p]); rperm.push_back(p); }
+        }
+        rptr.push_back((int)rcol.size() - G.rz0);
+        G.nrz = (int)rcol.size() - G.rz0;
+        G.lp0 = (int)lptr.size();
+        G.lz0 = (int)lcol.size();
+        for (int l = 0; l < B.nlink; ++l) {
+            const int i = link_rows[l];
+            lptr.push_back((int)lcol.size() - G.lz0);
+            for (int p = rp[i]; p < rp[i + 1]; ++p)
+                if (gof[ci[p]] == k) { lcol.push_back(ci[p]); lperm.push_back(p); }
+        }
+        lptr.push_back((int)lcol.size() - G.lz0);
+        G.nlz = (int)lcol.size() - G.lz0;
+        G.cp0 = (int)cptr.size();
+        G.cz0 = (int)crow.size();
+        for (int q = 0; q < G.nc; ++q) {
+            const int j = col_list[G.c0 + q];
+            cptr.push_back((int)crow.size() - G.cz0);
+            for (int e = colptr[j]; e < colptr[j + 1]; ++e) {
+                const int r = csc_row[e];
+                crow.push_back(linkidx[r] >= 0 ? -(linkidx[r] + 1) : r);
+                cperm.push_back(csc_p[e]);
+            }
+        }
+        cptr.push_back((int)crow.size() - G.cz0);
+        G.ncz = (int)crow.size() - G.cz0;
+    }
+    StreamLayout& L = h->st;
+    L.K = K;
+    L.slots = std::max(1, std::min(S, cap / K));
+    L.res = 0;
+    BorderGroup* gd;
+    if (dput(h, &gd, groups.data(), groups.size())) return -1;
+    B.grp = gd;
+    int* p;
+    auto put_ints = [&](const std::vector<int>& v, const int** dst) {
+        if (dput(h, &p, v.data(), v.size())) return -1;
+        *dst = p;
+        return 0;
+    };
+    if (put_ints(link_rows, &B.link_rows) || put_ints(col_list, &B.col_list) || put_ints(row_list, &B.row_list) ||
+        put_ints(rptr, &B.rptr) || put_ints(rcol, &B.rcol) || put_ints(rperm, &B.rperm) ||
+        put_ints(lptr, &B.lptr) || put_ints(lcol, &B.lcol) || put_ints(lperm, &B.lperm) ||
+        put_ints(cptr, &B.cptr) || put_ints(crow, &B.crow) || put_ints(cperm, &B.cperm))
+        return -1;
+    double* d;
+    if (dalloc(h, &d, (size_t)L.slots * 2 * K * std::max(1, B.nlink))) return -1;
+    B.plink = d;
+    const size_t Sn = (size_t)b->S * n, Sm = (size_t)b->S * m;
+    if (dalloc(h, &d, Sn)) return -1; L.cs = d;
+    if (dalloc(h, &d, Sn)) return -1; L.qs = d;
+    if (dalloc(h, &d, Sn)) return -1; L.lo = d;
+    if (dalloc(h, &d, Sn)) return -1; L.hi = d;
+    if (dalloc(h, &d, Sn)) return -1; L.xsum = d;
+    if (dalloc(h, &d, Sn)) return -1; L.aty = d;
+    if (dalloc(h, &d, Sn)) return -1; L.xr = d;
+    if (dalloc(h, &d, Sm)) return -1; L.ysum = d;
+    if (dalloc(h, &d, Sm)) return -1; L.axo = d;
+    if (dalloc(h, &d, Sm)) return -1; L.yr = d;
+    if (dalloc(h, &d, (size_t)L.slots * K * 16)) return -1; L.part = d;
+    unsigned* u;
+    if (dalloc(h, &u, (size_t)kCtrlBar + 3 * (size_t)L.slots)) return -1; L.ctrl = u;
+    int* e;
+    if (dalloc(h, &e, 1)) return -1; L.err = e;
+    h->stream_layout = true;
+    h->border_layout = true;
+    return 0;
+}
+
+// Streaming layout (pdhg_stream.hip).  Rows and columns are split into K contiguous ranges of
+// about equal nonzeros, one per workgroup of a slot; slots of K co-resident workgroups (one
+// 1024-thread workgroup per CU) take scenarios from a queue.  K: the smallest split whose largest
+// slice (CSR of the owned rows + CSC of the owned columns) fits in a workgroup's LDS -- the
+// resident variant, whose gathers then touch memory only for the published x / y -- raised to
+// fill the chip when there are few scenarios (at most 16); when no K <= 16 fits, the streamed
+// variant (structure and values read from memory every iteration) with K filling the chip.
 static int build_stream_layout(phg_handle* h, const phg_batch* b, const std::vector<int>& colptr,
-                               const std::vector<int>& csc_row, const std::vector<int>& csc_p) {
+                               const std::vector<int>& csc_row, const std::vector<int>& csc_p, int pol) {
     int cap = 0;
     CK(pdhg_stream_capacity(&cap));
-    int K = 1;
-    if (const char* ev = std::getenv("PHG_STREAM_K")) K = std::max(1, std::atoi(ev));
-    else K = std::max(1, std::min(16, cap / std::max(1, b->S)));
-    if (K > 1 && (long)K * b->S > cap) K = std::max(1, cap / b->S);
-    const int n = b->n, m = b->m, nnz = b->nnz;
-    auto split = [&](const int* ptr, int cnt, std::vector<int>& first) {
+    const char* eb = std::getenv("PHG_STREAM_BORDER");   // 0: AUTO skips the bordered form
+    if (pol == PHG_LAYOUT_BORDER || (pol == PHG_LAYOUT_AUTO && !(eb && std::atoi(eb) == 0))) {
+        const int r = build_border_layout(h, b, colptr, csc_row, csc_p, cap);
+        if (r <= 0) return r;
+        if (pol == PHG_LAYOUT_BORDER)
+            return fail("phg_load_batch: no bordered block-diagonal structure that fits (pdhg_border.hip)");
+    }
+    const int n = b->n, m = b->m, nnz = b->nnz, S = std::max(1, b->S);
+    auto split = [&](const int* ptr, int cnt, int K, std::vector<int>& first) {
         first.assign(K + 1, cnt);
         first[0] = 0;
         int q = 1;
@@ -949,11 +1149,41 @@ static int build_stream_layout(phg_handle* h, const phg_batch* b, const std::vec
         for (; q < K; ++q) first[q] = cnt;
         for (int k = 1; k <= K; ++k) first[k] = std::max(first[k], first[k - 1]);
     };
-    std::vector<int> rf, cf;
-    split(b->rowptr, m, rf);
-    split(colptr.data(), n, cf);
     StreamLayout& L = h->st;
+    std::vector<int> rf, cf;
+    auto plan = [&](int K) {   // split for K; fills the per-workgroup maxima, returns the LDS bytes
+        split(b->rowptr, m, K, rf);
+        split(colptr.data(), n, K, cf);
+        L.nr_max = L.nc_max = L.R_max = L.C_max = 0;
+        for (int k = 0; k < K; ++k) {
+            L.nr_max = std::max(L.nr_max, b->rowptr[rf[k + 1]] - b->rowptr[rf[k]]);
+            L.nc_max = std::max(L.nc_max, colptr[cf[k + 1]] - colptr[cf[k]]);
+            L.R_max = std::max(L.R_max, rf[k + 1] - rf[k]);
+            L.C_max = std::max(L.C_max, cf[k + 1] - cf[k]);
+        }
+        L.res = 1;
+        return pdhg_stream_lds_bytes(L);
+    };
+    const size_t budget = 156 * 1024;   // 160 KB per CU less the static reduction scratch
+    int K = 0, res = 0;
+    const char* ek = std::getenv("PHG_STREAM_K");
+    const char* er = std::getenv("PHG_STREAM_RES");
+    const bool allow_res = !(er && std::atoi(er) == 0);
+    if (ek) {
+        K = std::max(1, std::min(cap, std::atoi(ek)));
+        res = allow_res && plan(K) <= budget;
+    } else {
+        for (int k = 1; k <= 16 && allow_res && !res; ++k)
+            if (plan(k) <= budget) { K = k; res = 1; }
+        const int fill = std::max(1, std::min(16, cap / S));
+        if (!res) K = fill;
+        else if (fill > K) { K = fill; res = plan(K) <= budget; }
+    }
+    plan(K);
+    L.res = res;
     L.K = K;
+    L.slots = std::max(1, std::min(S, cap / K));
+    if (K > cap) return fail("phg_load_batch: stream layout wants more workgroups per scenario than fit");
     int* p;
     if (dput(h, &p, rf.data(), rf.size())) return -1; L.row_first = p;
     if (dput(h, &p, cf.data(), cf.size())) return -1; L.col_first = p;
@@ -974,9 +1204,9 @@ static int build_stream_layout(phg_handle* h, const phg_batch* b, const std::vec
     if (dalloc(h, &d, Sm)) return -1; L.ysum = d;
     if (dalloc(h, &d, Sm)) return -1; L.axo = d;
     if (dalloc(h, &d, Sm)) return -1; L.yr = d;
-    if (dalloc(h, &d, (size_t)b->S * K * 16)) return -1; L.part = d;
+    if (dalloc(h, &d, (size_t)L.slots * K * 16)) return -1; L.part = d;
     unsigned* u;
-    if (dalloc(h, &u, 2 * (size_t)b->S)) return -1; L.bar = u;
+    if (dalloc(h, &u, (size_t)kCtrlBar + 3 * (size_t)L.slots)) return -1; L.ctrl = u;
     int* e;
     if (dalloc(h, &e, 1)) return -1; L.err = e;
     h->stream_layout = true;
@@ -987,6 +1217,11 @@ static int build_stream_layout(phg_handle* h, const phg_batch* b, const std::vec
 static int build_stream_values(phg_handle* h) {
     StreamLayout& L = h->st;
     const int Sv = h->vals_shared ? 1 : h->S;
+    if (h->border_layout) {   // gathered into LDS through the layout's position arrays
+        L.rvals = h->vals;
+        L.vstride = h->vals_shared ? 0 : h->nnz;
+        return 0;
+    }
     int* perm;
     double* cv;
     if (dput(h, &perm, h->stream_cperm.data(), h->stream_cperm.size())) return -1;
@@ -1224,13 +1459,13 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
         gr = build_layout(h, b, colptr, csc_row, csc_p);
         if (gr < 0 || (gr > 0 && pol == PHG_LAYOUT_GATHER)) return -1;
     }
-    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && pol != PHG_LAYOUT_STREAM) {
+    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && pol != PHG_LAYOUT_STREAM && pol != PHG_LAYOUT_BORDER) {
         br = build_block_layout(h, b, colptr, csc_row, csc_p);
         if (br < 0 || (br > 0 && pol == PHG_LAYOUT_BLOCK)) return -1;
         h->variant = -1;
     }
     if (h->mfma_variant < 0 && lr != 0 && gr != 0 && br != 0) {
-        if (build_stream_layout(h, b, colptr, csc_row, csc_p)) return -1;
+        if (build_stream_layout(h, b, colptr, csc_row, csc_p, pol)) return -1;
         h->variant = -1;
     }
     if (h->mfma_variant >= 0) h->variant = -1;
@@ -1335,7 +1570,7 @@ int phg_mfma_info(phg_handle* h, int32_t* o) {
 int phg_info(phg_handle* h, int32_t* o) {
     if (!h || !h->loaded) return fail("phg_info: no batch loaded");
     o[0] = h->S; o[1] = h->n; o[2] = h->m_orig; o[3] = h->nnz; o[4] = h->N; o[5] = h->N_tot;
-    if (h->stream_layout) { o[6] = 400 + h->st.K; o[7] = 256; }
+    if (h->stream_layout) { o[6] = (h->border_layout ? 500 : 400) + h->st.K; o[7] = 1024 * h->st.K; }
     else if (h->mfma_variant >= 0) { o[6] = 300 + h->mfma_variant; o[7] = 4; }
     else if (h->local_variant >= 0) { o[6] = 100 + h->local_variant; o[7] = h->lshape[0]; }
     else if (h->block_variant >= 0) { o[6] = 200 + h->block_variant; o[7] = h->bshape[0]; }
@@ -1457,7 +1692,9 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.gate = o->skip_if_conv_below > 0 ? h->gate : nullptr;
     a.gate_below = o->skip_if_conv_below;
     a.queue = h->persist ? h->queue : nullptr;
-    if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));
+    a.bd = h->bd;
+    if (h->border_layout) CK(pdhg_border_launch(a, h->stream));
+    else if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));
     else if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
     else if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));

@@ -84,10 +84,40 @@ struct StreamLayout {
     long vstride;           // nnz, or 0 when every scenario has the same matrix
     double *cs, *qs, *lo, *hi, *xsum, *aty, *xr;   // [S*n]
     double *ysum, *axo, *yr;                        // [S*m]
-    double* part;           // [S*K*16] per-workgroup partial sums
-    unsigned* bar;          // [2*S] barrier arrivals, workgroups done (0 between launches)
+    double* part;           // [slots*K*16] per-workgroup partial sums
+    unsigned* ctrl;         // [kCtrlBar + 3*slots] queue head, per-slot barrier counters and mailboxes
     int* err;               // [1] a barrier wait ran past its bound
+    int slots;              // groups of K workgroups, each solving queued scenarios one at a time
+    int res;                // 1: each workgroup keeps its CSR / CSC slice in LDS (pdhg_stream_lds_bytes)
+    int nr_max, nc_max;     // largest per-workgroup nonzero counts (owned rows / owned columns)
+    int R_max, C_max;       // largest per-workgroup row / column counts
 };
+// Bordered block-diagonal layout (pdhg_border.hip): workgroup k of a slot owns a group of column
+// blocks and the rows inside them; the NL linking rows are replicated.  Per group, offsets into the
+// concatenated arrays below.
+struct BorderGroup {
+    int c0, nc;          // col_list[c0 .. c0 + nc): owned columns
+    int r0, nr;          // row_list[r0 .. r0 + nr): local rows
+    int rp0, rz0, nrz;   // rptr[rp0 ..] (nr + 1, local offsets), rcol / rperm[rz0 .. rz0 + nrz)
+    int lp0, lz0, nlz;   // lptr[lp0 ..] (NL + 1), lcol / lperm[lz0 .. lz0 + nlz): linking rows on owned columns
+    int cp0, cz0, ncz;   // cptr[cp0 ..] (nc + 1), crow / cperm[cz0 .. cz0 + ncz): owned columns (CSC)
+    int pad[3];
+};
+struct BorderLayout {
+    int nlink;                       // linking rows (<= 1024: one thread each)
+    int nrz_max, nlz_max, ncz_max;   // largest per-group entry counts
+    int R_max, C_max;                // largest per-group local-row / column counts
+    const BorderGroup* grp;          // [K]
+    const int* link_rows;            // [nlink]
+    const int *col_list, *row_list;
+    const int *rptr, *rcol, *rperm;  // local rows: CSR pointers, columns, positions in the CSR values
+    const int *lptr, *lcol, *lperm;  // linking rows restricted to each group
+    const int *cptr, *crow, *cperm;  // owned columns: CSC pointers, rows (-(l+1): linking row l), positions
+    double* plink;                   // [slots * 2 * K * nlink] double-buffered linking-row partials
+};
+
+constexpr int kCtrlHead = 0;     // StreamLayout::ctrl: queue head
+constexpr int kCtrlBar = 16;     //   then 2 words per slot (barrier counter), then 1 per slot (mailbox)
 
 struct PdhgArgs {
     int S, n, m, nnz, N, n_pad;
@@ -96,6 +126,7 @@ struct PdhgArgs {
     BlockLayout blk;
     MfmaLayout mf;
     StreamLayout st;
+    BorderLayout bd;
     // scenario data (scaled where noted)
     const double* vals;     // [S*nnz] scaled values
     const double* c;        // [S*n]   min-form objective, UNscaled

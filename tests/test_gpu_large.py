@@ -35,6 +35,10 @@ CASES = {
     "uc_small": (lambda S: uc.scenario_names_creator(S), uc.scenario_creator,
                  {"num_gens": 6, "num_periods": 8, "num_scens": 4},
                  lambda S: om.uc_names(S), om.uc, {"num_gens": 6, "num_periods": 8, "num_scens": 4}),
+    # 24 units x 12 periods: the demand / reserve rows (24 nonzeros) link the per-unit blocks
+    "uc_mid": (lambda S: uc.scenario_names_creator(S), uc.scenario_creator,
+               {"num_gens": 24, "num_periods": 12, "num_scens": 3},
+               lambda S: om.uc_names(S), om.uc, {"num_gens": 24, "num_periods": 12, "num_scens": 3}),
 }
 
 
@@ -56,8 +60,9 @@ def test_iter0_lp_block_kernel(case, S):
 @pytest.mark.parametrize("case,S,layout", [("sslp", 4, "auto"), ("netdes", 3, "auto"), ("sslp", 4, "stream"),
                                            ("uc_small", 4, "stream")])
 def test_prox_qp_block_kernel(case, S, layout):
-    """layout "stream": the multi-workgroup streaming kernel (pdhg_stream.hip) with K > 1
-    workgroups per scenario (few scenarios: K = 16), its cross-workgroup barriers and sums."""
+    """layout "stream": the range-split multi-workgroup kernel (pdhg_stream.hip) with K > 1
+    workgroups per scenario (few scenarios: K = 16), its cross-workgroup barriers and sums;
+    (the bordered kernel: test_border_matches_block_kernel)."""
     pn, pc, pkw, on, oc, okw = CASES[case]
     ph = PH(_opts(pdhg_layout=layout), pn(S), pc, scenario_creator_kwargs=pkw)
     ph.PH_Prep()
@@ -77,22 +82,69 @@ def test_prox_qp_block_kernel(case, S, layout):
         np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6)
         assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
     if layout == "stream":
-        assert ph.engine.layout == "stream" and ph.engine.workgroups_per_scenario > 1
+        assert ph.engine.layout == layout and ph.engine.workgroups_per_scenario > 1
 
 
-@pytest.mark.parametrize("S", [2])
-def test_uc_fullsize_stream_vs_oracle(S):
+def test_border_matches_block_kernel():
+    """The bordered block-diagonal kernel (pdhg_border.hip: 16 workgroups per scenario, one block
+    per unit, the 24-nonzero demand / reserve rows as linking rows) runs the same arithmetic as the
+    workgroup-per-scenario block kernel in a different order: on a 24-unit x 12-period UC LP and
+    one prox-QP at the oracle's W / x-bar, both reach the same iteration counts and objectives (to
+    rounding), and the objectives match HiGHS at 1e-6.  (This LP is hard for PDHG: one scenario
+    stops at the 2e5-iteration cap with a 1e-9-level KKT error, in both kernels.)"""
+    kw = {"num_gens": 24, "num_periods": 12, "num_scens": 3}
+    o = oph.OraclePH(_opts(), om.uc_names(3), om.uc, kw)
+    o.Iter0()
+    o.Compute_Xbar()
+    o.Update_W()
+    res = {}
+    for layout in ("block", "border"):
+        ph = PH(_opts(pdhg_layout=layout), uc.scenario_names_creator(3), uc.scenario_creator, scenario_creator_kwargs=kw)
+        ph.PH_Prep()
+        assert ph.engine.layout == layout
+        ph.Iter0()
+        ob0 = ph.engine.get(_lib.F_OBJ).copy()
+        ph.engine.set(_lib.F_W, o.W.ravel())
+        ph.engine.set(_lib.F_XBAR, o.xbar[0])
+        ph.solve_loop()
+        res[layout] = (ob0, ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get_i32(_lib.I_ITERS).copy(), ph.nonants())
+        if layout == "border":
+            assert ph.engine.workgroups_per_scenario > 1
+    (a0, a1, ai, ax), (b0, b1, bi, bx) = res["block"], res["border"]
+    np.testing.assert_array_equal(ai, bi)
+    np.testing.assert_allclose(b0, a0, rtol=1e-11)
+    np.testing.assert_allclose(b1, a1, rtol=1e-11)
+    np.testing.assert_allclose(bx, ax, atol=1e-8)
+    o.solve_loop()
+    np.testing.assert_allclose(b1, o.obj, rtol=1e-6)
+
+
+@pytest.mark.parametrize("S,layout", [(2, "auto"), (2, "stream"), (40, "auto")])
+def test_uc_fullsize_stream_vs_oracle(S, layout):
     """The UC-shaped LP at full size (n = 20 400, m = 20 326, N = 4 080) through the AUTO layout
-    (too large for a workgroup's LDS: the streaming kernel, K > 1 workgroups per scenario).  At this
-    size PDHG needs > 2e5 iterations for a 1e-9 relative KKT error, so the solve runs at
-    pdhg_eps = 1e-6 (the accuracy PDLP-class solvers default to): Iter0 LP objectives and dual
-    bounds against HiGHS at 1e-5 relative (LP optima may be non-unique: objectives only)."""
+    (too large for a workgroup's LDS: a multi-workgroup kernel, K > 1 workgroups per scenario):
+    the bordered block-diagonal kernel (pdhg_border.hip: one block per unit, the 96 demand /
+    reserve rows linking them; what AUTO picks) and the range-split kernel (pdhg_stream.hip,
+    layout "stream"); S = 40 puts several scenarios through each slot's queue.  At this size PDHG
+    needs > 2e5 iterations for a 1e-9 relative KKT error, so the solve runs at pdhg_eps = 1e-6 (the
+    accuracy PDLP-class solvers default to): Iter0 LP objectives and dual bounds against HiGHS at
+    1e-5 relative (LP optima may be non-unique: objectives only; the oracle solves a sample of
+    scenarios when S is large)."""
     so = {"pdhg_eps": 1e-6}
-    ph = PH(_opts(iter0_solver_options=so, iterk_solver_options=so), uc.scenario_names_creator(S),
+    ph = PH(_opts(iter0_solver_options=so, iterk_solver_options=so, pdhg_layout=layout), uc.scenario_names_creator(S),
             uc.scenario_creator, scenario_creator_kwargs={"num_scens": S})
     ph.PH_Prep()
-    assert ph.engine.layout == "stream" and ph.engine.workgroups_per_scenario > 1
+    assert ph.engine.layout == ("border" if layout == "auto" else "stream") and ph.engine.workgroups_per_scenario > 1
     tb = ph.Iter0()
+    if S > 4:
+        pick = [0, 1, S // 2, S - 1]
+        # (the generator's data depend on the scenario's name only; num_scens sets the probability)
+        o = oph.OraclePH(_opts(), [om.uc_names(S)[k] for k in pick], om.uc, {"num_scens": len(pick)})
+        o.Iter0()
+        assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+        np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ)[pick], o.obj, rtol=1e-5)
+        np.testing.assert_allclose(ph.engine.get(_lib.F_BOUND)[pick], o.outer, rtol=1e-5)
+        return
     o = oph.OraclePH(_opts(), om.uc_names(S), om.uc, {"num_scens": S})
     otb = o.Iter0()
     assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
