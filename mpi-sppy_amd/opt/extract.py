@@ -1,0 +1,207 @@
+"""Standard-form extraction: a model -> ``min/max c^T x + c0  s.t.  row_lo <= A x <= row_hi,
+col_lo <= x <= col_hi`` in CSR, the arrays ``phg_load_batch`` takes (include/phg.h).
+
+The reference hands each scenario's Pyomo model to a solver plugin, which writes it out for the
+external solver (``spopt.py:184-231``).  Here the same model is read ONCE into standard form and
+then lives in the batch.  Three sources:
+
+* :class:`~mpisppy_amd.model.LinearModel` -- already standard form;
+* any model following the duck-typed protocol below (what a modelling layer, or a test, supplies);
+* a Pyomo ``ConcreteModel`` when Pyomo is importable: the active variables, the active linear
+  constraints and the single active objective, through ``pyomo.repn.generate_standard_repn``.
+  Pyomo is absent on the build container and on the GPU box, so this path is written against
+  Pyomo's public API and is PARITY UNPINNED (never executed here); a nonlinear or quadratic body
+  raises.
+
+Duck-typed protocol (``extract`` checks for ``variables``):
+  ``model.variables()``   -> sequence of variable objects (``.name``, ``.lb``, ``.ub`` with None = unbounded,
+                             optional ``.fixed`` / ``.value``: a fixed variable gets lb = ub = value)
+  ``model.constraints()`` -> sequence of rows (``.name``, ``.terms`` = [(variable, coef), ...],
+                             ``.lower`` / ``.upper`` with None = unbounded, optional ``.constant`` moved
+                             to the bounds)
+  ``model.objective()``   -> object with ``.terms``, optional ``.constant``, ``.sense`` (1 min, -1 max)
+"""
+import numpy as np
+
+from ..model import INF, LinearModel, VarData
+from ..scenario_tree import ScenarioNode
+
+
+class StandardForm:
+    """CSR standard form of one model; ``variables`` are the source objects in column order."""
+
+    def __init__(self, name, variables, names, c, c0, sense, rowptr, colidx, vals, row_lo, row_hi, row_names,
+                 col_lo, col_hi):
+        self.name = name
+        self.variables = variables
+        self.names = names
+        self.c, self.c0, self.sense = c, c0, sense
+        self.rowptr, self.colidx, self.vals = rowptr, colidx, vals
+        self.row_lo, self.row_hi, self.row_names = row_lo, row_hi, row_names
+        self.col_lo, self.col_hi = col_lo, col_hi
+        self.col_of = {id(v): j for j, v in enumerate(variables)}
+
+    @property
+    def n(self):
+        return len(self.c)
+
+    @property
+    def m(self):
+        return len(self.row_lo)
+
+
+def _bound(v, default):
+    return default if v is None else float(v)
+
+
+def _csr(rows, n):
+    """rows: list of dict col -> coef -> (rowptr, colidx, vals), columns sorted in each row."""
+    rowptr = np.zeros(len(rows) + 1, np.int32)
+    cols, vals = [], []
+    for i, d in enumerate(rows):
+        for j in sorted(d):
+            cols.append(j)
+            vals.append(d[j])
+        rowptr[i + 1] = len(cols)
+    return rowptr, np.array(cols, np.int32), np.array(vals, np.float64)
+
+
+def _from_linear_model(m):
+    a = m.arrays()
+    cols = [VarData(m, j, nm) for j, nm in enumerate(m.column_names())]
+    sf = StandardForm(m.name, cols, m.column_names(), a["c"], m.obj_offset, m.sense, a["rowptr"], a["colidx"],
+                      a["vals"], a["row_lo"], a["row_hi"], [r[3] for r in m._rows], a["col_lo"], a["col_hi"])
+    sf.col_of = {}   # LinearModel variables map by column index (VarData objects are made on demand)
+    return sf
+
+
+def _from_duck(model):
+    variables = list(model.variables())
+    col = {id(v): j for j, v in enumerate(variables)}
+    n = len(variables)
+    lo = np.empty(n)
+    hi = np.empty(n)
+    for j, v in enumerate(variables):
+        if getattr(v, "fixed", False):
+            lo[j] = hi[j] = float(v.value)
+        else:
+            lo[j], hi[j] = _bound(v.lb, -INF), _bound(v.ub, INF)
+    rows, rlo, rhi, rnames = [], [], [], []
+    for r in model.constraints():
+        d = {}
+        for v, a in r.terms:
+            j = col[id(v)]
+            d[j] = d.get(j, 0.0) + float(a)
+        k = float(getattr(r, "constant", 0.0) or 0.0)
+        rows.append(d)
+        rlo.append(_bound(r.lower, -INF) - k)
+        rhi.append(_bound(r.upper, INF) - k)
+        rnames.append(getattr(r, "name", f"r{len(rows) - 1}"))
+    ob = model.objective()
+    c = np.zeros(n)
+    for v, a in ob.terms:
+        c[col[id(v)]] += float(a)
+    rp, ci, vals = _csr(rows, n)
+    return StandardForm(getattr(model, "name", ""), variables, [getattr(v, "name", f"x{j}") for j, v in enumerate(variables)],
+                        c, float(getattr(ob, "constant", 0.0) or 0.0), int(getattr(ob, "sense", 1)), rp, ci, vals,
+                        np.array(rlo), np.array(rhi), rnames, lo, hi)
+
+
+def _from_pyomo(model):   # parity unpinned: Pyomo is not importable here (module docstring)
+    import pyomo.environ as pyo
+    from pyomo.repn import generate_standard_repn
+    variables = list(model.component_data_objects(pyo.Var, active=True, descend_into=True))
+    col = {id(v): j for j, v in enumerate(variables)}
+    n = len(variables)
+    lo, hi = np.empty(n), np.empty(n)
+    for j, v in enumerate(variables):
+        if v.fixed:
+            lo[j] = hi[j] = float(pyo.value(v))
+        else:
+            lo[j], hi[j] = _bound(v.lb, -INF), _bound(v.ub, INF)
+    rows, rlo, rhi, rnames = [], [], [], []
+    for con in model.component_data_objects(pyo.Constraint, active=True, descend_into=True):
+        repn = generate_standard_repn(con.body, compute_values=True)
+        if not repn.is_linear():
+            raise ValueError(f"constraint {con.name}: only linear constraints are supported")
+        d = {}
+        for v, a in zip(repn.linear_vars, repn.linear_coefs):
+            d[col[id(v)]] = d.get(col[id(v)], 0.0) + float(a)
+        k = float(repn.constant)
+        rows.append(d)
+        rlo.append(-INF if con.lower is None else float(pyo.value(con.lower)) - k)
+        rhi.append(INF if con.upper is None else float(pyo.value(con.upper)) - k)
+        rnames.append(con.name)
+    objs = list(model.component_data_objects(pyo.Objective, active=True, descend_into=True))
+    if len(objs) != 1:
+        raise ValueError(f"expected one active objective, found {len(objs)}")
+    repn = generate_standard_repn(objs[0].expr, compute_values=True)
+    if not repn.is_linear():
+        raise ValueError("only a linear objective is supported (PH adds its own prox term)")
+    c = np.zeros(n)
+    for v, a in zip(repn.linear_vars, repn.linear_coefs):
+        c[col[id(v)]] += float(a)
+    rp, ci, vals = _csr(rows, n)
+    sense = 1 if objs[0].sense == pyo.minimize else -1
+    return StandardForm(model.name, variables, [v.name for v in variables], c, float(repn.constant), sense, rp, ci,
+                        vals, np.array(rlo), np.array(rhi), rnames, lo, hi)
+
+
+def extract(model):
+    """Standard form of ``model`` (LinearModel, duck-typed model, or Pyomo model)."""
+    if isinstance(model, LinearModel):
+        return _from_linear_model(model)
+    if hasattr(model, "variables") and hasattr(model, "constraints"):
+        return _from_duck(model)
+    if hasattr(model, "component_data_objects"):
+        return _from_pyomo(model)
+    raise TypeError(f"cannot extract a standard form from {type(model).__name__}")
+
+
+def to_linear_model(sf, name=None):
+    """The engine's model object for a standard form (one column per source variable, in order)."""
+    m = LinearModel(name or sf.name)
+    for j, nm in enumerate(sf.names):
+        col = m._new_col(str(nm))
+        m._lo[col], m._hi[col], m._cost[col] = float(sf.col_lo[j]), float(sf.col_hi[j]), float(sf.c[j])
+    for i in range(sf.m):
+        d = {int(sf.colidx[q]): float(sf.vals[q]) for q in range(sf.rowptr[i], sf.rowptr[i + 1])}
+        m._rows.append((d, float(sf.row_lo[i]), float(sf.row_hi[i]), str(sf.row_names[i])))
+    m.sense = sf.sense
+    m.obj_offset = float(sf.c0)
+    return m
+
+
+def as_scenario_model(model):
+    """A scenario model the batch can take: LinearModel as is; otherwise its standard form as a
+    LinearModel whose ``_mpisppy_node_list`` maps each node's nonant variables (source objects) to
+    columns, keeping names, probabilities and the source (``_source``, ``_source_vars``) so that
+    solutions can be written back (:func:`load_values`)."""
+    if isinstance(model, LinearModel):
+        return model
+    sf = extract(model)
+    lm = to_linear_model(sf, getattr(model, "name", None))
+    nodes = []
+    for nd in getattr(model, "_mpisppy_node_list", []):
+        vl = [VarData(lm, sf.col_of[id(v)], sf.names[sf.col_of[id(v)]]) for v in nd.nonant_vardata_list]
+        nodes.append(ScenarioNode(nd.name, nd.cond_prob, nd.stage, None, vl, lm, parent_name=getattr(nd, "parent_name", None)))
+    if nodes:
+        lm._mpisppy_node_list = nodes
+    if hasattr(model, "_mpisppy_probability"):
+        lm._mpisppy_probability = model._mpisppy_probability
+    lm._source = model
+    lm._source_vars = sf.variables
+    return lm
+
+
+def load_values(lm, x):
+    """Write column values ``x`` back into the model's variables (``load_vars``)."""
+    lm._solution = np.asarray(x, np.float64).copy()
+    src = getattr(lm, "_source_vars", None)
+    if src is None:
+        return
+    for v, xv in zip(src, lm._solution):
+        if hasattr(v, "set_value"):
+            v.set_value(float(xv))
+        else:
+            v.value = float(xv)

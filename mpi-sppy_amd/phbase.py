@@ -90,8 +90,6 @@ class PHBase(SPBase):
                     raise ValueError(f"smoothed PH needs option {k}")
         if self.options.get("linearize_proximal_terms"):
             raise NotImplementedError("linearize_proximal_terms: the engine solves the exact prox QP")
-        if self.options.get("bundles_per_rank", 0):
-            raise NotImplementedError("bundles are not supported by the GPU engine yet")
 
     # ------------------------------------------------------------------------------- engine
     def _virt_nproc(self):

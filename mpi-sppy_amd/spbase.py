@@ -50,7 +50,9 @@ class SPBase:
         self.global_rank = self.cylinder_rank
         self.E1_tolerance = E1_tolerance
         self.variable_probability = variable_probability
-        self.bundling = False
+        self.bundling = bool(options.get("bundles_per_rank", 0))
+        if self.bundling:
+            self._setup_loose_bundles(scenario_creator, scenario_creator_kwargs or {})
         self._calculate_scenario_ranks()
         self._create_scenarios(scenario_creator_kwargs or {})
         self._look_and_leap()
@@ -69,6 +71,51 @@ class SPBase:
         self._scenario_slices = [r for r, sl in enumerate(self._rank_slices) for _ in sl]
         self.local_scenario_names = [self.all_scenario_names[i] for i in self._rank_slices[self.cylinder_rank]]
         self.scen_global0 = self._rank_slices[self.cylinder_rank][0] if self._rank_slices[self.cylinder_rank] else 0
+
+    def _setup_loose_bundles(self, scenario_creator, kw):
+        """``bundles_per_rank`` (``spbase.py:223-257`` _assign_bundles, ``spopt.py:840-873``
+        _subproblem_creation): each rank's scenarios are split into that many contiguous groups and
+        each group is solved as one subproblem, its extensive form (``utils/ef.py``).  Here the
+        bundles then take the scenarios' place in the batch (named ``rank<r>bundle<b>`` as in the
+        reference, probability = the members' sum): the members of a bundle share one nonant copy,
+        so their W / x-bar updates coincide and PH over the bundles is PH over the scenarios with
+        every member's nonants equal (the conv metric weighs each bundle once -- the reference's
+        per-scenario count when the bundles are equal-sized).  Two-stage trees only."""
+        from .utils.ef import create_EF_from_scen_dict
+        from .utils.proper_bundler import bundle_scenarios
+        from .scenario_tree import attach_root_node
+        bpr = int(self.options["bundles_per_rank"])
+        S = len(self.all_scenario_names)
+        if self.n_proc * bpr > S:
+            raise RuntimeError("Not enough scenarios to satisfy the bundles_per_rank requirement")
+        slices = scen_names_to_ranks_slices(S, self.n_proc)
+        self.names_in_bundles = {}
+        bundle_names = []
+        for r, slc in enumerate(slices):
+            groups = bundle_scenarios([self.all_scenario_names[i] for i in slc], bpr)
+            self.names_in_bundles[r] = dict(enumerate(groups))
+            bundle_names += [f"rank{r}bundle{b}" for b in range(bpr)]
+        members = {nm: grp for r in range(self.n_proc) for nm, grp in
+                   zip(bundle_names[r * bpr:(r + 1) * bpr], self.names_in_bundles[r].values())}
+        self.all_scenario_names_unbundled = self.all_scenario_names
+        self.all_scenario_names = bundle_names
+
+        def bundle_creator(bname, **ckw):
+            sdict = {}
+            for sname in members[bname]:
+                sc = scenario_creator(sname, **ckw)
+                if len(sc._mpisppy_node_list) != 1:
+                    raise RuntimeError("bundles_per_rank: two-stage scenario trees only")
+                if getattr(sc, "_mpisppy_probability", None) in (None, "uniform"):
+                    sc._mpisppy_probability = 1.0 / S
+                sdict[sname] = sc
+            ef = create_EF_from_scen_dict(sdict, EF_name=bname, nonant_for_fixed_vars=False)
+            nonants = [v for (ndn, _i), v in sorted(ef.ref_vars.items(), key=lambda t: t[0][1]) if ndn == "ROOT"]
+            attach_root_node(ef, 0, nonants)
+            ef._mpisppy_probability = sum(float(sc._mpisppy_probability) for sc in sdict.values())
+            return ef
+
+        self.scenario_creator = bundle_creator
 
     def _create_scenarios(self, kw):
         self.local_scenarios = {}
