@@ -63,7 +63,7 @@ def parse():
                     help="PDHG primal weight at each solve: fresh estimate, the previous solve's, or "
                          "their geometric mean (default)")
     ap.add_argument("--no-presolve", action="store_true", help="keep singleton rows as rows")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     return ap.parse_args()
 
 

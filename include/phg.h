@@ -180,8 +180,10 @@ int  phg_mfma_info(phg_handle* h, int32_t* out4);
 int  phg_info(phg_handle* h, int32_t* out8);   /* S, n, m, nnz, N, N_tot, kernel variant
                                                   (>= 100: lane-local, >= 200: workgroup,
                                                   >= 300: shared-matrix MFMA, 400 + K:
-                                                  streaming, K workgroups per scenario),
-                                                  lanes (threads) per scenario             */
+                                                  range-split streaming, 500 + K / 600 + K:
+                                                  bordered block-diagonal, memory- /
+                                                  register-resident; K workgroups per
+                                                  scenario), lanes (threads) per scenario  */
 
 /* Solve every scenario's subproblem (solve_loop):
  *   min-form  c^T x + w_on * sum_k W_k x_k + prox_on * sum_k rho_k/2 (x_k - xbar_k)^2      */

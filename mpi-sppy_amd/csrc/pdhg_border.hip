@@ -446,24 +446,558 @@ __global__ __launch_bounds__(NT) void pdhg_border_kernel(PdhgArgs a) {
     }   // scenario queue
 }
 
+// ----------------------------------------------------------------------------- register-resident
+// The same solve with every owned element's state in registers (512-thread workgroups, see the
+// dispatch; E = 2: 254 VGPRs, no spills -- E = 4 spills ~100): thread t owns columns t + e NT and
+// local rows t + e NT (e < E); x and y of the group live in LDS (Xl, Yl, indexed by local position)
+// for the gathers, so a PDHG iteration touches memory only for the linking-row exchange -- the
+// memory-resident kernel above moves each iteration's vectors through L2 / HBM (PMC: ~1.7 TB per
+// UC launch at S = 64).  Needs C_max, R_max <= E NT (the host picks E, or this variant is not used).
+template <int NT, int E>
+__global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
+    if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
+    __shared__ double red[16 * (NT / 64)];
+    __shared__ int s_w;
+    extern __shared__ double dyn[];
+    const StreamLayout& L = a.st;
+    const BorderLayout& B = a.bd;
+    const int K = L.K;
+    const int slot = blockIdx.x / K, kw = blockIdx.x % K;
+    const int t = threadIdx.x;
+    const BorderGroup G = B.grp[kw];
+    const int NL = B.nlink;
+    const int nc = G.nc, nr = G.nr;
+    double* lrv = dyn;                               // [nrz_max]
+    double* lkv = lrv + B.nrz_max;                   // [nlz_max]
+    double* lcv = lkv + B.nlz_max;                   // [ncz_max]
+    double* Xl = lcv + B.ncz_max;                    // [C_max] x of the owned columns (local position)
+    double* Yl = Xl + B.C_max;                       // [R_max] y of the local rows
+    double* yl = Yl + B.R_max;                       // [NL]
+    double* ylx = yl + NL;                           // [NL]
+    double* xtmp = ylx + NL;                         // [max(NL + K, 16 K)] staged cross-workgroup partials
+    int* lrp = reinterpret_cast<int*>(xtmp + B.xtmp_len);   // [R_max + 1]
+    int* lci = lrp + B.R_max + 1;                    // [nrz_max] local column position
+    int* lkp = lci + B.nrz_max;                      // [NL + 1]
+    int* lkc = lkp + NL + 1;                         // [nlz_max] local column position
+    int* lcp = lkc + B.nlz_max;                      // [C_max + 1]
+    int* lri = lcp + B.C_max + 1;                    // [ncz_max] local row position, or -(l + 1)
+    for (int q = t; q <= nr; q += NT) lrp[q] = B.rptr[G.rp0 + q];
+    for (int q = t; q < G.nrz; q += NT) lci[q] = B.rcl[G.rz0 + q];
+    for (int q = t; q <= NL; q += NT) lkp[q] = B.lptr[G.lp0 + q];
+    for (int q = t; q < G.nlz; q += NT) lkc[q] = B.lcl[G.lz0 + q];
+    for (int q = t; q <= nc; q += NT) lcp[q] = B.cptr[G.cp0 + q];
+    for (int q = t; q < G.ncz; q += NT) lri[q] = B.crl[G.cz0 + q];
+    // owned elements of this thread (fixed for the launch)
+    int jc[E], ir[E];
+    bool cv_[E], rv_[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int q = t + e * NT;
+        cv_[e] = q < nc;
+        rv_[e] = q < nr;
+        jc[e] = cv_[e] ? B.col_list[G.c0 + q] : 0;
+        ir[e] = rv_[e] ? B.row_list[G.r0 + q] : 0;
+    }
+
+    unsigned* bar = L.ctrl + kCtrlBar + 2 * slot;
+    unsigned* mbox = L.ctrl + kCtrlBar + 2 * L.slots + slot;
+    unsigned nbar = 0;
+    bool alive = true;
+    auto barrier = [&]() {   // counter barrier: only for the per-scenario mailbox
+        if (K == 1) { __syncthreads(); return; }
+        ++nbar;
+        if (!scen_barrier(bar, nbar * (unsigned)K, L.err)) alive = false;
+    };
+    // Cross-workgroup sums as data-tagged granules (cdna_hip_programming.md Guideline 16, R2): a
+    // double is two 8-byte {tag = epoch, 32-bit half} words, each one sc1 store; a reader re-reads
+    // the pair until both tags are the epoch -- no counter, no drain, no barrier.  Every reading
+    // thread loads ONE pair, so a hop costs one round trip (the counter barrier and K dependent
+    // partial loads cost ~10 us of a ~14 us iteration, measured in-kernel).  Epochs count the hops
+    // of each kind (zeroed buffers every launch); buffers are double-buffered by epoch parity: a
+    // workgroup rewrites a parity only after a later hop that every workgroup joins after reading
+    // this one.  A bounded spin that gives up sets s_dead; callers read it after a barrier.
+    __shared__ int s_dead;
+    if (t == 0) s_dead = 0;
+    unsigned long long* G1 = reinterpret_cast<unsigned long long*>(B.plink);            // [slots][2][NL][K][2]
+    unsigned long long* G2 = G1 + (long)L.slots * 2 * NL * K * 2;                         // [slots][2][NL][2]
+    unsigned long long* GS = G2 + (long)L.slots * 2 * NL * 2;                             // [slots][2][K][16][2]
+    unsigned ex_ep = 0, ss_ep = 0;
+    auto gput = [&](unsigned long long* g, unsigned ep, double v) {
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+        const unsigned long long tag = (unsigned long long)ep << 32;
+        __hip_atomic_store(g, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto gget = [&](const unsigned long long* g, unsigned ep) {
+        unsigned long long lo = 0, hi = 0;
+        for (unsigned spins = 0;; ++spins) {
+            lo = __hip_atomic_load(const_cast<unsigned long long*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi = __hip_atomic_load(const_cast<unsigned long long*>(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(lo >> 32) == ep && (unsigned)(hi >> 32) == ep) break;
+            if (spins > (1u << 24)) {
+                s_dead = 1;
+                __hip_atomic_store(L.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+    };
+    // scenario sum of V <= 16 values: workgroup sums -> one granule hop -> every workgroup adds the
+    // K partials in workgroup order from LDS (same bits everywhere)
+    auto scen_sum = [&](auto& v) {
+        constexpr int V = sizeof(v) / sizeof(double);
+        wg_sum<NT, V>(v, red);
+        if (K == 1) return;
+        const unsigned ep = ++ss_ep;
+        unsigned long long* g = GS + ((long)slot * 2 + (ep & 1u)) * K * 16 * 2;
+        if (t < V) gput(g + ((long)kw * 16 + t) * 2, ep, v[t]);
+        for (int u = t; u < V * K; u += NT) xtmp[u] = gget(g + ((long)(u / V) * 16 + u % V) * 2, ep);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            double acc = xtmp[u];
+            for (int q = 1; q < K; ++q) acc += xtmp[q * V + u];
+            v[u] = acc;
+        }
+        __syncthreads();
+        if (s_dead) alive = false;
+    };
+    // linking-row sums (thread l < NL holds workgroup kw's partial of row l): reduce-scatter then
+    // allgather, two granule hops -- workgroup l mod K owns row l, reads the K partials (one pair
+    // per thread), adds them in workgroup order and publishes the sum; every workgroup reads the NL
+    // sums.  Returns row t's sum (threads t < NL); the caller follows with settle().
+    auto exchange = [&](double v) {
+        if (K == 1) return v;
+        const unsigned ep = ++ex_ep;
+        unsigned long long* g1 = G1 + ((long)slot * 2 + (ep & 1u)) * NL * K * 2;
+        unsigned long long* g2 = G2 + ((long)slot * 2 + (ep & 1u)) * NL * 2;
+        if (t < NL) gput(g1 + ((long)t * K + kw) * 2, ep, v);
+        const int nown = (NL - kw + K - 1) / K;   // rows kw, kw + K, ...
+        for (int u = t; u < nown * K; u += NT) xtmp[u] = gget(g1 + ((long)(kw + K * (u / K)) * K + u % K) * 2, ep);
+        __syncthreads();
+        if (t < nown) {
+            double acc = xtmp[t * K];
+            for (int q = 1; q < K; ++q) acc += xtmp[t * K + q];
+            gput(g2 + (long)(kw + K * t) * 2, ep, acc);
+        }
+        return t < NL ? gget(g2 + (long)t * 2, ep) : 0.0;
+    };
+    auto settle = [&]() {   // after an exchange: one workgroup barrier, then the give-up flag
+        __syncthreads();
+        if (s_dead) alive = false;
+    };
+    auto ax_loc = [&](int q) {   // A x of local row q from Xl
+        double acc = 0.0;
+        for (int p = lrp[q]; p < lrp[q + 1]; ++p) acc = fma(lrv[p], Xl[lci[p]], acc);
+        return acc;
+    };
+    auto ax_link = [&]() {
+        double acc = 0.0;
+        if (t < NL)
+            for (int p = lkp[t]; p < lkp[t + 1]; ++p) acc = fma(lkv[p], Xl[lkc[p]], acc);
+        return acc;
+    };
+    auto aty_col = [&](const double* ylv, int q) {
+        double acc = 0.0;
+        for (int p = lcp[q]; p < lcp[q + 1]; ++p) {
+            const int r = lri[p];
+            // two LDS reads and a select (a select of the two pointers compiles to a flat load)
+            const double yloc = Yl[r >= 0 ? r : 0], ylnk = ylv[r >= 0 ? 0 : -r - 1];
+            acc = fma(lcv[p], r >= 0 ? yloc : ylnk, acc);
+        }
+        return acc;
+    };
+    bool vals_loaded = false;
+
+    while (true) {
+    if (kw == 0 && t == 0) {
+        const unsigned w = __hip_atomic_fetch_add(L.ctrl + kCtrlHead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_w = (int)w;
+        if (K > 1) __hip_atomic_store(mbox, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (K > 1) {
+        barrier();
+        if (kw != 0 && t == 0) s_w = (int)__hip_atomic_load(mbox, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int wi = s_w;
+    if (!alive || wi >= a.S) break;
+    const int s = a.order ? a.order[wi] : wi;
+    const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
+    if (L.vstride != 0 || !vals_loaded) {
+        const double* rvs = L.rvals + (long)s * L.vstride;
+        for (int q = t; q < G.nrz; q += NT) lrv[q] = rvs[B.rperm[G.rz0 + q]];
+        for (int q = t; q < G.nlz; q += NT) lkv[q] = rvs[B.lperm[G.lz0 + q]];
+        for (int q = t; q < G.ncz; q += NT) lcv[q] = rvs[B.cperm[G.cz0 + q]];
+        vals_loaded = true;
+    }
+    double* XR = L.xr + sn;          // restart points (owner-only, touched at restarts)
+    double* YR = L.yr + sm;
+
+    // ------------------------------------------------------------------ prologue
+    double x[E], xs[E], aty[E], cs[E], qs[E], ip[E], lo[E], hi[E];
+    double y[E], ys[E], axo[E], rlo[E], rhi[E];
+    double c2 = 0.0, prox_const = 0.0, cs2 = 0.0, b2 = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        x[e] = xs[e] = aty[e] = cs[e] = qs[e] = lo[e] = hi[e] = 0.0;
+        ip[e] = 1.0;
+        if (cv_[e]) {
+            const int j = jc[e];
+            const long b = sn + j;
+            const double d = a.dc[b];
+            double cc = a.c[b], qq = 0.0;
+            double lo_ = a.cl[b], hi_ = a.cu[b];
+            const int kk = a.lay.col_nonant[j];
+            if (kk >= 0) {
+                ph_terms(a, sN + kk, cc, qq, prox_const);
+                if (a.fix_nonants) fixed_box(a, sN + kk, d, lo_, hi_);
+            }
+            c2 += cc * cc;
+            cs[e] = cc * d;
+            cs2 += cs[e] * cs[e];
+            qs[e] = qq * d * d;
+            lo[e] = lo_;
+            hi[e] = hi_;
+            x[e] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
+            XR[j] = x[e];
+            Xl[t + e * NT] = x[e];
+        }
+        y[e] = ys[e] = axo[e] = rlo[e] = rhi[e] = 0.0;
+        if (rv_[e]) {
+            const int i = ir[e];
+            row_bounds(a, i, sm + i, rlo[e], rhi[e]);
+            double yy = (a.warm & 1) ? a.ys_in[sm + i] : 0.0;
+            if (!fin(rlo[e])) yy = fmin(yy, 0.0); else b2 += rlo[e] * rlo[e];
+            if (!fin(rhi[e])) yy = fmax(yy, 0.0); else b2 += rhi[e] * rhi[e];
+            y[e] = yy;
+            YR[i] = yy;
+            Yl[t + e * NT] = yy;
+        }
+    }
+    double l_lo = 0.0, l_hi = 0.0, l_y = 0.0, l_ys = 0.0, l_yr = 0.0, l_ax = 0.0, l_dr = 1.0;
+    int l_i = 0;
+    if (t < NL) {
+        l_i = B.link_rows[t];
+        row_bounds(a, l_i, sm + l_i, l_lo, l_hi);
+        l_dr = a.dr[sm + l_i];
+        double yy = (a.warm & 1) ? a.ys_in[sm + l_i] : 0.0;
+        if (!fin(l_lo)) yy = fmin(yy, 0.0); else if (kw == 0) b2 += l_lo * l_lo;
+        if (!fin(l_hi)) yy = fmax(yy, 0.0); else if (kw == 0) b2 += l_hi * l_hi;
+        l_y = l_yr = yy;
+        yl[t] = yy;
+    }
+    double omega, cnorm;
+    {
+        double rr[4] = {c2, prox_const, cs2, b2};
+        scen_sum(rr);
+        cnorm = sqrt(rr[0]);
+        prox_const = rr[1];
+        const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
+        omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
+        if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
+        else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);
+    }
+    const double bnorm = a.bnorm[s], eta = a.eta[s];
+    double tau = eta / omega, sig = eta * omega;
+    auto step_coefs = [&]() {
+#pragma unroll
+        for (int e = 0; e < E; ++e) ip[e] = 1.0 / (1.0 + tau * qs[e]);
+    };
+    step_coefs();
+    auto products = [&]() {   // A x, A^T y at the current point (Xl, Yl, yl current; after a barrier)
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (rv_[e]) axo[e] = ax_loc(t + e * NT);
+        l_ax = exchange(ax_link());
+        settle();
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (cv_[e]) aty[e] = aty_col(yl, t + e * NT);
+    };
+    products();
+
+    // KKT pieces (pdhg_stream.hip); avg: the products of the running sums staged through Xl / Yl
+    auto kkt_part = [&](bool avg, double inv, const double* axa, const double* ata, double l_axs, double* o) {
+        double v[6] = {0, 0, 0, 0, 0, 0};
+        auto row_terms = [&](double axx, double yy, double lo_, double hi_, double dr) {
+            const double pr = axx - clampd(axx, lo_, hi_);
+            v[0] += pr * pr;
+            const double pu = pr / dr;
+            v[2] += pu * pu;
+            if (fin(lo_)) v[5] += lo_ * fmax(yy, 0.0);
+            if (fin(hi_)) v[5] += hi_ * fmin(yy, 0.0);
+        };
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (rv_[e])
+                row_terms(avg ? axa[e] * inv : axo[e], avg ? ys[e] * inv : y[e], rlo[e], rhi[e], a.dr[sm + ir[e]]);
+        if (kw == 0 && t < NL) row_terms(avg ? l_axs * inv : l_ax, avg ? l_ys * inv : l_y, l_lo, l_hi, l_dr);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+            if (cv_[e]) {
+                const double xx = avg ? xs[e] * inv : x[e];
+                const double at = avg ? ata[e] * inv : aty[e];
+                const double rc_ = cs[e] + qs[e] * xx - at;
+                double dres = 0.0;
+                if (!fin(lo[e]) && rc_ > 0.0) dres += rc_;
+                if (!fin(hi[e]) && rc_ < 0.0) dres += rc_;
+                v[1] += dres * dres;
+                const double du = dres / a.dc[sn + jc[e]];
+                v[3] += du * du;
+                const double hq = 0.5 * qs[e] * xx * xx;
+                v[4] += cs[e] * xx + hq;
+                if (fin(lo[e])) v[5] += lo[e] * fmax(rc_, 0.0);
+                if (fin(hi[e])) v[5] += hi[e] * fmin(rc_, 0.0);
+                v[5] -= hq;
+            }
+#pragma unroll
+        for (int u = 0; u < 6; ++u) o[u] = v[u];
+    };
+    auto rel_of = [&](const double* o) {
+        const double p = sqrt(o[2]) / (1.0 + bnorm);
+        const double d = sqrt(o[3]) / (1.0 + cnorm);
+        const double g = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
+        return fmax(fmax(p, d), g);
+    };
+    auto wkkt_of = [&](const double* o, double w) {
+        const double g = o[4] - o[5];
+        return sqrt(w * w * o[0] + o[1] / (w * w) + g * g);
+    };
+    double kkt_restart, kkt_prev = INFINITY;
+    {
+        double o[6];
+        kkt_part(false, 0.0, nullptr, nullptr, 0.0, o);
+        scen_sum(o);
+        kkt_restart = wkkt_of(o, omega);
+    }
+    int it = 0, since = 0, cnt = 0, st = 1;
+    double rel_final = INFINITY, pobj = 0.0, dobj = 0.0;
+    bool use_avg_final = false;
+    const int chk = a.check_every;
+
+    while (alive) {
+        for (int kk = 0; kk < chk && alive; ++kk) {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if (cv_[e]) {
+                    const double xn = clampd(fma(tau, aty[e] - cs[e], x[e]) * ip[e], lo[e], hi[e]);
+                    x[e] = xn;
+                    xs[e] += xn;
+                    Xl[t + e * NT] = xn;
+                }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if (rv_[e]) {
+                    const double axn = ax_loc(t + e * NT);
+                    const double g = y[e] - sig * (2.0 * axn - axo[e]);
+                    const double yn = fmax(fma(sig, rlo[e], g), 0.0) + fmin(fma(sig, rhi[e], g), 0.0);
+                    axo[e] = axn;
+                    y[e] = yn;
+                    ys[e] += yn;
+                    Yl[t + e * NT] = yn;
+                }
+            const double axn_l = exchange(ax_link());   // the iteration's one cross-workgroup step
+            if (t < NL) {
+                const double g = l_y - sig * (2.0 * axn_l - l_ax);
+                l_y = fmax(fma(sig, l_lo, g), 0.0) + fmin(fma(sig, l_hi, g), 0.0);
+                l_ax = axn_l;
+                l_ys += l_y;
+                yl[t] = l_y;
+            }
+            settle();
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if (cv_[e]) aty[e] = aty_col(yl, t + e * NT);
+        }
+        if (!alive) break;
+        it += chk;
+        since += chk;
+        cnt += chk;
+
+        const double inv = 1.0 / (double)cnt;
+        // products at the average: stage the running sums in Xl / Yl / ylx, gather, restore
+        double axa[E], ata[E];
+        __syncthreads();   // every ATY gather of the last iteration is done with Yl
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (cv_[e]) Xl[t + e * NT] = xs[e];
+            if (rv_[e]) Yl[t + e * NT] = ys[e];
+        }
+        if (t < NL) ylx[t] = l_ys;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            axa[e] = rv_[e] ? ax_loc(t + e * NT) : 0.0;
+            ata[e] = cv_[e] ? aty_col(ylx, t + e * NT) : 0.0;
+        }
+        const double l_axs = exchange(ax_link());
+        settle();   // every gather of the staged sums is done
+        if (!alive) break;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (cv_[e]) Xl[t + e * NT] = x[e];
+            if (rv_[e]) Yl[t + e * NT] = y[e];
+        }
+        double oc[6], oa[6];
+        kkt_part(false, 0.0, nullptr, nullptr, 0.0, oc);
+        kkt_part(true, inv, axa, ata, l_axs, oa);
+        {
+            double both[12];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) { both[u] = oc[u]; both[6 + u] = oa[u]; }
+            scen_sum(both);   // (its workgroup barriers also publish the restored Xl / Yl)
+#pragma unroll
+            for (int u = 0; u < 6; ++u) { oc[u] = both[u]; oa[u] = both[6 + u]; }
+        }
+        const double rel_cur = rel_of(oc), rel_avg = rel_of(oa);
+        const bool nan = !(rel_cur == rel_cur);
+        if (nan || rel_cur <= a.eps || rel_avg <= a.eps || it >= a.max_iter) {
+            use_avg_final = !nan && rel_avg < rel_cur;
+            rel_final = use_avg_final ? rel_avg : rel_cur;
+            pobj = use_avg_final ? oa[4] : oc[4];
+            dobj = use_avg_final ? oa[5] : oc[5];
+            st = nan ? 2 : ((rel_cur <= a.eps || rel_avg <= a.eps) ? 0 : 1);
+            break;
+        }
+        const double k_cur = wkkt_of(oc, omega), k_avg = wkkt_of(oa, omega);
+        const bool use_avg = k_avg < k_cur;
+        const double cand = use_avg ? k_avg : k_cur;
+        const bool restart = (cand <= a.beta_suf * kkt_restart) ||
+                             (cand <= a.beta_nec * kkt_restart && cand > kkt_prev) ||
+                             ((double)since >= a.beta_art * (double)it);
+        kkt_prev = cand;
+        if (restart) {
+            double mv[2] = {0.0, 0.0};
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                if (cv_[e]) {
+                    const int j = jc[e];
+                    const double xv = use_avg ? xs[e] * inv : x[e];
+                    const double d = xv - XR[j];
+                    mv[0] += d * d;
+                    XR[j] = xv;
+                    x[e] = xv;
+                    xs[e] = 0.0;
+                    Xl[t + e * NT] = xv;
+                }
+                if (rv_[e]) {
+                    const int i = ir[e];
+                    const double yv = use_avg ? ys[e] * inv : y[e];
+                    const double d = yv - YR[i];
+                    mv[1] += d * d;
+                    YR[i] = yv;
+                    y[e] = yv;
+                    ys[e] = 0.0;
+                    Yl[t + e * NT] = yv;
+                }
+            }
+            if (t < NL) {
+                const double yv = use_avg ? l_ys * inv : l_y;
+                const double d = yv - l_yr;
+                if (kw == 0) mv[1] += d * d;
+                l_yr = l_y = yv;
+                l_ys = 0.0;
+                yl[t] = yv;
+            }
+            scen_sum(mv);
+            omega = primal_weight(omega, mv[0], mv[1], a.theta);
+            tau = eta / omega;
+            sig = eta * omega;
+            step_coefs();
+            cnt = 0;
+            since = 0;
+            kkt_restart = cand;
+            kkt_prev = INFINITY;
+            if (use_avg) products();
+        }
+    }
+    if (!alive) { st = 2; rel_final = NAN; }
+
+    // ------------------------------------------------------------------ outputs
+    const double inv = cnt > 0 ? 1.0 / (double)cnt : 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (cv_[e]) {
+            const int j = jc[e];
+            const long b = sn + j;
+            const double xv = use_avg_final ? xs[e] * inv : x[e];
+            a.xs[b] = xv;
+            const double xu = xv * a.dc[b];
+            if (a.x_out) a.x_out[b] = xu;
+            const int kk = a.lay.col_nonant[j];
+            if (kk >= 0) a.xN[sN + kk] = xu;
+        }
+        if (rv_[e]) {
+            const long b = sm + ir[e];
+            const double yv = use_avg_final ? ys[e] * inv : y[e];
+            a.ys[b] = yv;
+            if (a.y_out) a.y_out[b] = yv * a.dr[b];
+        }
+    }
+    if (kw == 0 && t < NL) {
+        const long b = sm + l_i;
+        const double yv = use_avg_final ? l_ys * inv : l_y;
+        a.ys[b] = yv;
+        if (a.y_out) a.y_out[b] = yv * a.dr[b];
+    }
+    if (kw == 0 && t == 0) {
+        const double offs = a.obj_off[s] + (a.prox_on ? prox_const : 0.0);
+        a.omega[s] = omega;
+        a.obj[s] = a.sense * (pobj + offs);
+        a.bound[s] = a.sense * (dobj + offs);
+        a.kkt[s] = rel_final;
+        a.iters[s] = it;
+        a.iters_acc[s] += it;
+        a.status[s] = st;
+    }
+    if (!alive) break;
+    __syncthreads();
+    }   // scenario queue
+}
+
 // ----------------------------------------------------------------------------- dispatch
 constexpr int kBorderNT = 1024;
 
+// granule words of the register variant: G1 [slots][2][NL][K][2], G2 [slots][2][NL][2], GS [slots][2][K][16][2]
+size_t pdhg_border_granule_words(const BorderLayout& B, const StreamLayout& L) {
+    return (size_t)L.slots * 2 * 2 * ((size_t)B.nlink * L.K + B.nlink + 16 * (size_t)L.K);
+}
+
 size_t pdhg_border_lds_bytes(const BorderLayout& B) {
+    if (B.reg)   // register-resident: x / y in LDS, no column / row lists
+        return (size_t)(B.nrz_max + B.nlz_max + B.ncz_max + B.C_max + B.R_max + 2 * B.nlink + B.xtmp_len) * sizeof(double) +
+               (size_t)(B.R_max + 1 + B.nrz_max + B.nlink + 1 + B.nlz_max + B.C_max + 1 + B.ncz_max) * sizeof(int);
     return (size_t)(B.nrz_max + B.nlz_max + B.ncz_max + 2 * B.nlink) * sizeof(double) +
            (size_t)(B.C_max + B.R_max + B.R_max + 1 + B.nrz_max + B.nlink + 1 + B.nlz_max + B.C_max + 1 + B.ncz_max) *
                sizeof(int);
 }
 
+// register-resident variant: 512-thread workgroups (launch bounds allow 256 VGPRs: the owned
+// elements' state stays in registers), E = 2 elements per thread; its LDS request is padded
+// past half a CU's 160 KB so that, like the 1024-thread kernels, it runs one workgroup per CU (the
+// hand-off protocol of stream_sync.h is measured for that)
+constexpr int kBorderRegNT = 512;
+constexpr size_t kOnePerCuLds = 82 * 1024;
+
+int pdhg_border_max_per_thread() { return 2 * kBorderRegNT; }   // elements per workgroup (E = 2: no spills)
+
 hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream) {
     const StreamLayout& L = a.st;
     hipError_t e = hipMemsetAsync(L.ctrl, 0, (size_t)(kCtrlBar + 3 * L.slots) * sizeof(unsigned), stream);
     if (e != hipSuccess) return e;
-    const dim3 grid((unsigned)L.slots * (unsigned)L.K), block(kBorderNT);
-    const size_t lds = pdhg_border_lds_bytes(a.bd);
+    if (a.bd.reg && L.K > 1) {   // tagged granules start from tag 0 every launch
+        e = hipMemsetAsync(a.bd.plink, 0, pdhg_border_granule_words(a.bd, L) * sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+    }
+    const dim3 grid((unsigned)L.slots * (unsigned)L.K), block(a.bd.reg ? kBorderRegNT : kBorderNT);
+    const size_t lds = a.bd.reg ? std::max(pdhg_border_lds_bytes(a.bd), kOnePerCuLds) : pdhg_border_lds_bytes(a.bd);
     PdhgArgs copy = a;
     void* args[] = {&copy};
-    const void* fn = (const void*)pdhg_border_kernel<kBorderNT>;
+    const void* fn = a.bd.reg ? (const void*)pdhg_border_reg_kernel<kBorderRegNT, 2>
+                              : (const void*)pdhg_border_kernel<kBorderNT>;
     if (L.K == 1) return hipLaunchKernel(fn, grid, block, args, lds, stream);
     return hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)lds, stream);
 }

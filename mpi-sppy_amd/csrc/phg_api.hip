@@ -38,6 +38,8 @@ hipError_t pdhg_stream_capacity(int* out);
 size_t pdhg_stream_lds_bytes(const StreamLayout& L);
 hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream);
 size_t pdhg_border_lds_bytes(const BorderLayout& B);
+int pdhg_border_max_per_thread();
+size_t pdhg_border_granule_words(const BorderLayout& B, const StreamLayout& L);
 int pdhg_mfma_num_variants();
 void pdhg_mfma_variant_shape(int v, int* out2);
 hipError_t pdhg_mfma_launch(int v, const PdhgArgs& a, hipStream_t stream);
@@ -977,6 +979,9 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
     for (long w : wt) total += w;
 
     BorderLayout& B = h->bd;
+    const size_t budget = 156 * 1024;
+    const char* eregs = std::getenv("PHG_BORDER_REG");   // 0: memory-resident variant only
+    const bool allow_reg = !(eregs && std::atoi(eregs) == 0);
     std::vector<int> gof(n), rgrp(m), linkidx(m, -1);
     std::vector<BorderGroup> groups;
     std::vector<int> link_rows;
@@ -1014,20 +1019,37 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
         B.nrz_max = *std::max_element(nrz.begin(), nrz.end());
         B.nlz_max = *std::max_element(nlz.begin(), nlz.end());
         B.ncz_max = *std::max_element(ncz.begin(), ncz.end());
-        return pdhg_border_lds_bytes(B);
+        // register-resident variant (at most 2 owned columns and 2 rows per thread of 512)
+        const int per = std::max(B.C_max, B.R_max);
+        B.reg = (allow_reg && per <= pdhg_border_max_per_thread()) ? 2 : 0;
+        B.xtmp_len = std::max(B.nlink + K, 16 * K);
+        size_t bytes = pdhg_border_lds_bytes(B);
+        if (B.reg && bytes > budget) {   // the memory-resident variant needs less LDS
+            B.reg = 0;
+            bytes = pdhg_border_lds_bytes(B);
+        }
+        return bytes;
     };
-    const size_t budget = 156 * 1024;
     long gmax = 0;
     int K = 0;
     if (const char* ek = std::getenv("PHG_STREAM_K")) {
         K = std::max(1, std::min(cap, std::atoi(ek)));
         if (plan(K, &gmax) > budget) return 1;
     } else {
-        for (int k = 1; k <= 16 && K == 0; ++k)
-            if (plan(k, &gmax) <= budget) K = k;
+        // smallest K with the register-resident variant (K <= 32), else the smallest K <= 16 that
+        // fits the memory-resident one; then more workgroups per scenario while that fills the
+        // chip better (few scenarios), keeping the variant
+        int K_any = 0;
+        for (int k = 1; k <= 32 && K == 0; ++k)
+            if (plan(k, &gmax) <= budget) {
+                if (!K_any && k <= 16) K_any = k;
+                if (B.reg) K = k;
+            }
+        if (K == 0) K = K_any;
         if (K == 0) return 1;
-        const int fill = std::min(16, cap / S);
-        if (fill > K && plan(fill, &gmax) <= budget) K = fill;
+        const bool reg_at_K = (plan(K, &gmax), B.reg != 0);
+        const int fill = std::min(reg_at_K ? 32 : 16, cap / S);
+        if (fill > K && plan(fill, &gmax) <= budget && (B.reg != 0) == reg_at_K) K = fill;
         else plan(K, &gmax);
     }
     // a dominant block leaves the other workgroups idle: not this layout's shape
@@ -1035,6 +1057,7 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
 
     // concatenated per-group arrays
     std::vector<int> col_list, row_list, rptr, rcol, rperm, lptr, lcol, lperm, cptr, crow, cperm;
+    std::vector<int> rcl, lcl, crl, lpos_col(n, -1), lpos_row(m, -1);
     groups.assign(K, BorderGroup{});
     for (int k = 0; k < K; ++k) {
         BorderGroup& G = groups[k];
@@ -1042,16 +1065,18 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
         for (int j = 0; j < n; ++j)
             if (gof[j] == k) col_list.push_back(j);
         G.nc = (int)col_list.size() - G.c0;
+        for (int q = 0; q < G.nc; ++q) lpos_col[col_list[G.c0 + q]] = q;
         G.r0 = (int)row_list.size();
         for (int i = 0; i < m; ++i)
             if (rgrp[i] == k) row_list.push_back(i);
         G.nr = (int)row_list.size() - G.r0;
+        for (int q = 0; q < G.nr; ++q) lpos_row[row_list[G.r0 + q]] = q;
         G.rp0 = (int)rptr.size();
         G.rz0 = (int)rcol.size();
         for (int q = 0; q < G.nr; ++q) {
             const int i = row_list[G.r0 + q];
             rptr.push_back((int)rcol.size() - G.rz0);
-            for (int p = rp[i]; p < rp[i + 1]; ++p) { rcol.push_back(ci[p]); rperm.push_back(p); }
+            for (int p = rp[i]; p < rp[i + 1]; ++p) { rcol.push_back(ci[p]); rcl.push_back(lpos_col[ci[p]]); rperm.push_back(p); }
         }
         rptr.push_back((int)rcol.size() - G.rz0);
         G.nrz = (int)rcol.size() - G.rz0;
@@ -1061,7 +1086,7 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
             const int i = link_rows[l];
             lptr.push_back((int)lcol.size() - G.lz0);
             for (int p = rp[i]; p < rp[i + 1]; ++p)
-                if (gof[ci[p]] == k) { lcol.push_back(ci[p]); lperm.push_back(p); }
+                if (gof[ci[p]] == k) { lcol.push_back(ci[p]); lcl.push_back(lpos_col[ci[p]]); lperm.push_back(p); }
         }
         lptr.push_back((int)lcol.size() - G.lz0);
         G.nlz = (int)lcol.size() - G.lz0;
@@ -1073,6 +1098,7 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
             for (int e = colptr[j]; e < colptr[j + 1]; ++e) {
                 const int r = csc_row[e];
                 crow.push_back(linkidx[r] >= 0 ? -(linkidx[r] + 1) : r);
+                crl.push_back(linkidx[r] >= 0 ? -(linkidx[r] + 1) : lpos_row[r]);
                 cperm.push_back(csc_p[e]);
             }
         }
@@ -1095,10 +1121,12 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
     if (put_ints(link_rows, &B.link_rows) || put_ints(col_list, &B.col_list) || put_ints(row_list, &B.row_list) ||
         put_ints(rptr, &B.rptr) || put_ints(rcol, &B.rcol) || put_ints(rperm, &B.rperm) ||
         put_ints(lptr, &B.lptr) || put_ints(lcol, &B.lcol) || put_ints(lperm, &B.lperm) ||
-        put_ints(cptr, &B.cptr) || put_ints(crow, &B.crow) || put_ints(cperm, &B.cperm))
+        put_ints(cptr, &B.cptr) || put_ints(crow, &B.crow) || put_ints(cperm, &B.cperm) ||
+        put_ints(rcl, &B.rcl) || put_ints(lcl, &B.lcl) || put_ints(crl, &B.crl))
         return -1;
     double* d;
-    if (dalloc(h, &d, (size_t)L.slots * 2 * K * std::max(1, B.nlink))) return -1;
+    // (register variant: 8-byte tagged granules, pdhg_border_granule_words)
+    if (dalloc(h, &d, std::max((size_t)L.slots * 2 * K * std::max(1, B.nlink), pdhg_border_granule_words(B, L)))) return -1;
     B.plink = d;
     const size_t Sn = (size_t)b->S * n, Sm = (size_t)b->S * m;
     if (dalloc(h, &d, Sn)) return -1; L.cs = d;
@@ -1570,7 +1598,7 @@ int phg_mfma_info(phg_handle* h, int32_t* o) {
 int phg_info(phg_handle* h, int32_t* o) {
     if (!h || !h->loaded) return fail("phg_info: no batch loaded");
     o[0] = h->S; o[1] = h->n; o[2] = h->m_orig; o[3] = h->nnz; o[4] = h->N; o[5] = h->N_tot;
-    if (h->stream_layout) { o[6] = (h->border_layout ? 500 : 400) + h->st.K; o[7] = 1024 * h->st.K; }
+    if (h->stream_layout) { o[6] = (h->border_layout ? (h->bd.reg ? 600 : 500) : 400) + h->st.K; o[7] = (h->bd.reg ? 512 : 1024) * h->st.K; }
     else if (h->mfma_variant >= 0) { o[6] = 300 + h->mfma_variant; o[7] = 4; }
     else if (h->local_variant >= 0) { o[6] = 100 + h->local_variant; o[7] = h->lshape[0]; }
     else if (h->block_variant >= 0) { o[6] = 200 + h->block_variant; o[7] = h->bshape[0]; }

@@ -113,7 +113,11 @@ struct BorderLayout {
     const int *rptr, *rcol, *rperm;  // local rows: CSR pointers, columns, positions in the CSR values
     const int *lptr, *lcol, *lperm;  // linking rows restricted to each group
     const int *cptr, *crow, *cperm;  // owned columns: CSC pointers, rows (-(l+1): linking row l), positions
-    double* plink;                   // [slots * 2 * K * nlink] double-buffered linking-row partials
+    const int *rcl, *lcl, *crl;      // the same indices as LOCAL positions in the group (register variant)
+    double* plink;                   // [slots * 2 * K * nlink * 2] double-buffered linking-row partials
+                                     // (register variant: tagged 8-byte granules, two per partial)
+    int reg;                         // 0: memory-resident kernel; E = 2: register-resident, E elements per thread
+    int xtmp_len;                    // register variant: LDS doubles staging cross-workgroup partials
 };
 
 constexpr int kCtrlHead = 0;     // StreamLayout::ctrl: queue head

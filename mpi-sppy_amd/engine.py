@@ -169,6 +169,8 @@ class Engine:
                        "local" if self.variant >= 100 else "gather")
         # multi-workgroup layouts (range-split stream 400 + K, bordered 500 + K): workgroups per scenario
         self.workgroups_per_scenario = self.variant % 100 if self.variant >= 400 else 1
+        # bordered layout: 600 + K the register-resident kernel, 500 + K the memory-resident one
+        self.border_reg = self.variant >= 600
         pi = np.zeros(2, np.int32)
         _lib.check(self.lib.phg_presolve_info(self.h, ptr(pi)))
         self.rows_folded, self.rows_kept = int(pi[0]), int(pi[1])
