@@ -27,6 +27,9 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 dense peak: the VALU rate (v_fma_f64, 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak
 
 
+DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_r02.json")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -63,7 +66,7 @@ def parse():
                     help="PDHG primal weight at each solve: fresh estimate, the previous solve's, or "
                          "their geometric mean (default)")
     ap.add_argument("--no-presolve", action="store_true", help="keep singleton rows as rows")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-json", default=DEFAULT_TRAFFIC)
     return ap.parse_args()
 
 
@@ -279,11 +282,14 @@ def main():
     bytes_it = 16 * nnz_distinct + 16 * b.n + 16 * m_run + 8 * (b.n * c_var + m_run * b_var)
     achieved_gbs = bytes_it * pdhg_iters / args.steps / avg_launch_s / 1e9
     traffic = None
-    if os.path.exists(args.traffic_json):
+    # PMC bytes per launch (tools/traffic_from_pmc.py): only for the case and kernel (layout) they
+    # were measured on; farmer: profiles/traffic_r02.json, other cases profiles/cases_r02/<case>_traffic.json
+    tpath = args.traffic_json if args.case == "farmer" or args.traffic_json != DEFAULT_TRAFFIC else \
+        os.path.join(ROOT, "profiles", "cases_r02", f"{args.case}_traffic.json")
+    if os.path.exists(tpath):
         try:
-            tj = json.load(open(args.traffic_json))
-            # PMC bytes only count for the kernel (layout) they were measured on
-            if tj.get("layout") == eng.layout and args.case == "farmer":
+            tj = json.load(open(tpath))
+            if tj.get("layout") == eng.layout and tj.get("case", "farmer") == args.case:
                 traffic = tj.get("pdhg_bytes_per_launch")
         except Exception:
             traffic = None

@@ -79,3 +79,42 @@ def test_wheel_hub_and_spokes_gap():
     assert ob <= ef + 1e-3 and ib >= ef - 1e-3, (ob, ib)
     assert (ib - ob) / abs(ob) <= 0.01 + 1e-9, (ob, ib)
     assert wheel.spcomm.opt._PHIter < 200
+
+
+def test_bounds_invalid_at_iteration_cap():
+    """An iteration-limited PDHG solve gives no bound (ADVICE: a dual iterate that has not reached
+    the KKT tolerance can overshoot): Iter0's trivial bound is -inf (farmer minimises) and the
+    Lagrangian spoke reports nothing, when the solves are capped at 64 PDHG iterations."""
+    cap = {"pdhg_max_iter": 64}
+    ph = _ph(3, 1, iter0_solver_options=cap, iterk_solver_options=cap, PHIterLimit=2)
+    ph.PH_Prep()
+    tb = ph.Iter0()
+    assert (ph.engine.get_i32(_lib.I_STATUS) == 1).all()
+    assert tb == -np.inf
+    sp = LagrangianOuterBound(ph)
+    sp.update()
+    assert sp.finalize() is None
+    sp.close()
+
+
+def test_spoke_copy_ordered_against_queued_hub_updates():
+    """The spoke's copy of the hub's W (phg_copy_from, on the spoke's stream) is ordered both ways
+    against the hub's stream: hub W updates queued right after the copy never tear it, so every
+    copy satisfies sum_s p_s W_s = 0 and equals one of the hub's W states (ADVICE: cross-stream
+    ordering).  10 000 scenarios x 30 nonants, so a torn copy would be likely if unordered."""
+    ph = _ph(10000, 10, PHIterLimit=2)
+    ph.ph_main(finalize=False)
+    sp = LagrangianOuterBound(ph)
+    p = ph.engine.batch.prob
+    for _ in range(4):
+        before = ph.engine.get(_lib.F_W)
+        sp.engine.copy_from(ph.engine, _lib.F_W)      # queued on the spoke's stream
+        ph.Compute_Xbar()                             # hub updates queued right behind it
+        ph.Update_W()
+        ph.engine.sync()
+        sp.engine.sync()
+        Wc = sp.engine.get(_lib.F_W)
+        assert np.array_equal(Wc, before)
+        Wc = Wc.reshape(len(p), -1)
+        assert np.abs(p @ Wc).max() <= 1e-9 * max(1.0, np.abs(Wc).max())
+    sp.close()

@@ -4,7 +4,7 @@ Per /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section): both count
 on gfx950 FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so it is doubled.
 The first dispatch of each kernel (PH iteration 0's cold solve / setup) is excluded.
 
-Usage: python tools/traffic_from_pmc.py FETCH_CSV WRITE_CSV LAYOUT OUT_JSON
+Usage: python tools/traffic_from_pmc.py FETCH_CSV WRITE_CSV LAYOUT OUT_JSON [CASE [BENCH_ARGS]]
 """
 import csv
 import json
@@ -26,11 +26,11 @@ def per_launch_kb(path, pattern, counter):
     return (sum(vals) / len(vals) if vals else None), len(vals), name
 
 
-def main(fetch_csv, write_csv, layout, out):
+def main(fetch_csv, write_csv, layout, out, case="farmer", args=""):
     pat = KERNELS[layout]
     f_kb, nf, name = per_launch_kb(fetch_csv, pat, "FETCH_SIZE")
     w_kb, nw, _ = per_launch_kb(write_csv, pat, "WRITE_SIZE")
-    res = {"layout": layout, "pdhg_kernel": name, "launches": [nf, nw],
+    res = {"case": case, "bench_args": args, "layout": layout, "pdhg_kernel": name, "launches": [nf, nw],
            "pdhg_fetch_kb_raw": f_kb, "pdhg_write_kb": w_kb,
            "pdhg_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024) if f_kb is not None else None}
     for k, p in AUX.items():
@@ -38,11 +38,11 @@ def main(fetch_csv, write_csv, layout, out):
         wk, _, _ = per_launch_kb(write_csv, p, "WRITE_SIZE")
         res[f"{k}_bytes_per_launch"] = int(2 * fk * 1024 + wk * 1024) if fk is not None and wk is not None else None
     res["method"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of "
-                     "the default `bench.py` workload (--steps 20 --warmup 5); KB units; FETCH doubled (gfx950 correction, "
+                     "the `bench.py` workload named by case / bench_args; KB units; FETCH doubled (gfx950 correction, "
                      "MI355X_MICROARCH.md); per PH-iteration launch, first dispatch excluded")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:7])
