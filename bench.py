@@ -352,14 +352,21 @@ def main():
                       "nnz_distinct": nnz_distinct, "tflops_fp64": round(achieved_tf, 4),
                       "valu_frac_fp64": round(achieved_tf / FP64_PEAK_TFLOPS, 5)}) | {
                      "traffic": traffic,
+                     # measured HBM rate of the same kernel: PMC bytes per launch / launch duration
+                     "hbm_measured_GBs": round(traffic / avg_launch_s / 1e9, 2) if traffic else None,
+                     "hbm_measured_frac": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5) if traffic else None,
                      "kernel": {"local": "pdhg_local_kernel (lane-local, fp64 VALU)",
                                 "gather": "pdhg_kernel (wave LDS-gather, fp64 VALU)",
                                 "block": "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)",
                                 "mfma": "pdhg_mfma_kernel (shared matrix, v_mfma_f64_16x16x4_f64, 16 scenarios per wave)",
                                 "stream": f"pdhg_stream_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
                                           "range split, iterates and values streamed)",
-                                "border": f"pdhg_border_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
-                                          "bordered block-diagonal, slices in LDS, linking rows exchanged)"}[eng.layout],
+                                "border": (f"pdhg_border_reg_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
+                                           "bordered block-diagonal, owned state in registers, x / y and slices in LDS, "
+                                           "linking rows as tagged-granule reduce-scatter + allgather)"
+                                           if eng.border_reg else
+                                           f"pdhg_border_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
+                                           "bordered block-diagonal, slices in LDS, linking rows exchanged)")}[eng.layout],
                      "flops_per_pdhg_iter_per_scen": f_it,
                      "pdhg_iters_per_scen_per_step": round(pdhg_iters / args.steps / S_loc, 2),
                      "max_pdhg_iters": max_iters,
@@ -477,6 +484,12 @@ def cpu_baseline(args, names, W, xbar):
     """The reference's CPU path restated (oracle): one QP solve per scenario, P processes (the CPU
     share of this job, _cpu_share), on the same W / xbar the GPU just used; bounded sample."""
     import multiprocessing as mp
+    if args.case == "uc":
+        # measured in the build container: HiGHS 1.8's QP solver returns "Unbounded" after 238 s on
+        # one UC prox-QP (the LP relaxation alone: 0.38 s), and the oracle's interior-point QP (dense
+        # normal equations, m ~ 2e4) does not finish in 15 min -- no CPU solver here completes a sample
+        return {"value": None, "kind": "port", "note": "no CPU QP solver in this image completes a UC "
+                "prox-QP (HiGHS 1.8 QP: Unbounded after 238 s; oracle IPM: > 15 min); DESIGN.md (d)"}
     try:
         P, visible, why = _cpu_share()
         per = max(1, len(names) // P)
