@@ -551,9 +551,16 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         // ---------------------------------------------------------- restart / termination check
         const double inv = 1.0 / (double)cnt;
         double oc[6], oa[6];
-        kkt_both(true, inv, oc, oa);
+        // the average iterate's KKT (products of the running sums: ~half the check) every
+        // avg_every-th check of the group -- uniform over the wave, the check's reductions are
+        // group-local but the products are wave-wide
+        const bool avg = wave_any(live && (a.avg_every <= 1 || ((it / chk) % a.avg_every) == 0));
+        kkt_both(avg, inv, oc, oa);
+        if (!avg)
+#pragma unroll
+            for (int u = 0; u < 6; ++u) oa[u] = u == 4 ? INFINITY : (u == 5 ? -INFINITY : INFINITY);
         const bool nan = !(oc[2] + oc[3] + oc[4] + oc[5] == oc[2] + oc[3] + oc[4] + oc[5]);
-        const bool ok_cur = converged(oc), ok_avg = converged(oa);
+        const bool ok_cur = converged(oc), ok_avg = avg && converged(oa);
         const bool term = live && (nan || ok_cur || ok_avg);
         const bool cap = live && !term && it >= a.max_iter;
         if (term || cap) {

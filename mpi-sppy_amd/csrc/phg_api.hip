@@ -127,6 +127,13 @@ struct phg_handle {
     int* order = nullptr;      // launch schedule (schedule.hip)
     unsigned* queue = nullptr; // work queue of the persistent lane-local kernel
     bool persist = false;      // PHG_LOCAL_PERSIST=1 selects the persistent work-queue grid (measured slower)
+    // PHG_AVG_EVERY: the lane-local kernel evaluates the average iterate at every avg_every-th
+    // check only (restarts / termination on the current iterate otherwise).  Farmer 10k A/B on the
+    // box: 1 -> 26.7 M solves/s (272.7 PDHG iterations per solve), 3 -> 27.4 M, 6 -> 27.9 M
+    // (283.6), never -> 28.1 M (283.2): the average's products are ~half of a check's work, and on
+    // these warm-started prox-QPs the current iterate restarts about as well.  6 keeps the average
+    // in reach of long (cold, LP) solves.
+    int avg_every = 6;
     bool have_order = false;
     double* pinned = nullptr;  // page-locked readback buffer (convergence partials)
     int summary[2] = {0, 0};   // scenarios not optimal / NaN, as of the last phg_conv_finish
@@ -233,6 +240,7 @@ int phg_create(int device, phg_handle** out) {
     phg_handle* h = new phg_handle();
     h->device = device;
     if (const char* ev = std::getenv("PHG_LOCAL_PERSIST")) h->persist = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("PHG_AVG_EVERY")) h->avg_every = std::max(1, std::atoi(ev));
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return fail("phg_create: hipStreamCreate failed");
@@ -1720,6 +1728,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.gate = o->skip_if_conv_below > 0 ? h->gate : nullptr;
     a.gate_below = o->skip_if_conv_below;
     a.queue = h->persist ? h->queue : nullptr;
+    a.avg_every = h->avg_every;
     a.bd = h->bd;
     if (h->border_layout) CK(pdhg_border_launch(a, h->stream));
     else if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));

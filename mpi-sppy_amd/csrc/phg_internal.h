@@ -186,6 +186,7 @@ struct PdhgArgs {
     // work queue of the persistent lane-local kernel ([0] next item, [1] waves done; both 0
     // between launches), or nullptr: one work item per lane group
     unsigned* queue;
+    int avg_every;          // lane-local kernel: the average iterate's KKT at every avg_every-th check (1: all)
 };
 
 struct PrepArgs {
