@@ -132,11 +132,70 @@ __device__ __forceinline__ void finish_k(unsigned* counter, unsigned* done, int 
 // every node's segment partials in segment order (element range split K ways):
 // nodesum[e] = sum p x, nodesum[N_tot + e] = sum p x^2 (the buffer the cross-GPU all-reduce sums).
 __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
-    __shared__ double sh[2 * 256];
+    __shared__ double sh[2 * 512];
     const int tid = threadIdx.x;
     const NodeSeg sg = a.seg[blockIdx.x];
     double* out = a.segpart + (long)blockIdx.x * 2 * a.maxk;
-    for (int k0 = 256 * (int)blockIdx.y; k0 < sg.klen; k0 += 256 * (int)gridDim.y) {
+    // element pairs with 16-byte loads when every row's slice starts 16-byte aligned (even N,
+    // offset and length) and the probability is per node: thread (k2, so) adds nonants 2 k2, 2 k2 + 1
+    // of rows s0 + so + j q2 (eight rows in flight), then the q2 row lanes are added in order
+    const bool pairs = (a.N % 2 == 0) && (sg.kofs % 2 == 0) && (sg.klen % 2 == 0) && !a.pcv;
+    for (int k0 = 256 * (int)blockIdx.y; pairs && k0 < sg.klen; k0 += 256 * (int)gridDim.y) {
+        const int kl = min(256, sg.klen - k0), kl2 = kl / 2;
+        const int q2 = 256 / kl2;
+        const int k2 = tid % kl2, so = tid / kl2;
+        double s1a = 0.0, s1b = 0.0, s2a = 0.0, s2b = 0.0;
+        if (so < q2) {
+            const long kg = sg.kofs + k0 + 2 * k2;
+            auto ld = [&](int s) { return *reinterpret_cast<const double2*>(a.xN + (long)s * a.N + kg); };
+            auto pr = [&](int s) { return a.pc[(long)s * a.L + sg.level]; };
+            int s = sg.s0 + so;
+            constexpr int R = 8;
+            double ta[R], tb[R], ua[R], ub[R];
+#pragma unroll
+            for (int u = 0; u < R; ++u) ta[u] = tb[u] = ua[u] = ub[u] = 0.0;
+            for (; s + (R - 1) * q2 < sg.s1; s += R * q2) {
+                double2 xv[R];
+                double p[R];
+#pragma unroll
+                for (int u = 0; u < R; ++u) { xv[u] = ld(s + u * q2); p[u] = pr(s + u * q2); }
+#pragma unroll
+                for (int u = 0; u < R; ++u) {
+                    ta[u] += p[u] * xv[u].x;
+                    tb[u] += p[u] * xv[u].y;
+                    ua[u] += p[u] * xv[u].x * xv[u].x;
+                    ub[u] += p[u] * xv[u].y * xv[u].y;
+                }
+            }
+            for (; s < sg.s1; s += q2) {
+                const double2 xv = ld(s);
+                const double p = pr(s);
+                ta[0] += p * xv.x;
+                tb[0] += p * xv.y;
+                ua[0] += p * xv.x * xv.x;
+                ub[0] += p * xv.y * xv.y;
+            }
+            s1a = ((ta[0] + ta[1]) + (ta[2] + ta[3])) + ((ta[4] + ta[5]) + (ta[6] + ta[7]));
+            s1b = ((tb[0] + tb[1]) + (tb[2] + tb[3])) + ((tb[4] + tb[5]) + (tb[6] + tb[7]));
+            s2a = ((ua[0] + ua[1]) + (ua[2] + ua[3])) + ((ua[4] + ua[5]) + (ua[6] + ua[7]));
+            s2b = ((ub[0] + ub[1]) + (ub[2] + ub[3])) + ((ub[4] + ub[5]) + (ub[6] + ub[7]));
+        }
+        if (so < q2) {   // sh[so][k], k = 2 k2 + h
+            sh[so * kl + 2 * k2] = s1a;
+            sh[so * kl + 2 * k2 + 1] = s1b;
+            sh[512 + so * kl + 2 * k2] = s2a;
+            sh[512 + so * kl + 2 * k2 + 1] = s2b;
+        }
+        __syncthreads();
+        if (tid < kl) {
+            double t1 = 0.0, t2 = 0.0;
+            for (int j = 0; j < q2; ++j) { t1 += sh[j * kl + tid]; t2 += sh[512 + j * kl + tid]; }
+            publish(&out[k0 + tid], t1);
+            publish(&out[a.maxk + k0 + tid], t2);
+        }
+        __syncthreads();
+    }
+    for (int k0 = 256 * (int)blockIdx.y; !pairs && k0 < sg.klen; k0 += 256 * (int)gridDim.y) {
         const int kl = min(256, sg.klen - k0);
         const int q = 256 / kl;
         const int k = tid % kl;
@@ -171,11 +230,11 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
             s2 = ((t2[0] + t2[1]) + (t2[2] + t2[3])) + ((t2[4] + t2[5]) + (t2[6] + t2[7]));
         }
         sh[tid] = s1;
-        sh[256 + tid] = s2;
+        sh[512 + tid] = s2;
         __syncthreads();
         if (tid < kl) {
             double t1 = 0.0, t2 = 0.0;
-            for (int j = 0; j < q; ++j) { t1 += sh[j * kl + tid]; t2 += sh[256 + j * kl + tid]; }
+            for (int j = 0; j < q; ++j) { t1 += sh[j * kl + tid]; t2 += sh[512 + j * kl + tid]; }
             publish(&out[k0 + tid], t1);
             publish(&out[a.maxk + k0 + tid], t2);
         }
@@ -282,6 +341,57 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
     const int dk = ROOT_ONLY ? 256 % a.N : 0;
     int k = ROOT_ONLY ? (int)(e % a.N) : 0;
     auto adv = [&](int kk) { kk += dk; return kk >= a.N ? kk - a.N : kk; };
+    if (ROOT_ONLY && !a.smooth_on && !a.pcv) {
+        // two-stage fast path: 16-byte loads / stores of element PAIRS (hipMalloc'd arrays: pair
+        // (e, e + 1) is 16-byte aligned for even e), four pairs in flight per thread; an odd first
+        // or last element of the segment is done by thread 0
+        long b = e0;
+        if (b & 1) {
+            if (tid == 0) acc += upd(b, a.xN[b], nodesum[(int)(b % a.N)], a.W[b], a.rho[b]);
+            ++b;
+        }
+        const long npair = (e1 - b) >> 1;
+        if (((e1 - b) & 1) && tid == 0) {
+            const long l = e1 - 1;
+            acc += upd(l, a.xN[l], nodesum[(int)(l % a.N)], a.W[l], a.rho[l]);
+        }
+        const double2* X2 = reinterpret_cast<const double2*>(a.xN + b);
+        const double2* R2 = reinterpret_cast<const double2*>(a.rho + b);
+        double2* W2 = reinterpret_cast<double2*>(a.W + b);
+        const int N = a.N;
+        const int dk2 = 512 % N;   // k advance per 256-pair stride
+        int kp = (int)((b + 2L * tid) % N);
+        auto adv2 = [&](int kk) { kk += dk2; return kk >= N ? kk - N : kk; };
+        auto nxt = [&](int kk) { return kk + 1 == N ? 0 : kk + 1; };
+        long pp = tid;
+        for (; pp + 3 * 256 < npair; pp += 4 * 256) {
+            double2 xv[4], wv[4], rv[4];
+            double xb0[4], xb1[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                xv[u] = X2[pp + u * 256];
+                wv[u] = W2[pp + u * 256];
+                rv[u] = R2[pp + u * 256];
+                xb0[u] = nodesum[kp];
+                xb1[u] = nodesum[nxt(kp)];
+                kp = adv2(kp);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double d0 = xv[u].x - xb0[u], d1 = xv[u].y - xb1[u];
+                W2[pp + u * 256] = make_double2(fma(rv[u].x, d0, wv[u].x), fma(rv[u].y, d1, wv[u].y));
+                acc += fabs(d0) + fabs(d1);
+            }
+        }
+        for (; pp < npair; pp += 256) {
+            const double2 xv = X2[pp], wv = W2[pp], rv = R2[pp];
+            const double d0 = xv.x - nodesum[kp], d1 = xv.y - nodesum[nxt(kp)];
+            W2[pp] = make_double2(fma(rv.x, d0, wv.x), fma(rv.y, d1, wv.y));
+            acc += fabs(d0) + fabs(d1);
+            kp = adv2(kp);
+        }
+        e = e1;   // the generic loops below are skipped
+    }
     // four elements in flight per thread (all loads before the stores), then the remainder
     for (; e + 3 * 256 < e1; e += 4 * 256) {
         double xv[4], xb[4], w[4], r[4];
