@@ -232,14 +232,19 @@ def main():
     el = time.perf_counter() - t0
     pdhg_ms, n_solves, pdhg_iters = eng.timing(0)
     assert n_solves == args.steps, n_solves
-    # the W-update kernel (phg_ph_head) and node sums, timed separately (HIP events only on them)
-    # over extra iterations of the sequential statements
+    # the PH update timed separately (HIP events only on it) over extra iterations: on one GPU the
+    # step the timed loop ran (phg_ph_step: node sums + W update, one launch where fusable), on
+    # several the sequential statements (node sums, all-reduce, W update)
     W_saved = eng.get(_lib.F_W)
     eng.timing_reset(solves=False, updates=True)
+    upd_fused = False
     for _ in range(args.steps):
-        ph.Compute_Xbar()
-        ph.Update_W()
-        ph.convergence_diff()
+        if comm is None:
+            upd_fused = eng.ph_step(0.0, False)
+        else:
+            ph.Compute_Xbar()
+            ph.Update_W()
+            ph.convergence_diff()
     upd_ms, n_upd, _ = eng.timing(1)
     eng.timing_reset(solves=False, updates=False)
     eng.set(_lib.F_W, W_saved)
@@ -374,7 +379,8 @@ def main():
         "roofline_ph_update": {"bound": "hbm", "achieved": round(ph_gbs, 2), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(ph_gbs / HBM_PEAK_GBS, 5),
                                "bytes_per_launch": ph_bytes, "avg_ms": round(upd_ms / args.steps, 4),
-                               "kernels": "node sums + W update (two launches per PH iteration)"},
+                               "kernels": ("ph_step_kernel (node sums + W update, one launch)" if upd_fused
+                                           else "node sums + W update (two launches per PH iteration)")},
         "per_rank": per_rank,
         "host_and_exchange_ms_per_step": round(ms_per_step - max(per_rank["pdhg_ms_per_step"]), 4),
         "setup_s": round(t_setup, 3),

@@ -232,6 +232,12 @@ int  phg_ph_update(phg_handle* h, double* host_conv);
 int  phg_exchange_layout(phg_handle* h, int32_t* out3);
 int  phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t first);
 int  phg_solve_undo(phg_handle* h);
+/* One GPU (nothing to exchange): phg_node_sums + phg_ph_head on the handle's own buffer.  With
+ * PHG_FUSE=1 and a batch that allows it (two-stage tree, one virtual rank, no smoothing, no variable
+ * probability) as ONE launch (the node-sum pass, then the W update by the last workgroups, x
+ * streamed once; the same bits as the two launches) -- measured slower than the two launches on
+ * farmer 10k, so off by default.  out_fused (may be NULL) = 1 if the fused kernel ran.           */
+int  phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fused);
 
 /* smoothed PH (phbase.py:329-346, 641-760): while on, every prox-on solve adds
  * p/2 (x_k - z_k)^2 per nonant and phg_apply_xbar also does Update_z: z += beta (x - z)        */

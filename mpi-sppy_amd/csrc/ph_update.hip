@@ -131,7 +131,7 @@ __device__ __forceinline__ void finish_k(unsigned* counter, unsigned* done, int 
 // nonant) -> coalesced rows of xN, 8 rows in flight per thread.  The last K workgroups then add
 // every node's segment partials in segment order (element range split K ways):
 // nodesum[e] = sum p x, nodesum[N_tot + e] = sum p x^2 (the buffer the cross-GPU all-reduce sums).
-__global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
+__device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
     __shared__ double sh[2 * 512];
     const int tid = threadIdx.x;
     const NodeSeg sg = a.seg[blockIdx.x];
@@ -240,9 +240,14 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
         }
         __syncthreads();
     }
-    const int K = min(a.n_final, (int)(gridDim.x * gridDim.y));
-    const int rank = last_k_workgroups(a.ticket, K);
-    if (rank < 0) return;
+}
+
+// final node sums of elements [e_lo, e_hi) (rank `rank` of K): per node, its segments' partials in
+// segment order (written with the given store: plain, or sc1 when other workgroups of the same
+// launch read them)
+template <bool PUBLISH>
+__device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum, int rank, int K) {
+    const int tid = threadIdx.x;
     // elements [e_lo, e_hi) of this rank; T lanes per element (power of two <= 64), each summing
     // every T-th segment of the node, then a fixed xor-butterfly over the T lanes: wide enough to
     // hide the L2 latency when there are few elements per rank, one lane per element otherwise
@@ -274,10 +279,25 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
             t2 += __shfl_xor(t2, o, 64);
         }
         if (e < e_hi && sub == 0) {
-            nodesum[e] = t1;
-            nodesum[a.N_tot + e] = t2;
+            if (PUBLISH) {
+                publish(&nodesum[e], t1);
+                publish(&nodesum[a.N_tot + e], t2);
+                publish(&a.xbar[e], t1);
+                publish(&a.xsqbar[e], t2);
+            } else {
+                nodesum[e] = t1;
+                nodesum[a.N_tot + e] = t2;
+            }
         }
     }
+}
+
+__global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
+    node_sum_partials(a);
+    const int K = min(a.n_final, (int)(gridDim.x * gridDim.y));
+    const int rank = last_k_workgroups(a.ticket, K);
+    if (rank < 0) return;
+    node_sum_final<false>(a, nodesum, rank, K);
     finish_k(a.ticket, a.ticket + 2, K);
 }
 
@@ -312,20 +332,14 @@ __device__ __forceinline__ double block_sum_range(const double* v, int first, in
 // before the solve that followed it, so this update must not happen (phbase.py:1008-1010).  The
 // partials of THIS update then overwrite convpart (by the last workgroup, after every workgroup
 // has read the old ones).
-template <bool ROOT_ONLY, bool HEAD>
-__global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* nodesum, double* convpart,
-                                                       double head_thr, int first) {
+// W update of convergence segment b (see w_update_kernel): W += rho (x - x-bar), its sum |x - x-bar|
+// and the segment's status counts, published for the final reduction.  Ends with a workgroup barrier
+// (a workgroup may run several segments).
+template <bool ROOT_ONLY>
+__device__ __forceinline__ void w_update_segment(const PhArgs& a, int b, const double* nodesum) {
     __shared__ double red[4];
     __shared__ int bad[8];
-    const int b = blockIdx.x;
     const int tid = threadIdx.x;
-    if constexpr (HEAD) {
-        __shared__ double red256[256];
-        // first PH iteration: no update precedes it, whatever the buffer holds
-        const double conv = first ? INFINITY : conv_value_block(convpart, a.P, red256);
-        if (b == 0 && tid == 0) publish_gate(conv, convpart, a.P, a.gate, a.gate_host, a.gate_seq);
-        if (conv < head_thr) return;   // grid-uniform: no workgroup touches the tickets
-    }
     const int s0 = a.cseg_s0[b], s1 = a.cseg_s1[b];
     const long e0 = (long)s0 * a.N, e1 = (long)s1 * a.N;
     double acc = 0.0;
@@ -433,12 +447,15 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
         publish(&a.csegbad[2 * b], bad[0] + bad[1] + bad[2] + bad[3]);
         publish(&a.csegbad[2 * b + 1], bad[4] + bad[5] + bad[6] + bad[7]);
     }
-    if (b == 0)
-        for (int j = tid; j < a.N_tot; j += 256) {
-            a.xbar[j] = nodesum[j];
-            a.xsqbar[j] = nodesum[a.N_tot + j];
-        }
-    if (!last_workgroup(a.ticket + 1)) return;
+    __syncthreads();
+}
+
+// the last workgroup's part of convergence_diff: segment partials per virtual rank (fixed order)
+// into convpart[2v], convpart[2v+1] = (sum, count); the status counts; the flag
+__device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart) {
+    __shared__ double red[4];
+    __shared__ int bad[8];
+    const int tid = threadIdx.x;
     for (int v = 0; v < a.P; ++v) {
         const int g0 = a.vr_first[v], g1 = a.vr_first[v + 1];
         const double t = block_sum_range(a.csegpart, g0, g1, red);
@@ -449,7 +466,7 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
     }
     {
         int tb = 0, tn = 0;
-        for (int g = tid; g < (int)gridDim.x; g += 256) { tb += a.csegbad[2 * g]; tn += a.csegbad[2 * g + 1]; }
+        for (int g = tid; g < a.n_cseg; g += 256) { tb += a.csegbad[2 * g]; tn += a.csegbad[2 * g + 1]; }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             tb += __shfl_xor(tb, o, 64);
@@ -464,10 +481,101 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
             convpart[2 * a.P + 2] = 1.0;   // the partials are a W update's
         }
     }
+}
+
+template <bool ROOT_ONLY, bool HEAD>
+__global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* nodesum, double* convpart,
+                                                       double head_thr, int first) {
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    if constexpr (HEAD) {
+        __shared__ double red256[256];
+        // first PH iteration: no update precedes it, whatever the buffer holds
+        const double conv = first ? INFINITY : conv_value_block(convpart, a.P, red256);
+        if (b == 0 && tid == 0) publish_gate(conv, convpart, a.P, a.gate, a.gate_host, a.gate_seq);
+        if (conv < head_thr) return;   // grid-uniform: no workgroup touches the tickets
+    }
+    w_update_segment<ROOT_ONLY>(a, b, nodesum);
+    if (b == 0)
+        for (int j = tid; j < a.N_tot; j += 256) {
+            a.xbar[j] = nodesum[j];
+            a.xsqbar[j] = nodesum[a.N_tot + j];
+        }
+    if (!last_workgroup(a.ticket + 1)) return;
+    conv_partials_final(a, convpart);
     if (!HEAD && a.gate) {   // single GPU: nothing to all-reduce, finish convergence_diff here
         __syncthreads();
         conv_gate_block(convpart, a.P, a.gate, a.gate_host, a.gate_seq);
     }
+}
+
+// Single-GPU PH step (phg_ph_step): the pipelined head (phg_ph_head) and the node sums in ONE launch,
+// for batches where no cross-GPU exchange sits between them (one GPU) and the tree is two-stage with
+// one virtual rank, no smoothing and no variable probability (PhArgs::fusable).  Grid = the node-sum
+// grid.  Every workgroup first computes the previous update's conv from `packed` (the same tree, the
+// same bits as phg_ph_head / phg_conv_finish) and the whole grid returns if it is below head_thr;
+// workgroup 0 publishes it.  Then the node-sum partials (node_sums_kernel's pass over x); the LAST K
+// workgroups to arrive (every other has finished: they spin only on running workgroups) form the node
+// sums and x-bar of their element ranges, meet at a counter of the K, and each applies the W update
+// to a K-th of the convergence segments (w_update_segment, the same loops and partials as the
+// two-launch path: the same bits) -- x is read again from the caches, not from HBM at these sizes;
+// the last of the K reduces the segment partials (conv_partials_final) and re-arms the counters.  Replaces node sums + W update (phbase.py:32-112,
+// :301-326, the local half of :349-371): one launch, x streamed from HBM once.
+__global__ __launch_bounds__(256) void ph_step_kernel(PhArgs a, double* packed, double head_thr, int first) {
+    __shared__ double red256[256];
+    __shared__ int s_last;
+    double* nodesum = packed;
+    double* convpart = packed + 2 * (long)a.N_tot;
+    const int tid = threadIdx.x;
+    const double conv = first ? INFINITY : conv_value_block(convpart, a.P, red256);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) publish_gate(conv, convpart, a.P, a.gate, a.gate_host, a.gate_seq);
+    if (conv < head_thr) return;   // grid-uniform
+    node_sum_partials(a);
+    // K: enough workgroups for the W update (the node sums' own final reduction needs far fewer,
+    // PhArgs::n_final), still far below the resident capacity (the ranked ones spin)
+    const int K = min(min(128, a.n_cseg), (int)(gridDim.x * gridDim.y));
+    const int rank = last_k_workgroups(a.fticket, K);
+    if (rank < 0) return;
+    node_sum_final<true>(a, nodesum, rank, K);
+    // the K ranks meet: every node sum / x-bar published (sc1 stores, drained) before the W update
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __hip_atomic_fetch_add(a.fticket + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(a.fticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)K)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // W update of this rank's convergence segments, exactly as w_update_kernel's workgroups do
+    // them (same per-segment loops and partials, so the same bits as the two-launch path)
+    const int b0 = (int)((long)a.n_cseg * rank / K), b1 = (int)((long)a.n_cseg * (rank + 1) / K);
+    for (int b = b0; b < b1; ++b) w_update_segment<true>(a, b, nodesum);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.fticket + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == (unsigned)K - 1;
+        if (s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    conv_partials_final(a, convpart);
+    __syncthreads();
+    if (tid == 0) {   // every rank is past all three counters: re-arm them for the next launch
+        __hip_atomic_store(a.fticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.fticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.fticket + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+hipError_t ph_step_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st) {
+    hipLaunchKernelGGL(ph_step_kernel, dim3(a.n_seg, (a.maxk + 255) / 256), dim3(256), 0, st, a, packed, thr, first);
+    return hipGetLastError();
 }
 
 // per-scenario objective value with the current W / xbar / rho (pyo.value(objfct))

@@ -50,6 +50,7 @@ hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hi
 hipError_t unscale_launch(const double* sv, const double* d, long cnt, double* out, hipStream_t st);
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
 hipError_t ph_head_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st);
+hipError_t ph_step_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st);
 hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double* gate_host, double seq,
                             hipStream_t st);
 constexpr int kSchedEvery = 4;
@@ -134,6 +135,11 @@ struct phg_handle {
     // these warm-started prox-QPs the current iterate restarts about as well.  6 keeps the average
     // in reach of long (cold, LP) solves.
     int avg_every = 6;
+    // PHG_FUSE=1: phg_ph_step runs node sums + W update as ONE launch (ph_step_kernel) where the batch
+    // allows.  Off by default: on farmer 10k the fused launch took 23.7 us against 18.4 us for the two
+    // launches back to back (its last-K hand-offs cost more than the launch and the x re-read save),
+    // 0.364 vs 0.361 ms per PH iteration; same bits either way (test_pipelined_iteration_matches_sequential)
+    bool no_fuse = true;
     bool have_order = false;
     double* pinned = nullptr;  // page-locked readback buffer (convergence partials)
     int summary[2] = {0, 0};   // scenarios not optimal / NaN, as of the last phg_conv_finish
@@ -241,6 +247,7 @@ int phg_create(int device, phg_handle** out) {
     h->device = device;
     if (const char* ev = std::getenv("PHG_LOCAL_PERSIST")) h->persist = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("PHG_AVG_EVERY")) h->avg_every = std::max(1, std::atoi(ev));
+    if (const char* ev = std::getenv("PHG_FUSE")) h->no_fuse = std::atoi(ev) == 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return fail("phg_create: hipStreamCreate failed");
@@ -746,6 +753,8 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
         unsigned* t;
         if (dalloc(h, &t, 3)) return -1;
         a.ticket = t;
+        if (dalloc(h, &t, 4)) return -1;
+        a.fticket = t;
     }
     if (dput(h, &ip, vfirst.data(), vfirst.size())) return -1; a.vr_first = ip;
     if (dput(h, &ip, xidx.data(), xidx.size())) return -1; h->xidx = ip;
@@ -1780,6 +1789,27 @@ int phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t fi
     a.gate_seq = (double)(++h->gate_seq);
     if (timing_event(h, 1, 0)) return -1;
     CK(ph_head_launch(a, dev_packed ? dev_packed : h->packed, convthresh, first, h->stream));
+    if (timing_event(h, 1, 1)) return -1;
+    h->gate_fused = false;
+    return 0;
+}
+
+int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fused) {
+    if (!h || !h->loaded) return fail("phg_ph_step: no batch loaded");
+    const PhArgs& p = h->ph;
+    const bool fusable = p.root_only && p.P == 1 && !p.smooth_on && !p.pcv && !h->no_fuse;
+    if (out_fused) *out_fused = fusable ? 1 : 0;
+    if (!fusable) {
+        if (phg_node_sums(h, nullptr)) return -1;
+        return phg_ph_head(h, nullptr, convthresh, first);
+    }
+    CK(hipSetDevice(h->device));
+    PhArgs a = h->ph;
+    a.gate = h->gate;
+    a.gate_host = h->gate_host;
+    a.gate_seq = (double)(++h->gate_seq);
+    if (timing_event(h, 1, 0)) return -1;
+    CK(ph_step_launch(a, h->packed, convthresh, first, h->stream));
     if (timing_event(h, 1, 1)) return -1;
     h->gate_fused = false;
     return 0;

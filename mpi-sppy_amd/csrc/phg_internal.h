@@ -244,6 +244,7 @@ struct PhArgs {
     const double* beta;     // [S*N]
     int smooth_on;
     unsigned* ticket;       // [3] last-workgroup counters of the two kernels + node_sums' done count
+    unsigned* fticket;      // [4] counters of the fused single-GPU step (ph_step_kernel)
     int n_final;            // workgroups sharing node_sums' final reduction (last_k_workgroups)
     // single-GPU PH update: the last w_update workgroup also computes conv into gate (device, read
     // by predicated solves) and gate_host (pinned host memory, read after the handle's event)

@@ -255,6 +255,15 @@ class Engine:
         the exchanged partials; unless it is below ``convthresh``, xbar / W / this update's partials."""
         _lib.check(self.lib.phg_ph_head(self.h, self._ns_ptr(), float(convthresh), int(bool(first))))
 
+    def ph_step(self, convthresh, first):
+        """One GPU (no exchange): node sums + the gated W update of the pipelined iteration, fused into
+        one launch where the batch allows it (phg_ph_step).  Returns True if the fused kernel ran."""
+        if self.exchange is not None:
+            raise RuntimeError("ph_step is the single-GPU form: exchange the node sums with ph_head")
+        fused = np.zeros(1, np.int32)
+        _lib.check(self.lib.phg_ph_step(self.h, float(convthresh), int(bool(first)), ptr(fused)))
+        return bool(fused[0])
+
     def solve_undo(self):
         """Restore the solve state from before the last solve (phg_solve_undo)."""
         _lib.check(self.lib.phg_solve_undo(self.h))

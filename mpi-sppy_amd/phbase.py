@@ -297,10 +297,12 @@ class PHBase(SPBase):
         Returns conv_{k-1} (+inf when ``first``: no update precedes iteration 1)."""
         eng = self.engine
         thr = float(self.options["convthresh"])
-        eng.node_sums()
         if eng.exchange is not None:
+            eng.node_sums()
             self.mpicomm.allreduce_sum_(eng.exchange)
-        eng.ph_head(thr, first)
+            eng.ph_head(thr, first)
+        else:   # one GPU: node sums and the gated W update in one launch (phg_ph_step)
+            eng.ph_step(thr, first)
         self.solve_loop(solver_options=self.current_solver_options, gripe=verbose, verbose=verbose,
                         skip_below=thr if thr > 0 else 0.0)
         self._spec_pending = True

@@ -316,10 +316,14 @@ def test_singleton_row_presolve_same_solutions():
 
 
 # ----------------------------------------------------------------------------- pipelined PH loop
-def test_pipelined_iteration_matches_sequential():
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_pipelined_iteration_matches_sequential(fuse, monkeypatch):
     """PHBase.update_and_solve (solve enqueued gated on the device conv, phg_conv_start/wait) runs
     the same PH as the sequential Compute_Xbar / Update_W / convergence_diff / solve_loop loop,
-    including the break before solve_loop at conv < convthresh (the gated solve is a no-op)."""
+    including the break before solve_loop at conv < convthresh (the gated solve is a no-op); with
+    PHG_FUSE=1 the single-GPU step is the fused ph_step_kernel (node sums + W update in one launch),
+    bit-identical too."""
+    monkeypatch.setenv("PHG_FUSE", fuse)
     out = []
     for pipe in (True, False):
         ph = _farmer_ph(4, cm=1, PHIterLimit=200, convthresh=1e-3, pdhg_pipeline=pipe)
