@@ -43,7 +43,13 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
     for (int k = 0; k < K; ++k) v[k] = red[16 * NW + k];
 }
 
-template <int NT, int CPL, int RPL, int PPT, int QPT>
+// RE / CE > 0: every row (column) piece slot holds at most RE (CE) entries, and the thread's piece
+// values and LDS indices are loaded into registers once, in the prologue -- the matrix is constant
+// over the solve, so the iterations read only LDS (x, y, partials).  RE = CE = 0: values and
+// indices are re-read from memory every iteration (the streaming form, for pieces that do not fit
+// the register budget).  Both forms add the same products in the same order (padding entries are
+// fma(0, x[0], acc) = acc), so they return the same bits.
+template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -114,21 +120,59 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         }
     }
 
+    // ------------------------------------------------------------------ register-resident pieces
+    constexpr int RE1 = RE > 0 ? RE : 1, CE1 = CE > 0 ? CE : 1;
+    double rvr[RE > 0 ? PPT : 1][RE1], cvr[CE > 0 ? QPT : 1][CE1];
+    int rir[RE > 0 ? PPT : 1][RE1], cir[CE > 0 ? QPT : 1][CE1];
+    if constexpr (RE > 0) {
+        int off = 0;
+#pragma unroll
+        for (int ps = 0; ps < PPT; ++ps) {
+            const int kk = B.rk[ps];
+#pragma unroll
+            for (int k = 0; k < RE; ++k) {
+                const int e = off + k * NT + t;
+                rvr[ps][k] = k < kk ? rv[e] : 0.0;
+                rir[ps][k] = k < kk ? B.ridx[e] : 0;
+            }
+            off += kk * NT;
+        }
+    }
+    if constexpr (CE > 0) {
+        int off = 0;
+#pragma unroll
+        for (int ps = 0; ps < QPT; ++ps) {
+            const int kk = B.ck[ps];
+#pragma unroll
+            for (int k = 0; k < CE; ++k) {
+                const int e = off + k * NT + t;
+                cvr[ps][k] = k < kk ? cv[e] : 0.0;
+                cir[ps][k] = k < kk ? B.cidx[e] : 0;
+            }
+            off += kk * NT;
+        }
+    }
+
     // ------------------------------------------------------------------ SpMVs through LDS
     // A x for the x currently in xl: pieces -> rp, barrier, row owners add their pieces
     auto spmv_ax = [&](double (&out)[RPL]) {
         int off = 0;
 #pragma unroll
         for (int ps = 0; ps < PPT; ++ps) {
-            const int kk = B.rk[ps];
             double acc = 0.0;
+            if constexpr (RE > 0) {
+#pragma unroll
+                for (int k = 0; k < RE; ++k) acc = fma(rvr[ps][k], xl[rir[ps][k]], acc);
+            } else {
+                const int kk = B.rk[ps];
 #pragma unroll 2
-            for (int k = 0; k < kk; ++k) {
-                const int e = off + k * NT + t;
-                acc = fma(rv[e], xl[B.ridx[e]], acc);
+                for (int k = 0; k < kk; ++k) {
+                    const int e = off + k * NT + t;
+                    acc = fma(rv[e], xl[B.ridx[e]], acc);
+                }
+                off += kk * NT;
             }
             rp[ps * NT + t] = acc;
-            off += kk * NT;
         }
         __syncthreads();
 #pragma unroll
@@ -144,15 +188,20 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         int off = 0;
 #pragma unroll
         for (int ps = 0; ps < QPT; ++ps) {
-            const int kk = B.ck[ps];
             double acc = 0.0;
+            if constexpr (CE > 0) {
+#pragma unroll
+                for (int k = 0; k < CE; ++k) acc = fma(cvr[ps][k], yl[cir[ps][k]], acc);
+            } else {
+                const int kk = B.ck[ps];
 #pragma unroll 2
-            for (int k = 0; k < kk; ++k) {
-                const int e = off + k * NT + t;
-                acc = fma(cv[e], yl[B.cidx[e]], acc);
+                for (int k = 0; k < kk; ++k) {
+                    const int e = off + k * NT + t;
+                    acc = fma(cv[e], yl[B.cidx[e]], acc);
+                }
+                off += kk * NT;
             }
             cp[ps * NT + t] = acc;
-            off += kk * NT;
         }
         __syncthreads();
 #pragma unroll
@@ -413,13 +462,15 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 
 // ----------------------------------------------------------------------------- dispatch
 struct BlockVariant {
-    int NT, CPL, RPL, PPT, QPT;
+    int NT, CPL, RPL, PPT, QPT, RE, CE;
     void (*fn)(PdhgArgs);
 };
 
-#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, pdhg_block_kernel<a_, b_, c_, d_, e_>}
+#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0>}
+#define PHG_BR(a_, b_, c_, d_, e_, f_, g_) {a_, b_, c_, d_, e_, f_, g_, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
+    PHG_BR(256, 3, 1, 2, 3, 8, 2),   // sslp-like with register-resident pieces (columns in <= 2 rows)
     PHG_B(256, 3, 1, 2, 3),      // sslp-like: n <= 768, m <= 256
     PHG_B(256, 4, 4, 4, 4),      // n, m, pieces <= 1024
     PHG_B(512, 4, 4, 4, 4),      // <= 2048
@@ -427,12 +478,13 @@ static const BlockVariant kBlockVariants[] = {
     PHG_B(1024, 4, 4, 4, 4),     // <= 4096
 };
 #undef PHG_B
+#undef PHG_BR
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
 
-void pdhg_block_variant_shape(int v, int* out5) {
+void pdhg_block_variant_shape(int v, int* out7) {
     const BlockVariant& V = kBlockVariants[v];
-    out5[0] = V.NT; out5[1] = V.CPL; out5[2] = V.RPL; out5[3] = V.PPT; out5[4] = V.QPT;
+    out7[0] = V.NT; out7[1] = V.CPL; out7[2] = V.RPL; out7[3] = V.PPT; out7[4] = V.QPT; out7[5] = V.RE; out7[6] = V.CE;
 }
 
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad) {

@@ -152,3 +152,29 @@ def test_uc_fullsize_stream_vs_oracle(S, layout):
     assert abs(tb - otb) <= 1e-5 * abs(otb), (tb, otb)
     np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-5)
     np.testing.assert_allclose(ph.engine.get(_lib.F_BOUND), o.outer, rtol=1e-5)
+
+
+def test_block_register_pieces_same_bits(monkeypatch):
+    """sslp's pieces fit the registers (row pieces <= 8, columns in <= 2 rows), so AUTO runs the
+    block kernel with the matrix held in registers for the whole solve; PHG_BLOCK_STREAM=1 forces
+    the form that re-reads values / indices every iteration.  Same products in the same order:
+    Iter0 and one prox-QP solve give bit-identical objectives, iteration counts and nonants."""
+    S = 8
+    o = oph.OraclePH(_opts(), om.sslp_names(S), om.sslp, {})
+    o.Iter0()
+    o.Compute_Xbar()
+    o.Update_W()
+    res = []
+    for stream in ("0", "1"):
+        monkeypatch.setenv("PHG_BLOCK_STREAM", stream)
+        ph = PH(_opts(), sslp.scenario_names_creator(S), sslp.scenario_creator)
+        ph.PH_Prep()
+        assert ph.engine.layout == "block"
+        ph.Iter0()
+        ob0 = ph.engine.get(_lib.F_OBJ).copy()
+        ph.engine.set(_lib.F_W, o.W.ravel())
+        ph.engine.set(_lib.F_XBAR, o.xbar[0])
+        ph.solve_loop()
+        res.append((ob0, ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get_i32(_lib.I_ITERS).copy(), ph.nonants()))
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
