@@ -43,6 +43,15 @@ __device__ __forceinline__ void block_sum(double (&v)[K], double* red) {
     for (int k = 0; k < K; ++k) v[k] = red[16 * NW + k];
 }
 
+// sum of a row's (column's) cnt piece partials, left to right (the owner's fixed order).  (Issuing
+// the loads four at a time with predicated tails measured slower on sslp: 12.0 -> 15.2 ms.)
+__device__ __forceinline__ double piece_sum(const double* p, int cnt) {
+    double acc = 0.0;
+#pragma unroll 1
+    for (int u = 0; u < cnt; ++u) acc += p[u];
+    return acc;
+}
+
 // RE / CE > 0: every row (column) piece slot holds at most RE (CE) entries, and the thread's piece
 // values and LDS indices are loaded into registers once, in the prologue -- the matrix is constant
 // over the solve, so the iterations read only LDS (x, y, partials).  RE = CE = 0: values and
@@ -176,12 +185,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < RPL; ++r) {
-            double acc = 0.0;
-#pragma unroll 1
-            for (int u = 0; u < rn[r]; ++u) acc += rp[rf[r] + u];
-            out[r] = acc;
-        }
+        for (int r = 0; r < RPL; ++r) out[r] = piece_sum(rp + rf[r], rn[r]);
     };
     // A^T y for the y currently in yl
     auto spmv_aty = [&](double (&out)[CPL]) {
@@ -205,12 +209,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-            double acc = 0.0;
-#pragma unroll 1
-            for (int u = 0; u < cn[k]; ++u) acc += cp[cf[k] + u];
-            out[k] = acc;
-        }
+        for (int k = 0; k < CPL; ++k) out[k] = piece_sum(cp + cf[k], cn[k]);
     };
     auto put_x = [&](const double (&v)[CPL]) {
 #pragma unroll
@@ -346,7 +345,15 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         const double inv = 1.0 / (double)cnt;
         double oc[6], oa[6];
         kkt(x, aty, y, ax, oc);
-        {
+        // the average iterate at every check: on these LP relaxations (sslp, netdes) evaluating
+        // it at every 3rd / 6th check only (as the lane-local kernel does) measured 1.3-2.6x the
+        // PDHG iterations and 1.4-8x the time per launch
+        constexpr bool avg = true;
+        if (!avg) {
+            oa[0] = oa[1] = oa[2] = oa[3] = INFINITY;
+            oa[4] = INFINITY;
+            oa[5] = -INFINITY;
+        } else {
             double xa[CPL], ya[RPL], ata[CPL], axa[RPL];
 #pragma unroll
             for (int k = 0; k < CPL; ++k) xa[k] = xsum[k] * inv;
@@ -360,7 +367,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             spmv_aty(ata);
             kkt(xa, ata, ya, axa, oa);
         }
-        const double rel_cur = rel_of(oc), rel_avg = rel_of(oa);
+        const double rel_cur = rel_of(oc), rel_avg = avg ? rel_of(oa) : INFINITY;
         const bool nan = !(rel_cur == rel_cur);
         if (nan || rel_cur <= a.eps || rel_avg <= a.eps || it >= a.max_iter) {
             use_avg_final = !nan && rel_avg < rel_cur;
@@ -370,7 +377,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             st = nan ? 2 : ((rel_cur <= a.eps || rel_avg <= a.eps) ? 0 : 1);
             break;
         }
-        const double k_cur = wkkt_of(oc, omega), k_avg = wkkt_of(oa, omega);
+        const double k_cur = wkkt_of(oc, omega), k_avg = avg ? wkkt_of(oa, omega) : INFINITY;
         const bool use_avg = k_avg < k_cur;
         const double cand = use_avg ? k_avg : k_cur;
         const bool restart = (cand <= a.beta_suf * kkt_restart) ||
@@ -422,7 +429,10 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             kkt_restart = cand;
             kkt_prev = INFINITY;
         }
-        products();   // exact A x, A^T y at the current point (xl/yl held the average)
+        // A x, A^T y at a new point (restart to the average); otherwise the registers still hold
+        // the products of the current point (what a recomputation would return, bit for bit)
+        if (restart && use_avg) products();
+        else __syncthreads();
     }
 
     // ------------------------------------------------------------------ outputs
