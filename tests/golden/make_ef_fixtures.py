@@ -198,14 +198,68 @@ def separable_fixture(sizes, cm=10):
         print(fn, obj, out.get("rel_diff_vs_lp_ef"), flush=True)
 
 
-def oracle_ph(S=30, cm=10, thr=1e-4, max_iter=5000):
+_POOL_ARR = None
+
+
+def _pool_solve(args):
+    """One scenario QP in a worker (the oracle's highs.solve on the forked scenario arrays)."""
+    from oracle import highs
+    k, c, q, off, threads = args
+    a = _POOL_ARR[k]
+    r = highs.solve(c, a["rowptr"], a["colidx"], a["vals"], a["row_lo"], a["row_hi"], a["col_lo"], a["col_hi"],
+                    qdiag=q, offset=off, threads=threads)
+    return k, bool(r.ok), str(r.status), r.x, r.obj
+
+
+def oracle_ph(S=30, cm=10, thr=1e-4, max_iter=20000, procs=8):
     """The oracle's own PH to convergence on the same instance (``oracle/ph.py``, HiGHS subproblem
-    solves certified by KKT checks): ``oracle_ph_farmer_cm{cm}_S{S}.json``."""
+    solves certified by KKT checks): ``oracle_ph_farmer_cm{cm}_S{S}.json``.  The scenario solves
+    of each PH iteration go to a process pool (the oracle's solve_one, split into building the
+    objective here and the HiGHS call in a worker; same results, ~procs x faster)."""
+    import multiprocessing as mp
     from oracle import ph as oph
+
+    class PoolPH(oph.OraclePH):
+        def solve_loop(self):
+            jobs = []
+            for k in range(self.S):
+                a = self.arr[k]
+                sg = 1.0 if self.scen[k].sense == 1 else -1.0
+                c = sg * a["c"].copy()
+                q = None
+                off = 0.0
+                cols = self.cols[k]
+                if self.W_on:
+                    np.add.at(c, cols, self.W[k])
+                if self.prox_on:
+                    rho = self.rho[k]
+                    xb = self.xbar[k]
+                    np.add.at(c, cols, -rho * xb)
+                    q = np.zeros_like(c)
+                    np.add.at(q, cols, rho)
+                    off = float(np.sum(rho / 2.0 * xb * xb))
+                jobs.append((k, c, q, off, self.threads))
+            for k, ok, st, x, obj in pool.map(_pool_solve, jobs):
+                if not ok:
+                    raise RuntimeError(f"[oracle] Solve failed for scenario {self.names[k]}: {st}")
+                sg = 1.0 if self.scen[k].sense == 1 else -1.0
+                self.feasible[k] = True
+                self.x[k] = x
+                self.obj[k] = sg * obj
+                self.outer[k] = sg * obj
+            self.solve_count += self.S
+            if self._PHIter % 100 == 0:
+                print(f"PH iter {self._PHIter} conv {self.conv}", flush=True)
+
+    global _POOL_ARR
     opts = {"defaultPHrho": 1.0, "PHIterLimit": max_iter, "convthresh": thr}
     t0 = time.perf_counter()
-    o = oph.OraclePH(opts, om.farmer_names(S), om.farmer, dict(crops_multiplier=cm, num_scens=S))
+    o = PoolPH(opts, om.farmer_names(S), om.farmer, dict(crops_multiplier=cm, num_scens=S))
+    _POOL_ARR = o.arr
+    o._PHIter = 0
+    pool = mp.get_context("fork").Pool(procs)
     conv, eobj, tb = o.ph_main()
+    pool.close()
     out = {"instance": f"farmer crops_multiplier={cm}, scen0..scen{S - 1}, rho=1, convthresh={thr}",
            "S": S, "cm": cm, "conv": conv, "ph_iters": o._PHIter, "Eobj": eobj, "trivial_bound": tb,
            "xbar": list(map(float, o.xbar[0])), "seconds": round(time.perf_counter() - t0, 1)}

@@ -101,7 +101,10 @@ def main():
     import torch
     torch.cuda.set_device(0)
     out = []
-    for S, N in ((10000, 100), (100000, 100), (100000, 1000)):
+    cases = ((10000, 100), (100000, 100), (100000, 1000))
+    if os.environ.get("SWEEP_CASES"):   # e.g. "100000x1000,10000x100"
+        cases = tuple(tuple(int(v) for v in c.split("x")) for c in os.environ["SWEEP_CASES"].split(","))
+    for S, N in cases:
         r = run(S, N)
         print(json.dumps(r), flush=True)
         out.append(r)
