@@ -58,8 +58,13 @@ __device__ __forceinline__ double piece_sum(const double* p, int cnt) {
 // indices are re-read from memory every iteration (the streaming form, for pieces that do not fit
 // the register budget).  Both forms add the same products in the same order (padding entries are
 // fma(0, x[0], acc) = acc), so they return the same bits.
-template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE>
+//
+// CL (with CE > 0): every column is ONE piece, held by the thread and slot that own the column
+// (QPT == CPL; checked on the host) -- so A^T y needs no partials in LDS and no workgroup barrier:
+// three barriers per PDHG iteration instead of four (sslp: every column has <= 2 entries).
+template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
+    static_assert(!CL || (CE > 0 && QPT == CPL), "column-local A^T y needs register pieces, one per column slot");
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const BlockLayout& B = a.blk;
@@ -205,11 +210,14 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
                 }
                 off += kk * NT;
             }
-            cp[ps * NT + t] = acc;
+            if constexpr (CL) out[ps] = 0.0 + acc;   // (the same bits as a one-piece piece_sum)
+            else cp[ps * NT + t] = acc;
         }
-        __syncthreads();
+        if constexpr (!CL) {
+            __syncthreads();
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) out[k] = piece_sum(cp + cf[k], cn[k]);
+            for (int k = 0; k < CPL; ++k) out[k] = piece_sum(cp + cf[k], cn[k]);
+        }
     };
     auto put_x = [&](const double (&v)[CPL]) {
 #pragma unroll
@@ -472,15 +480,16 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 
 // ----------------------------------------------------------------------------- dispatch
 struct BlockVariant {
-    int NT, CPL, RPL, PPT, QPT, RE, CE;
+    int NT, CPL, RPL, PPT, QPT, RE, CE, CL;
     void (*fn)(PdhgArgs);
 };
 
-#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0>}
-#define PHG_BR(a_, b_, c_, d_, e_, f_, g_) {a_, b_, c_, d_, e_, f_, g_, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_>}
+#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false>}
+#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
-    PHG_BR(256, 3, 1, 2, 3, 8, 2),   // sslp-like with register-resident pieces (columns in <= 2 rows)
+    PHG_BR(256, 3, 1, 2, 3, 8, 2, true),    // sslp-like: register-resident pieces, column-local A^T y
+    PHG_BR(256, 3, 1, 2, 3, 8, 2, false),   // the same with A^T y through LDS partials
     PHG_B(256, 3, 1, 2, 3),      // sslp-like: n <= 768, m <= 256
     PHG_B(256, 4, 4, 4, 4),      // n, m, pieces <= 1024
     PHG_B(512, 4, 4, 4, 4),      // <= 2048
@@ -492,9 +501,10 @@ static const BlockVariant kBlockVariants[] = {
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
 
-void pdhg_block_variant_shape(int v, int* out7) {
+void pdhg_block_variant_shape(int v, int* out8) {
     const BlockVariant& V = kBlockVariants[v];
-    out7[0] = V.NT; out7[1] = V.CPL; out7[2] = V.RPL; out7[3] = V.PPT; out7[4] = V.QPT; out7[5] = V.RE; out7[6] = V.CE;
+    out8[0] = V.NT; out8[1] = V.CPL; out8[2] = V.RPL; out8[3] = V.PPT; out8[4] = V.QPT; out8[5] = V.RE; out8[6] = V.CE;
+    out8[7] = V.CL;
 }
 
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad) {

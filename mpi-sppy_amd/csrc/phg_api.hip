@@ -30,7 +30,7 @@ int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc);
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_block_num_variants();
-void pdhg_block_variant_shape(int v, int* out7);
+void pdhg_block_variant_shape(int v, int* out8);
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad);
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream);
@@ -97,7 +97,7 @@ struct phg_handle {
     std::vector<int> stream_cperm;   // CSC entry -> CSR position (values gathered after prep)
     int mshape[2] = {0, 0};
     MfmaLayout mf{};
-    int bshape[7] = {0};
+    int bshape[8] = {0};
     std::vector<int> block_rperm, block_cperm;   // piece layout -> CSR position (host copies)
     bool vals_shared = false;
     int layout_policy = PHG_LAYOUT_AUTO;
@@ -801,12 +801,19 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     // PHG_BLOCK_STREAM=1: skip the register-resident variants (A/B of the two forms)
     const char* es = std::getenv("PHG_BLOCK_STREAM");
     const bool stream_only = es && std::atoi(es) != 0;
-    int sh[7], chosen = -1;
+    // every column one piece (then piece j is column j, in the column owner's thread and slot)
+    bool col_one_piece = true;
+    for (int j = 0; j < n && col_one_piece; ++j) col_one_piece = cpf[j] == j && cpc[j] == 1;
+    // PHG_BLOCK_CL=0: skip the column-local variants (A/B)
+    const char* ec = std::getenv("PHG_BLOCK_CL");
+    const bool cl_off = ec && std::atoi(ec) == 0;
+    int sh[8], chosen = -1;
     for (int v = 0; v < pdhg_block_num_variants(); ++v) {
         pdhg_block_variant_shape(v, sh);
-        const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4], RE = sh[5], CE = sh[6];
+        const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4], RE = sh[5], CE = sh[6], CL = sh[7];
         if (n > CPL * NT || m > RPL * NT || (int)rps.size() > PPT * NT || (int)cps.size() > QPT * NT) continue;
         if (RE > 0 && (stream_only || rlen > RE || clen > CE)) continue;   // pieces must fit the registers
+        if (CL && (!col_one_piece || cl_off)) continue;
         if (pdhg_block_lds_bytes(v, n_pad, m_pad) > 160 * 1024) continue;
         chosen = v;
         break;

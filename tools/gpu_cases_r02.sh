@@ -15,6 +15,9 @@ one() {   # name layout args...
   timeout -k 10 400 python3 -u bench.py --traffic-json $O/${nm}_traffic.json --conv-time 60 --cpu-seconds 6 $* > $O/$nm.json 2> $O/$nm.err || { echo "$nm bench failed"; tail -5 $O/$nm.err; return 1; }
   echo "$nm ok"; head -c 400 $O/$nm.json; echo
 }
-one sslp block --case sslp --scen 4096 && \
-one netdes block --case netdes --scen 1024 && \
-one hydro mfma --case hydro --scen 20000
+case "${CASES:-all}" in
+  sslp) one sslp block --case sslp --scen 4096 ;;
+  *) one sslp block --case sslp --scen 4096 && \
+     one netdes block --case netdes --scen 1024 && \
+     one hydro mfma --case hydro --scen 20000 ;;
+esac
