@@ -302,7 +302,10 @@ def main():
     # + 8 S + 16 N_tot
     ph_bytes = 8 * S_loc * b.N * 4 + 8 * S_loc + 16 * b.N_tot
     ph_gbs = ph_bytes / (upd_ms / args.steps / 1e3) / 1e9
-    valu = eng.layout in ("local", "gather")
+    # the block kernel on a SHARED matrix (sslp) holds its pieces in registers and x / y in LDS: no
+    # per-iteration HBM stream exists to price against the HBM roofline, so it is reported like the
+    # register-resident kernels (fp64 flops against the fp64 peak), with the PMC-measured HBM rate beside
+    valu = eng.layout in ("local", "gather") or (eng.layout == "block" and nnz_distinct == 0)
     # shared-matrix MFMA layout: SURVEY 8(d)2 F = 4 m n flops per scenario per PDHG iteration (A x and
     # A^T y as dense GEMM) and the flops the matrix cores actually execute (16 x 16 x 4 fragments:
     # 2048 flops per 16 scenarios each, the all-zero ones skipped)
@@ -362,7 +365,9 @@ def main():
                      "hbm_measured_frac": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5) if traffic else None,
                      "kernel": {"local": "pdhg_local_kernel (lane-local, fp64 VALU)",
                                 "gather": "pdhg_kernel (wave LDS-gather, fp64 VALU)",
-                                "block": "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)",
+                                "block": ("pdhg_block_kernel (workgroup per scenario, shared matrix: pieces in registers, "
+                                          "x / y in LDS)" if nnz_distinct == 0 else
+                                          "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)"),
                                 "mfma": "pdhg_mfma_kernel (shared matrix, v_mfma_f64_16x16x4_f64, 16 scenarios per wave)",
                                 "stream": f"pdhg_stream_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
                                           "range split, iterates and values streamed)",

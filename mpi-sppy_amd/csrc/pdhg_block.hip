@@ -59,12 +59,12 @@ __device__ __forceinline__ double piece_sum(const double* p, int cnt) {
 // the register budget).  Both forms add the same products in the same order (padding entries are
 // fma(0, x[0], acc) = acc), so they return the same bits.
 //
-// CL (with CE > 0): every column is ONE piece, held by the thread and slot that own the column
-// (QPT == CPL; checked on the host) -- so A^T y needs no partials in LDS and no workgroup barrier:
-// three barriers per PDHG iteration instead of four (sslp: every column has <= 2 entries).
+// CL: every column is ONE piece, held by the thread and slot that own the column (QPT == CPL;
+// checked on the host) -- so A^T y needs no partials in LDS and no workgroup barrier: three
+// barriers per PDHG iteration instead of four (sslp: every column has <= 2 entries; netdes <= 3).
 template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
-    static_assert(!CL || (CE > 0 && QPT == CPL), "column-local A^T y needs register pieces, one per column slot");
+    static_assert(!CL || QPT == CPL, "column-local A^T y needs one piece slot per column slot");
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const BlockLayout& B = a.blk;
@@ -485,6 +485,7 @@ struct BlockVariant {
 };
 
 #define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false>}
+#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true>}
 #define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
@@ -493,11 +494,13 @@ static const BlockVariant kBlockVariants[] = {
     PHG_B(256, 3, 1, 2, 3),      // sslp-like: n <= 768, m <= 256
     PHG_B(256, 4, 4, 4, 4),      // n, m, pieces <= 1024
     PHG_B(512, 4, 4, 4, 4),      // <= 2048
+    PHG_BC(1024, 3, 2, 3, 3),    // netdes-like with column-local A^T y (streamed values)
     PHG_B(1024, 3, 2, 3, 3),     // netdes-like: n <= 3072, m <= 2048
     PHG_B(1024, 4, 4, 4, 4),     // <= 4096
 };
 #undef PHG_B
 #undef PHG_BR
+#undef PHG_BC
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
 
