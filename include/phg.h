@@ -269,6 +269,23 @@ int  phg_timing(phg_handle* h, int32_t which, double* total_ms, int32_t* launche
  * and its conv / status partials (2*virt_nproc+2 doubles, followed by the flag)                */
 int  phg_exchange_buffers(phg_handle* h, double** dev_nodesum, double** dev_convpart);
 
+/* RCCL group: the cross-GPU exchange inside the library (SURVEY 8(b) phg_create_group), for callers
+ * without torch.distributed -- e.g. the reference's mpi4py ranks: rank 0 calls phg_group_unique_id
+ * and MPI_Bcast's the 128 bytes, then every rank calls phg_create_group with its own device (one
+ * process per GPU: ncclCommInitRank; collective over the nranks processes).  Replaces the MPI
+ * Allreduces of phbase.py:88-92 (node sums) and :369 (convergence) for the pipelined iteration:
+ *     phg_node_sums(h, NULL); phg_ph_exchange(h, g); phg_ph_head(h, NULL, thr, first); phg_solve(...)
+ *   phg_group_allreduce : in-place SUM of count doubles at dev_buf, on h's stream (h on g's device)
+ *   phg_ph_exchange     : phg_group_allreduce of h's own packed exchange buffer
+ *   phg_group_size      : out2 = {nranks, rank}                                                  */
+typedef struct phg_group phg_group;
+int  phg_group_unique_id(uint8_t* out128);
+int  phg_create_group(int32_t nranks, int32_t rank, const uint8_t* id128, int32_t device, phg_group** out);
+int  phg_group_size(phg_group* g, int32_t* out2);
+int  phg_group_allreduce(phg_group* g, phg_handle* h, double* dev_buf, int64_t count);
+int  phg_ph_exchange(phg_handle* h, phg_group* g);
+void phg_destroy_group(phg_group* g);
+
 #ifdef __cplusplus
 }
 #endif

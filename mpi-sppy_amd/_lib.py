@@ -79,6 +79,12 @@ SIGNATURES = {
     "phg_solve_undo": (C.c_int, [C.c_void_p]),
     "phg_ph_step": (C.c_int, [C.c_void_p, C.c_double, C.c_int32, i32p]),
     "phg_mfma_info": (C.c_int, [C.c_void_p, i32p]),
+    "phg_group_unique_id": (C.c_int, [C.c_void_p]),
+    "phg_create_group": (C.c_int, [C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
+    "phg_group_size": (C.c_int, [C.c_void_p, i32p]),
+    "phg_group_allreduce": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
+    "phg_ph_exchange": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "phg_destroy_group": (None, [C.c_void_p]),
 }
 
 _lib = None
@@ -126,3 +132,38 @@ def ptr(a):
     if a.dtype == np.int32:
         return a.ctypes.data_as(i32p)
     raise TypeError(a.dtype)
+
+
+class PhgGroup:
+    """An RCCL communicator owned by libphg.so (``phg_create_group``: one process per GPU,
+    ``ncclCommInitRank``).  Collective over the ``nranks`` processes, which must share the 128-byte
+    id of :meth:`unique_id` (made by one rank, broadcast by the caller)."""
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * 128)()
+        check(load().phg_group_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, nranks, rank, uid, device):
+        if len(uid) != 128:
+            raise ValueError("the group id is 128 bytes (PhgGroup.unique_id)")
+        self.lib = load()
+        g = C.c_void_p()
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        check(self.lib.phg_create_group(int(nranks), int(rank), buf, int(device), C.byref(g)))
+        self.g = g
+        self.nranks, self.rank, self.device = int(nranks), int(rank), int(device)
+
+    def allreduce(self, handle, dev_ptr, count):
+        """In-place SUM of ``count`` doubles at device address ``dev_ptr``, on ``handle``'s stream."""
+        check(self.lib.phg_group_allreduce(self.g, handle, C.c_void_p(int(dev_ptr)), C.c_int64(int(count))))
+
+    def ph_exchange(self, handle):
+        """All-reduce the handle's own packed exchange buffer (``phg_ph_exchange``)."""
+        check(self.lib.phg_ph_exchange(handle, self.g))
+
+    def close(self):
+        if self.g:
+            self.lib.phg_destroy_group(self.g)
+            self.g = None

@@ -102,3 +102,45 @@ class TorchComm:
         out = [None] * self.size
         self.dist.all_gather_object(out, obj, group=self.group)
         return out
+
+
+class PhgGroupComm:
+    """Device all-reduces through libphg.so's own RCCL communicator (``phg_create_group``,
+    include/phg.h), everything else through ``host`` (any communicator of this module).
+
+    This is the pure C-ABI multi-GPU path: what a reference-side integration with mpi4py would use
+    instead of torch.distributed -- rank 0 makes the 128-byte group id, ``host``
+    broadcasts it, every rank joins with its own device.  The PH exchange buffer (a device tensor)
+    is summed by ``phg_group_allreduce`` on the engine's stream; ``PHBase`` hands the engine's handle
+    over once the engine exists (``attach``)."""
+
+    def __init__(self, host, device):
+        from ._lib import PhgGroup
+        self.host = host
+        self.rank, self.size = host.Get_rank(), host.Get_size()
+        uid = host.bcast_object(PhgGroup.unique_id() if self.rank == 0 else None, root=0)
+        self.group = PhgGroup(self.size, self.rank, uid, device)
+        self.handle = None
+
+    def attach(self, engine):
+        self.handle = engine.h
+
+    def Get_rank(self):
+        return self.rank
+
+    def Get_size(self):
+        return self.size
+
+    def allreduce_sum_(self, t):
+        if getattr(t, "is_cuda", False):
+            if self.handle is None:
+                raise RuntimeError("PhgGroupComm: no engine attached (PHBase attaches its engine)")
+            self.group.allreduce(self.handle, t.data_ptr(), t.numel())
+            return t
+        return self.host.allreduce_sum_(t)
+
+    def close(self):
+        self.group.close()
+
+    def __getattr__(self, name):   # host-side collectives (arrays, scalars, objects, barrier)
+        return getattr(self.host, name)

@@ -4,6 +4,7 @@
 // of the PDHG kernel from the shared sparsity pattern, the node / virtual-rank segment tables of
 // the PH update kernels, and orders every launch on one HIP stream.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1903,6 +1904,79 @@ int phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on) {
                        h->stream));
     CK(hipStreamSynchronize(h->stream));
     return 0;
+}
+
+// ----------------------------------------------------------------------------- RCCL group
+// The PH exchange inside the library (SURVEY 8(b) phg_create_group; replaces the MPI Allreduces of
+// phbase.py:88-92 and :369 for callers without torch.distributed, e.g. mpi4py ranks that broadcast
+// the unique id).  One process per GPU: ncclCommInitRank, not the single-process ncclCommInitAll.
+struct phg_group {
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0, device = 0;
+};
+
+#define NCK(call)                                                                             \
+    do {                                                                                      \
+        ncclResult_t r_ = (call);                                                             \
+        if (r_ != ncclSuccess) return fail(std::string(#call) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+
+int phg_group_unique_id(uint8_t* out128) {
+    if (!out128) return fail("phg_group_unique_id: null output");
+    ncclUniqueId id;
+    NCK(ncclGetUniqueId(&id));
+    std::memcpy(out128, &id, sizeof id);
+    return 0;
+}
+
+int phg_create_group(int32_t nranks, int32_t rank, const uint8_t* id128, int32_t device, phg_group** out) {
+    if (!out || !id128 || nranks < 1 || rank < 0 || rank >= nranks) return fail("phg_create_group: bad arguments");
+    *out = nullptr;
+    CK(hipSetDevice(device));
+    ncclUniqueId id;
+    std::memcpy(&id, id128, sizeof id);
+    auto* g = new phg_group();
+    g->nranks = nranks;
+    g->rank = rank;
+    g->device = device;
+    const ncclResult_t r = ncclCommInitRank(&g->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        delete g;
+        return fail(std::string("phg_create_group: ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    *out = g;
+    return 0;
+}
+
+int phg_group_size(phg_group* g, int32_t* out2) {
+    if (!g || !out2) return fail("phg_group_size: null argument");
+    out2[0] = g->nranks;
+    out2[1] = g->rank;
+    return 0;
+}
+
+int phg_group_allreduce(phg_group* g, phg_handle* h, double* dev_buf, int64_t count) {
+    if (!g || !h || !h->loaded || !dev_buf || count < 0) return fail("phg_group_allreduce: bad arguments");
+    if (g->device != h->device) return fail("phg_group_allreduce: the group and the handle are on different devices");
+    CK(hipSetDevice(h->device));
+    NCK(ncclAllReduce(dev_buf, dev_buf, (size_t)count, ncclDouble, ncclSum, g->comm, h->stream));
+    return 0;
+}
+
+int phg_ph_exchange(phg_handle* h, phg_group* g) {
+    if (!h || !h->loaded) return fail("phg_ph_exchange: no batch loaded");
+    int32_t lay[3];
+    if (phg_exchange_layout(h, lay)) return -1;
+    return phg_group_allreduce(g, h, h->packed, lay[2]);
+}
+
+void phg_destroy_group(phg_group* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->device);
+    if (g->comm) (void)ncclCommDestroy(g->comm);
+    delete g;
 }
 
 int phg_exchange_buffers(phg_handle* h, double** ns, double** cp) {

@@ -107,6 +107,8 @@ class PHBase(SPBase):
         self.engine = Engine(batch, device=device, stream=stream, exchange=exchange,
                              layout=self.options.get("pdhg_layout", "auto"),
                              presolve=self.options.get("pdhg_presolve", True))
+        if hasattr(self.mpicomm, "attach"):   # comm.PhgGroupComm: the library's own RCCL group
+            self.mpicomm.attach(self.engine)
         self.engine.set(_lib.F_RHO, float(self.options["defaultPHrho"]))
 
     def _device_setup(self, batch):
@@ -118,7 +120,9 @@ class PHBase(SPBase):
             if torch.cuda.is_available():
                 device = torch.cuda.current_device() if "device" not in self.options else device
                 stream = torch.cuda.current_stream(device).cuda_stream
-                if self.n_proc > 1:   # one packed buffer, one all-reduce per pipelined iteration
+                # one packed buffer, one all-reduce per pipelined iteration (pdhg_exchange: also on
+                # one rank, to run the exchange path through a 1-rank communicator in tests)
+                if self.n_proc > 1 or self.options.get("pdhg_exchange", False):
                     exchange = torch.zeros(2 * batch.N_tot + 2 * batch.virt_nproc + 3, dtype=torch.float64,
                                            device=f"cuda:{device}")
         except ImportError:
