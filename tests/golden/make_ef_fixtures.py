@@ -269,9 +269,76 @@ def oracle_ph(S=30, cm=10, thr=1e-4, max_iter=20000, procs=8):
     print(fn, o._PHIter, conv, eobj, flush=True)
 
 
+def oracle_ph_iters(S=30, cm=10, iters=100, procs=8):
+    """The oracle's PH for a FIXED number of iterations (convthresh 0: no early stop) on farmer
+    cm={cm}: per-iteration convergence metric, E[obj], trivial bound, x-bar and W after the last
+    iteration -> ``oracle_ph_farmer_cm{cm}_S{S}_it{iters}.json``.  (The oracle's PH to conv < 1e-4
+    does not finish here: its HiGHS 1.8 QP solves stop ~1e-2 short of the optimum, and at S = 30
+    its metric hovered around 1e-3 after 2 900 iterations / 95 min on 8 processes.)"""
+    import multiprocessing as mp
+    from oracle import ph as oph
+    opts = {"defaultPHrho": 1.0, "PHIterLimit": iters, "convthresh": 0.0}
+    t0 = time.perf_counter()
+    state = {}
+
+    class PoolPH(oph.OraclePH):
+        def solve_loop(self):
+            jobs = []
+            for k in range(self.S):
+                a = self.arr[k]
+                sg = 1.0 if self.scen[k].sense == 1 else -1.0
+                c = sg * a["c"].copy()
+                q = None
+                off = 0.0
+                cols = self.cols[k]
+                if self.W_on:
+                    np.add.at(c, cols, self.W[k])
+                if self.prox_on:
+                    rho = self.rho[k]
+                    xb = self.xbar[k]
+                    np.add.at(c, cols, -rho * xb)
+                    q = np.zeros_like(c)
+                    np.add.at(q, cols, rho)
+                    off = float(np.sum(rho / 2.0 * xb * xb))
+                jobs.append((k, c, q, off, self.threads))
+            for k, ok, st, x, obj in state["pool"].map(_pool_solve, jobs):
+                if not ok:
+                    raise RuntimeError(f"[oracle] Solve failed for scenario {self.names[k]}: {st}")
+                sg = 1.0 if self.scen[k].sense == 1 else -1.0
+                self.feasible[k] = True
+                self.x[k] = x
+                self.obj[k] = sg * obj
+                self.outer[k] = sg * obj
+            self.solve_count += self.S
+
+    global _POOL_ARR
+    o = PoolPH(opts, om.farmer_names(S), om.farmer, dict(crops_multiplier=cm, num_scens=S))
+    _POOL_ARR = o.arr
+    state["pool"] = mp.get_context("fork").Pool(procs)
+    tb = o.Iter0()
+    # Iter0's LPs may have several optimal x (the trivial bound is unique, the nonants need not
+    # be): the GPU test starts its PH from THESE nonants, after which every prox-QP has unique ones
+    x0 = np.array([o.nonants(k) for k in range(o.S)])
+    o.iterk_loop()
+    eobj = o.Eobjective()
+    conv = o.conv
+    state["pool"].close()
+    out = {"instance": f"farmer crops_multiplier={cm}, scen0..scen{S - 1}, rho=1, {iters} PH iterations (no early stop)",
+           "S": S, "cm": cm, "iters": iters, "x0_nonants": x0.tolist(),
+           "conv_history": list(map(float, o.history)), "Eobj": eobj,
+           "trivial_bound": tb, "xbar": list(map(float, o.xbar[0])), "W": np.asarray(o.W).tolist(),
+           "solver": "oracle/ph.py (HiGHS 1.8 QP via scipy per scenario)", "seconds": round(time.perf_counter() - t0, 1)}
+    fn = os.path.join(HERE, f"oracle_ph_farmer_cm{cm}_S{S}_it{iters}.json")
+    with open(fn, "w") as f:
+        json.dump(out, f)
+    print(fn, o._PHIter, conv, eobj, flush=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1:2] == ["sep"]:
         separable_fixture([int(a) for a in sys.argv[2:]])
+    elif sys.argv[1:2] == ["phit"]:
+        oracle_ph_iters(*[int(a) for a in sys.argv[2:5]])
     elif sys.argv[1:2] == ["ph"]:
         oracle_ph(*[int(a) for a in sys.argv[2:3]])
     else:
