@@ -16,7 +16,10 @@ Findings kept for the record (farmer cm=10, 100 scenarios, 30 PH iterations, eps
     1.4 s): not adopted;
   * restart to the current iterate only (noavg=1): +2 % iterations here, but 136 of 10 000
     scenarios hit the iteration cap late in a long PH run on the GPU: not adopted;
-  * Halpern / reflected Halpern ("hal"): 20-110 % more iterations: not adopted.
+  * Halpern / reflected Halpern ("hal"): 20-110 % more iterations: not adopted;
+  * extrapolated warm start x_k + a (x_k - x_{k-1}) (and y), "ex=a": 276.3 / 275.4 / 279.4 mean
+    iterations per solve at a = 0 / 0.5 / 1 (40 PH iterations, 100 scenarios, presolved, the
+    kernels' settings): no gain, not adopted.
 """
 import os
 import sys
@@ -257,11 +260,13 @@ def main():
             else:
                 kw[k_ if v_ else "gamma"] = float(v_ if v_ else k_)
         lab.check = int(kw.pop("chk", lab.check)) if "chk" in kw else lab.check
+        ex = kw.pop("ex", 0.0)          # extrapolated warm start x + ex (x - x_prev)
         W = np.zeros((S, N))
         xbar = np.zeros(N)
         x = np.zeros(b.A.shape[1])
         y = np.zeros(b.A.shape[0])
         its = []
+        xp, yp = None, None
         t0 = time.perf_counter()
         for k in range(K + 1):
             c = c0.copy().reshape(S, n)
@@ -269,7 +274,11 @@ def main():
             if k > 0:
                 c[:, cols] += W - 1.0 * xbar
                 q[:, cols] = 1.0
-            x, y, it = lab.solve(c.ravel(), q.ravel(), x, y, variant=name, **kw)
+            x0, y0 = x, y
+            if ex and xp is not None and k > 1:
+                x0, y0 = x + ex * (x - xp), y + ex * (y - yp)
+            xp, yp = x, y
+            x, y, it = lab.solve(c.ravel(), q.ravel(), x0, y0, variant=name, **kw)
             if k > 0:
                 its.append(it.mean())
             xn = x.reshape(S, n)[:, cols]
