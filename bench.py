@@ -164,7 +164,13 @@ def main():
     device = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
     torch.cuda.set_device(device)
     comm = None
-    if world > 1:
+    # PHG_FORCE_DIST=1 (tests): the multi-GPU code path on ONE rank -- process group, TorchComm and
+    # the packed device exchange all-reduced by the backend (nccl = RCCL), which a one-GPU box can
+    # otherwise never run (RCCL refuses two ranks on one device)
+    force_dist = os.environ.get("PHG_FORCE_DIST", "0") == "1"
+    if force_dist and "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(_free_port())
+    if world > 1 or force_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(f"cuda:{device}"))
@@ -177,7 +183,7 @@ def main():
     from mpisppy_amd.comm import TorchComm
     from mpisppy_amd.examples import farmer, hydro, netdes, sslp, uc
     from mpisppy_amd.ph import PH
-    if world > 1:
+    if world > 1 or force_dist:
         comm = TorchComm()
 
     default_scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024, "hydro": 2000, "uc": 64}[args.case]
@@ -192,7 +198,8 @@ def main():
             "pdhg_schedule": not args.no_schedule, "pdhg_check_every": args.check_every,
             "pdhg_beta_artificial": args.beta_art, "pdhg_primal_weight_theta": args.theta, "pdhg_presolve": not args.no_presolve,
             "pdhg_keep_omega": {"fresh": False, "carry": True, "blend": "blend"}[args.keep_omega],
-            "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps}}
+            "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps},
+            "pdhg_exchange": force_dist}
     args.creator_kwargs = ckw
     t_setup = time.perf_counter()
     ph = PH(dict(opts), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw, all_nodenames=nodenames)
@@ -455,7 +462,7 @@ def main():
             out["cpu_baseline"]["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

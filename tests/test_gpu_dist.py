@@ -39,3 +39,20 @@ def test_two_ranks_match_one_rank():
     assert two["value"] > 0
     c1, c2 = one["conv_at_end"], two["conv_at_end"]
     assert abs(c1 - c2) <= 1e-9 * max(1.0, abs(c1)), (c1, c2)
+
+
+def test_rccl_backend_single_rank_matches():
+    """The production multi-GPU code path -- nccl (= RCCL) process group, TorchComm, the packed
+    device exchange all-reduced by RCCL on torch's stream, the conv run's collectives -- on ONE rank
+    (PHG_FORCE_DIST=1: a one-GPU box cannot hold two RCCL ranks).  A one-rank SUM is the identity,
+    so the PH trajectory equals the single-GPU path's bit for bit."""
+    args = ["--steps", "3", "--warmup", "2", "--conv-iters", "400", "--cpu-seconds", "0", "--cm", "2",
+            "--scen", "1000"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("PHG_DIST_BACKEND", None)
+    plain = _run([sys.executable, "bench.py"] + args, env)
+    forced = _run([sys.executable, "bench.py"] + args, dict(env, PHG_FORCE_DIST="1"))
+    assert forced["n_gpus"] == 1 and forced["config"]["scenarios"] == 1000
+    assert forced["conv_at_end"] == plain["conv_at_end"]
+    tp, tf = plain["time_to_conv"], forced["time_to_conv"]
+    assert tf["ph_iters"] == tp["ph_iters"] and tf["conv"] == tp["conv"] and tf["Eobj"] == tp["Eobj"]
