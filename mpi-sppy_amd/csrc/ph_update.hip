@@ -9,6 +9,8 @@
 // inside one node) and then, by the last workgroup, per node in segment order; the cross-GPU
 // all-reduce (RCCL) of the 2*N_tot node sums and of the 2*P+2 convergence partials happens
 // between / after the kernels (see include/phg.h).
+#include <type_traits>
+
 #include "phg_internal.h"
 
 namespace phg {
@@ -361,13 +363,13 @@ __device__ __forceinline__ void w_update_segment(const PhArgs& a, int b, const d
         // or last element of the segment is done by thread 0
         long b = e0;
         if (b & 1) {
-            if (tid == 0) acc += upd(b, a.xN[b], nodesum[(int)(b % a.N)], a.W[b], a.rho[b]);
+            if (tid == 0) acc += upd(b, a.xN[b], nodesum[(int)(b % a.N)], a.W[b], a.rho_k ? a.rho_k[(int)(b % a.N)] : a.rho[b]);
             ++b;
         }
         const long npair = (e1 - b) >> 1;
         if (((e1 - b) & 1) && tid == 0) {
             const long l = e1 - 1;
-            acc += upd(l, a.xN[l], nodesum[(int)(l % a.N)], a.W[l], a.rho[l]);
+            acc += upd(l, a.xN[l], nodesum[(int)(l % a.N)], a.W[l], a.rho_k ? a.rho_k[(int)(l % a.N)] : a.rho[l]);
         }
         const double2* X2 = reinterpret_cast<const double2*>(a.xN + b);
         const double2* R2 = reinterpret_cast<const double2*>(a.rho + b);
@@ -378,32 +380,43 @@ __device__ __forceinline__ void w_update_segment(const PhArgs& a, int b, const d
         auto adv2 = [&](int kk) { kk += dk2; return kk >= N ? kk - N : kk; };
         auto nxt = [&](int kk) { return kk + 1 == N ? 0 : kk + 1; };
         long pp = tid;
-        for (; pp + 3 * 256 < npair; pp += 4 * 256) {
-            double2 xv[4], wv[4], rv[4];
-            double xb0[4], xb1[4];
+        // RK: rho the same in every scenario -- its two values come from the [N] copy (cached), not
+        // from a third S*N stream
+        auto pairs = [&](auto rkc) {
+            constexpr bool RK = decltype(rkc)::value;
+            auto rho2 = [&](long q, int k0) {
+                if constexpr (RK) return make_double2(a.rho_k[k0], a.rho_k[nxt(k0)]);
+                else return R2[q];
+            };
+            for (; pp + 3 * 256 < npair; pp += 4 * 256) {
+                double2 xv[4], wv[4], rv[4];
+                double xb0[4], xb1[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                xv[u] = X2[pp + u * 256];
-                wv[u] = W2[pp + u * 256];
-                rv[u] = R2[pp + u * 256];
-                xb0[u] = nodesum[kp];
-                xb1[u] = nodesum[nxt(kp)];
+                for (int u = 0; u < 4; ++u) {
+                    xv[u] = X2[pp + u * 256];
+                    wv[u] = W2[pp + u * 256];
+                    rv[u] = rho2(pp + u * 256, kp);
+                    xb0[u] = nodesum[kp];
+                    xb1[u] = nodesum[nxt(kp)];
+                    kp = adv2(kp);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double d0 = xv[u].x - xb0[u], d1 = xv[u].y - xb1[u];
+                    W2[pp + u * 256] = make_double2(fma(rv[u].x, d0, wv[u].x), fma(rv[u].y, d1, wv[u].y));
+                    acc += fabs(d0) + fabs(d1);
+                }
+            }
+            for (; pp < npair; pp += 256) {
+                const double2 xv = X2[pp], wv = W2[pp], rv = rho2(pp, kp);
+                const double d0 = xv.x - nodesum[kp], d1 = xv.y - nodesum[nxt(kp)];
+                W2[pp] = make_double2(fma(rv.x, d0, wv.x), fma(rv.y, d1, wv.y));
+                acc += fabs(d0) + fabs(d1);
                 kp = adv2(kp);
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const double d0 = xv[u].x - xb0[u], d1 = xv[u].y - xb1[u];
-                W2[pp + u * 256] = make_double2(fma(rv[u].x, d0, wv[u].x), fma(rv[u].y, d1, wv[u].y));
-                acc += fabs(d0) + fabs(d1);
-            }
-        }
-        for (; pp < npair; pp += 256) {
-            const double2 xv = X2[pp], wv = W2[pp], rv = R2[pp];
-            const double d0 = xv.x - nodesum[kp], d1 = xv.y - nodesum[nxt(kp)];
-            W2[pp] = make_double2(fma(rv.x, d0, wv.x), fma(rv.y, d1, wv.y));
-            acc += fabs(d0) + fabs(d1);
-            kp = adv2(kp);
-        }
+        };
+        if (a.rho_k) pairs(std::true_type{});
+        else pairs(std::false_type{});
         e = e1;   // the generic loops below are skipped
     }
     // four elements in flight per thread (all loads before the stores), then the remainder
@@ -416,7 +429,7 @@ __device__ __forceinline__ void w_update_segment(const PhArgs& a, int b, const d
             if constexpr (ROOT_ONLY) { xb[u] = nodesum[k]; k = adv(k); }
             else xb[u] = nodesum[a.xidx[f]];
             w[u] = a.W[f];
-            r[u] = a.rho[f];
+            r[u] = a.rho_k ? a.rho_k[(int)(f % a.N)] : a.rho[f];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc += upd(e + u * 256, xv[u], xb[u], w[u], r[u]);
@@ -425,7 +438,7 @@ __device__ __forceinline__ void w_update_segment(const PhArgs& a, int b, const d
         double xb;
         if constexpr (ROOT_ONLY) { xb = nodesum[k]; k = adv(k); }
         else xb = nodesum[a.xidx[e]];
-        acc += upd(e, a.xN[e], xb, a.W[e], a.rho[e]);
+        acc += upd(e, a.xN[e], xb, a.W[e], a.rho_k ? a.rho_k[(int)(e % a.N)] : a.rho[e]);
     }
     int nb = 0, nn = 0;
     if (a.status)

@@ -172,6 +172,7 @@ struct phg_handle {
     // the launch schedule is recomputed after every kSchedEvery-th solve (iteration counts move
     // slowly under warm starts; the sort is a latency-bound single-workgroup launch)
     int solves = 0;
+    double* rho_k = nullptr;   // [N] copy of rho when it is the same in every scenario (PhArgs::rho_k)
     std::vector<int> row_map;  // original row -> kept row, or -1 (folded into a column bound)
 };
 
@@ -313,6 +314,17 @@ int phg_copy_from(phg_handle* dst, phg_handle* src, int32_t field) {
     CK(hipSetDevice(dst->device));
     if (cross_stream_wait(dst, src)) return -1;
     CK(hipMemcpyAsync(pd, ps, nd * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
+    if (field == PHG_F_RHO) {   // dst's rho is now src's: so is its shared [N] copy (or its absence)
+        if (src->ph.rho_k && !dst->rho_k) {
+            double* q;
+            if (dalloc(dst, &q, (size_t)std::max(1, dst->N))) return -1;
+            dst->rho_k = q;
+        }
+        if (src->ph.rho_k)
+            CK(hipMemcpyAsync(dst->rho_k, src->ph.rho_k, (size_t)dst->N * sizeof(double), hipMemcpyDeviceToDevice,
+                              dst->stream));
+        dst->ph.rho_k = src->ph.rho_k ? dst->rho_k : nullptr;
+    }
     // and the other direction: src's next work (e.g. the hub's W update, which rewrites W in place)
     // must not start before the copy has read src's buffer
     return cross_stream_wait(src, dst);
@@ -714,6 +726,7 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     bool root_only = true;   // x-bar slot == k for every scenario (two-stage): w_update_kernel<true>
     for (size_t e = 0; e < xidx.size() && root_only; ++e) root_only = xidx[e] == (int)(e % (size_t)N);
     PhArgs& a = h->ph;
+    a.rho_k = nullptr;   // until phg_set(PHG_F_RHO) finds rho the same in every scenario
     a.root_only = root_only ? 1 : 0;
     a.S = S; a.N = N; a.N_tot = b->N_tot; a.L = L; a.P = P; a.maxk = maxk; a.n_nodes = b->n_nodes;
     a.n_seg = (int)segs.size();
@@ -1680,6 +1693,17 @@ int phg_set(phg_handle* h, int32_t f, const double* in) {
         in = packed.data();
     }
     CK(hipMemcpyAsync(p, in, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    if (f == PHG_F_RHO) {   // rho the same in every scenario? then the W update reads its [N] copy
+        bool shared = true;
+        for (size_t e = (size_t)h->N; e < cnt && shared; ++e) shared = in[e] == in[e % (size_t)h->N];
+        if (shared && !h->rho_k) {
+            double* q;
+            if (dalloc(h, &q, (size_t)std::max(1, h->N))) return -1;
+            h->rho_k = q;
+        }
+        if (shared) CK(hipMemcpyAsync(h->rho_k, in, (size_t)h->N * sizeof(double), hipMemcpyHostToDevice, h->stream));
+        h->ph.rho_k = shared ? h->rho_k : nullptr;
+    }
     CK(hipStreamSynchronize(h->stream));
     return 0;
 }

@@ -146,6 +146,9 @@ struct PdhgArgs {
     // PH parameters
     const double* W;        // [S*N]
     const double* rho;      // [S*N]
+    const double* rho_k;    // [N] when rho[s*N + k] == rho_k[k] for every scenario (set by phg_set on the
+                            // host check; the usual case: defaultPHrho / a per-variable rho_setter), else
+                            // null -- the W update then reads N doubles instead of streaming S*N
     const double* xbar;     // [N_tot]
     const int*    xidx;     // [S*N]   xbar slot of (s,k)
     const double* fixed;    // [S*N]
@@ -215,6 +218,9 @@ struct PhArgs {
     const double* xN;       // [S*N]
     double* W;              // [S*N]
     const double* rho;      // [S*N]
+    const double* rho_k;    // [N] when rho[s*N + k] == rho_k[k] for every scenario (set by phg_set on the
+                            // host check; the usual case: defaultPHrho / a per-variable rho_setter), else
+                            // null -- the W update then reads N doubles instead of streaming S*N
     const int* xidx;        // [S*N]
     int root_only;          // xidx[s*N + k] == k for all s (two-stage trees): xidx is not read
     const double* pc;       // [S*L]

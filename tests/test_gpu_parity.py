@@ -74,6 +74,32 @@ def test_ph_update_kernels_vs_oracle_farmer(vnp):
         o.solve_loop()
 
 
+@pytest.mark.parametrize("varies", [False, True])
+def test_w_update_per_variable_rho_vs_oracle(varies):
+    """rho per variable (a rho_setter): the same in every scenario -> the W update reads its [N]
+    copy (PhArgs::rho_k); different per scenario -> the S*N stream.  W against the oracle at 1e-12."""
+    S = 7
+    ph = _farmer_ph(S, cm=2)
+    ph.PH_Prep()
+    o = _farmer_oracle(S, cm=2, PHIterLimit=4)
+    o.Iter0()
+    N = ph.engine.N
+    R = np.tile(0.5 + 0.1 * np.arange(N), (S, 1))
+    if varies:
+        R = R + 0.01 * np.arange(S)[:, None]
+    ph.engine.set(_lib.F_RHO, R.ravel())
+    for k in range(S):
+        o.rho[k] = R[k].copy()
+    for it in range(1, 4):
+        ph.engine.set(_lib.F_XN, np.array([o.nonants(k) for k in range(S)]).ravel())
+        o.Compute_Xbar()
+        o.Update_W()
+        ph.Compute_Xbar()
+        ph.Update_W()
+        np.testing.assert_allclose(ph.Ws(), o.W, rtol=1e-12, atol=1e-9)
+        o.solve_loop()
+
+
 def test_ph_update_kernels_vs_oracle_hydro():
     """Multistage: per-node reductions with the stage-2 nodes of the 3x3 tree."""
     bf = [3, 3]
