@@ -126,7 +126,7 @@ __device__ __forceinline__ void finish_k(unsigned* counter, unsigned* done, int 
 }
 
 // Node sums (first half of _Compute_Xbar).  One workgroup per node segment (a contiguous scenario
-// range inside one node, sized on the host so that large batches get ~512 segments per level) and
+// range inside one node, sized on the host so that large batches get ~256 segments per level) and
 // 256-nonant column chunk (blockIdx.y; wide nodes get several workgroups per segment, so the
 // number of loads in flight does not depend on the final reduction's segment count);
 // thread t handles nonant k = t % klen of scenarios s0 + t / klen + q*i (q = 256 / klen lanes per

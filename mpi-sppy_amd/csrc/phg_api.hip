@@ -655,13 +655,13 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     // node segments: contiguous scenario ranges per node, chunked
     std::vector<std::vector<NodeSeg>> per_node(b->n_nodes);
     // segments per level cap (PHG_NODESEG_MAX: tuning knob for tools/ph_update_sweep.py)
-    int seg_max = 512;
+    int seg_max = 256;   // (512 -> 256 measured: S*N 1e6 / 1e7 / 1e8 33 -> 29, 73 -> 71, ~670 -> ~657 us)
     if (const char* ev = std::getenv("PHG_NODESEG_MAX")) seg_max = std::max(1, std::atoi(ev));
     for (int lv = 0; lv < L; ++lv) {
         const int klen = b->level_len[lv];
         // ~8 scenarios per thread of a 256-thread workgroup: enough workgroups to hide the load
         // latency at small S, whole-row coalesced streaming at large S
-        // and at most ~512 segments per level, so the final per-node sums stay short at large S
+        // and at most ~256 segments per level, so the final per-node sums stay short at large S
         const int chunk = std::max(klen >= 256 ? 8 : 8 * (256 / std::max(1, klen)), (S + seg_max - 1) / seg_max);
         int s = 0;
         while (s < S) {
