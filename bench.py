@@ -150,6 +150,12 @@ def main():
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
         _self_launch(args)
+    # stdout carries exactly ONE line, the JSON result: RCCL prints a version banner to stdout when
+    # a communicator comes up (at the first collective), so from here on fd 1 points at stderr and
+    # the JSON goes to a saved copy of the real stdout
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -185,6 +191,14 @@ def main():
     from mpisppy_amd.ph import PH
     if world > 1 or force_dist:
         comm = TorchComm()
+        # the per-iteration exchange through the library's own RCCL communicator (phg_create_group,
+        # on the library's stream): measured on one rank, host + exchange 0.026-0.029 vs 0.034-0.035 ms
+        # per PH iteration through torch.distributed's, time to conv 1.02 vs 1.07 s (same trajectory).
+        # Setup and host-side collectives stay on torch.distributed.  PHG_EXCHANGE=torch: the torch
+        # path (and always under gloo, which puts several ranks on one device)
+        if backend == "nccl" and os.environ.get("PHG_EXCHANGE", "lib") == "lib":
+            from mpisppy_amd.comm import PhgGroupComm
+            comm = PhgGroupComm(comm, device)
 
     default_scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024, "hydro": 2000, "uc": 64}[args.case]
     if args.scen is None:
@@ -353,7 +367,8 @@ def main():
         "config": {"workload": f"{desc}, {S} scenarios ({args.scen} per GPU), PH rho={args.rho}, "
                                f"PDHG eps_rel={args.eps}",
                    "scenarios": S, "n": b.n, "m": b.m, "nnz": b.nnz, "nonants": b.N,
-                   "parallelism": f"scenario shards over {world} GPU(s), one packed all-reduce per PH iteration",
+                   "parallelism": f"scenario shards over {world} GPU(s), one packed all-reduce per PH iteration"
+                       + (" (libphg RCCL group)" if type(comm).__name__ == "PhgGroupComm" else ""),
                    "pdhg_layout": eng.layout, "lanes_per_scenario": eng.lanes_per_scenario,
                    "presolve_rows_folded": eng.rows_folded},
         # fp64 VALU-bound kernels (lane-local / gather): flops against the fp64 peak; the streaming
@@ -461,7 +476,9 @@ def main():
         if out["cpu_baseline"].get("value"):
             out["cpu_baseline"]["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
+    if type(comm).__name__ == "PhgGroupComm":
+        comm.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

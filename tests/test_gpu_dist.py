@@ -23,8 +23,9 @@ ARGS = ["--steps", "3", "--warmup", "2", "--conv-iters", "0", "--cpu-seconds", "
 def _run(cmd, env):
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    lines = r.stdout.strip().splitlines()
+    # the driver reads stdout: exactly one line, the JSON (RCCL's version banner goes to stderr)
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
     return json.loads(lines[0])
 
 
