@@ -197,8 +197,8 @@ def main():
         # Setup and host-side collectives stay on torch.distributed.  PHG_EXCHANGE=torch: the torch
         # path (and always under gloo, which puts several ranks on one device)
         if backend == "nccl" and os.environ.get("PHG_EXCHANGE", "lib") == "lib":
-            from mpisppy_amd.comm import PhgGroupComm
-            comm = PhgGroupComm(comm, device)
+            from mpisppy_amd.comm import group_or_host
+            comm = group_or_host(comm, device, log=lambda s: print(f"[bench] {s}", file=sys.stderr))
 
     default_scen = {"farmer": 10000, "sslp": 2048, "netdes": 1024, "hydro": 2000, "uc": 64}[args.case]
     if args.scen is None:

@@ -118,7 +118,15 @@ class PhgGroupComm:
         from ._lib import PhgGroup
         self.host = host
         self.rank, self.size = host.Get_rank(), host.Get_size()
-        uid = host.bcast_object(PhgGroup.unique_id() if self.rank == 0 else None, root=0)
+        uid, err = None, None
+        if self.rank == 0:
+            try:
+                uid = PhgGroup.unique_id()
+            except Exception as e:    # every rank still joins the broadcast, then all raise
+                err = e
+        uid = host.bcast_object(uid, root=0)
+        if uid is None:
+            raise RuntimeError(f"phg_group_unique_id failed on rank 0{f': {err}' if err else ''}")
         self.group = PhgGroup(self.size, self.rank, uid, device)
         self.handle = None
 
@@ -144,3 +152,26 @@ class PhgGroupComm:
 
     def __getattr__(self, name):   # host-side collectives (arrays, scalars, objects, barrier)
         return getattr(self.host, name)
+
+
+def group_or_host(host, device, log=None):
+    """``PhgGroupComm(host, device)`` when every rank creates the library group, else ``host``
+    on every rank: each rank reports whether its ``phg_create_group`` succeeded and the ranks agree
+    through ``host`` (one scalar SUM), so no rank is left on a different exchange path than the
+    others.  The fallback is the same device all-reduce through torch.distributed's RCCL, not a CPU
+    path; ``log`` (a callable) receives the reason."""
+    from ._lib import PhgError
+    comm, err = None, None
+    try:
+        comm = PhgGroupComm(host, device)
+    except (PhgError, OSError, RuntimeError) as e:
+        err = e
+    n_ok = host.allreduce_scalar(1.0 if comm is not None else 0.0)
+    if n_ok == host.Get_size():
+        return comm
+    if comm is not None:
+        comm.close()
+    if log is not None:
+        log(f"libphg RCCL group not created on {host.Get_size() - int(n_ok)} rank(s)"
+            + (f" ({err})" if err is not None else "") + "; exchange through torch.distributed")
+    return host

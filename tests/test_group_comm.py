@@ -73,3 +73,58 @@ def test_routing(monkeypatch):
     assert c.allreduce_array([1.0, 2.0]).tolist() == [1.0, 2.0]   # delegated (SingleComm)
     c.close()
     assert g.calls[-1] == "closed"
+
+
+class _Host2(_Host):
+    """Rank ``rank`` of 2 whose peer reports ``peer_ok`` for the group creation."""
+
+    def __init__(self, rank, peer_ok):
+        super().__init__()
+        self.rank_, self.peer_ok = rank, peer_ok
+
+    def Get_rank(self):
+        return self.rank_
+
+    def Get_size(self):
+        return 2
+
+    def allreduce_scalar(self, v):
+        return float(v) + (1.0 if self.peer_ok else 0.0)
+
+    def bcast_object(self, obj, root=0):     # rank 0's id reaches rank 1
+        return super().bcast_object(obj if self.rank_ == 0 else bytes(range(128)), root)
+
+
+class _FailingGroup(_FakeGroup):
+    def __init__(self, *a):
+        raise _lib.PhgError("ncclCommInitRank: unhandled system error")
+
+
+@pytest.mark.parametrize("rank", [0, 1])
+def test_group_or_host_agreement(monkeypatch, rank):
+    """Every rank ends on the same exchange path: the library group only when all ranks created it;
+    a rank whose group was created while a peer's failed closes it and uses the host communicator."""
+    from mpisppy_amd.comm import group_or_host
+    monkeypatch.setattr(_lib, "PhgGroup", _FakeGroup)
+    c = group_or_host(_Host2(rank, True), 0)
+    assert isinstance(c, PhgGroupComm) and c.group.args[:2] == (2, rank)
+    host, logs = _Host2(rank, False), []
+    assert group_or_host(host, 0, log=logs.append) is host
+    assert _FakeGroup.made[-1].calls == ["closed"] and "1 rank(s)" in logs[0]
+    monkeypatch.setattr(_lib, "PhgGroup", _FailingGroup)
+    host, logs = _Host2(rank, True), []
+    assert group_or_host(host, 0, log=logs.append) is host and "unhandled system error" in logs[0]
+
+
+def test_uid_failure_still_broadcasts(monkeypatch):
+    """Rank 0 failing to make the id still joins the broadcast (its peers would block in it), and
+    every rank then raises."""
+    class _NoId(_FakeGroup):
+        @staticmethod
+        def unique_id():
+            raise _lib.PhgError("ncclGetUniqueId failed")
+    monkeypatch.setattr(_lib, "PhgGroup", _NoId)
+    host = _Host()
+    with pytest.raises(RuntimeError, match="ncclGetUniqueId failed"):
+        PhgGroupComm(host, 0)
+    assert host.bcast == [(None, 0)]
