@@ -57,6 +57,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
     const int lane = threadIdx.x;
     const int g = lane >> 4;                       // lane row: element offset inside a tile row block
     auto CS = [&](int item) -> double& { return cold[item * 64 + lane]; };
+    // per-scenario scalars: one slot per scenario, written with the same bits by its 4 lanes
+    auto SS = [&](int item) -> double& { return cold[CI::SC * 64 + item * 16 + (lane & 15)]; };
     const int w_raw = blockIdx.x * 16 + (lane & 15);
     const bool valid = w_raw < a.S;
     const int w = valid ? w_raw : a.S - 1;         // a tail lane mirrors the last item, writes nothing
@@ -174,20 +176,20 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
     {
         double rr[4] = {c2, prox_const, cs2, b2};
         ssum_many<4>(rr);
-        CS(CI::SC + CI::CNORM) = sqrt(rr[0]);
-        CS(CI::SC + CI::PROX) = rr[1];
+        SS(CI::CNORM) = sqrt(rr[0]);
+        SS(CI::PROX) = rr[1];
         const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
         omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
         if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
         else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);
     }
     const double eta = a.eta[s];
-    CS(CI::SC + CI::BNORM) = a.bnorm[s];
-    CS(CI::SC + CI::ETA) = eta;
+    SS(CI::BNORM) = a.bnorm[s];
+    SS(CI::ETA) = eta;
     {
-        const double tp = a.eps * (1.0 + a.bnorm[s]), td = a.eps * (1.0 + CS(CI::SC + CI::CNORM));
-        CS(CI::SC + CI::TP) = tp * tp;
-        CS(CI::SC + CI::TD) = td * td;
+        const double tp = a.eps * (1.0 + a.bnorm[s]), td = a.eps * (1.0 + SS(CI::CNORM));
+        SS(CI::TP) = tp * tp;
+        SS(CI::TD) = td * td;
     }
     double tau = eta / omega, sig = eta * omega;
     auto rescale_bounds = [&]() {
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
             if (fin(hi[k])) t[5] += hi[k] * fmin(rc_, 0.0);
             t[5] -= hq;
         }
-        t[0] = fma(CS(CI::SC + CI::W2), pr2, dr2 * CS(CI::SC + CI::IW2));
+        t[0] = fma(SS(CI::W2), pr2, dr2 * SS(CI::IW2));
     };
     auto kkt_both = [&](bool avg, double inv, double* oc, double* oa) {
         double t[12];
@@ -267,13 +269,13 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
             for (int u = 0; u < 6; ++u) oa[u] = t[6 + u];
     };
     auto rel_of = [&](const double* o) {
-        const double p = sqrt(o[2]) / (1.0 + CS(CI::SC + CI::BNORM));
-        const double d = sqrt(o[3]) / (1.0 + CS(CI::SC + CI::CNORM));
+        const double p = sqrt(o[2]) / (1.0 + SS(CI::BNORM));
+        const double d = sqrt(o[3]) / (1.0 + SS(CI::CNORM));
         const double gg = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
         return fmax(fmax(p, d), gg);
     };
     auto converged = [&](const double* o) {
-        return o[2] <= CS(CI::SC + CI::TP) && o[3] <= CS(CI::SC + CI::TD) &&
+        return o[2] <= SS(CI::TP) && o[3] <= SS(CI::TD) &&
                fabs(o[4] - o[5]) <= a.eps * (1.0 + fabs(o[4]) + fabs(o[5]));
     };
     auto wkkt2_of = [&](const double* o) {
@@ -281,14 +283,14 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
         return fma(gg, gg, o[0]);
     };
 
-    CS(CI::SC + CI::OMEGA) = omega;
-    CS(CI::SC + CI::W2) = omega * omega;
-    CS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
+    SS(CI::OMEGA) = omega;
+    SS(CI::W2) = omega * omega;
+    SS(CI::IW2) = 1.0 / (omega * omega);
     {
         double o[6];
         kkt_both(false, 0.0, o, o);
-        CS(CI::SC + CI::KRST) = wkkt2_of(o);
-        CS(CI::SC + CI::KPREV) = INFINITY;
+        SS(CI::KRST) = wkkt2_of(o);
+        SS(CI::KPREV) = INFINITY;
     }
     int it = 0, since = 0, cnt = 0;
     bool live = true;
@@ -324,8 +326,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
             }
         }
         if (g == 0) {
-            const double offs = a.obj_off[sl] + (a.prox_on ? CS(CI::SC + CI::PROX) : 0.0);
-            a.omega[sl] = CS(CI::SC + CI::OMEGA);
+            const double offs = a.obj_off[sl] + (a.prox_on ? SS(CI::PROX) : 0.0);
+            a.omega[sl] = SS(CI::OMEGA);
             a.obj[sl] = a.sense * (pobj + offs);
             a.bound[sl] = a.sense * (dobj + offs);
             a.kkt[sl] = rel;
@@ -382,11 +384,11 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
         const double k_cur = wkkt2_of(oc), k_avg = wkkt2_of(oa);
         const bool use_avg = k_avg < k_cur;
         const double cand = use_avg ? k_avg : k_cur;
-        const double krst = CS(CI::SC + CI::KRST);
+        const double krst = SS(CI::KRST);
         const bool restart = live && ((cand <= a.beta_suf * a.beta_suf * krst) ||
-                                      (cand <= a.beta_nec * a.beta_nec * krst && cand > CS(CI::SC + CI::KPREV)) ||
+                                      (cand <= a.beta_nec * a.beta_nec * krst && cand > SS(CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
-        CS(CI::SC + CI::KPREV) = cand;
+        SS(CI::KPREV) = cand;
         if (wave_any(restart)) {
             const bool ra = restart && use_avg;
             if (wave_any(ra)) {
@@ -406,8 +408,8 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
             for (int r = 0; r < KR; ++r) { const double t = y[r] - CS(CI::YR + r); mv[1] += t * t; }
             ssum_many<2>(mv);
             if (restart) {
-                omega = primal_weight(CS(CI::SC + CI::OMEGA), mv[0], mv[1], a.theta);
-                const double et = CS(CI::SC + CI::ETA);
+                omega = primal_weight(SS(CI::OMEGA), mv[0], mv[1], a.theta);
+                const double et = SS(CI::ETA);
                 tau = et / omega;
                 sig = et * omega;
                 rescale_bounds();
@@ -416,11 +418,11 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
                 for (int k = 0; k < KC; ++k) { CS(CI::XR + k) = x[k]; xsum[k] = 0.0; }
 #pragma unroll
                 for (int r = 0; r < KR; ++r) { CS(CI::YR + r) = y[r]; ysum[r] = 0.0; }
-                CS(CI::SC + CI::OMEGA) = omega;
-                CS(CI::SC + CI::W2) = omega * omega;
-                CS(CI::SC + CI::IW2) = 1.0 / (omega * omega);
-                CS(CI::SC + CI::KRST) = cand;
-                CS(CI::SC + CI::KPREV) = INFINITY;
+                SS(CI::OMEGA) = omega;
+                SS(CI::W2) = omega * omega;
+                SS(CI::IW2) = 1.0 / (omega * omega);
+                SS(CI::KRST) = cand;
+                SS(CI::KPREV) = INFINITY;
                 cnt = 0;
                 since = 0;
             }
@@ -452,7 +454,9 @@ void pdhg_mfma_variant_shape(int v, int* out2) {
 
 size_t pdhg_mfma_lds_bytes(int v) {
     const MfmaVariant& V = kMfmaVariants[v];
-    return (size_t)(4 * 4 * V.TN + 4 * 4 * V.TM + 11) * 64 * sizeof(double);
+    // per-lane vector items + per-scenario scalars (MCold): 17.4 KB for one tile, so LDS admits the
+    // 2 waves per SIMD the registers allow (8 per CU; per-lane scalars made it 21.5 KB: 7 per CU)
+    return ((size_t)(4 * 4 * V.TN + 4 * 4 * V.TM) * 64 + (size_t)MCold<1, 1>::NSC * 16) * sizeof(double);
 }
 
 hipError_t pdhg_mfma_launch(int v, const PdhgArgs& a, hipStream_t stream) {
