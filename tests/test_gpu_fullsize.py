@@ -94,3 +94,65 @@ def test_full_size_properties_and_sampled_parity(case):
         xo = o.nonants(i)
         np.testing.assert_allclose(xg[i], xo, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(xo).max()))
         assert abs(og[i] - o.obj[i]) <= 1e-6 * max(1.0, abs(o.obj[i])), (sample[i], og[i], o.obj[i])
+
+
+def test_hydro_mfma_full_size_properties_and_sampled_parity():
+    """The shared-matrix MFMA kernel at the scale it is chosen for (hydro 3-stage non-uniform tree,
+    20 000 scenarios, bench.py --case hydro --scen 20000): the same certificates and update
+    properties per tree NODE (x̄ of node g = sum over its scenarios of prob_coeff * x, phbase.py:
+    32-112; sum over the node of prob_coeff * W = 0), and a seeded sample re-solved by the oracle
+    with the device's W and per-scenario x̄ (each nonant's slot taken from its scenario's node)."""
+    from mpisppy_amd.examples import hydro
+    S = 20000
+    fan = hydro.synthetic_fanouts(S)
+    names, kw = hydro.scenario_names_creator(S), {"fanouts": fan}
+    ph = PH(_opts(), names, hydro.synthetic_scenario_creator, all_nodenames=hydro.synthetic_nodenames(fan),
+            scenario_creator_kwargs=kw)
+    ph.PH_Prep()
+    assert ph.engine.layout == "mfma"
+    ph.Iter0()
+    _certificates(ph)
+    b = ph.engine.batch
+    # per-scenario slot of every nonant in the node-major x̄ vector
+    slot = b.node_off[b.scen_node[:, b.nonant_level]] + b.nonant_pos[None, :]      # [S, N]
+    pc = b.prob_coeff[:, b.nonant_level]                                              # [S, N]
+
+    x = ph.nonants().copy()
+    W0 = ph.Ws().copy()
+    ph.Compute_Xbar()
+    ph.Update_W()
+    xbar = ph.xbars()
+    xb_host = np.zeros(b.N_tot)
+    np.add.at(xb_host, slot.ravel(), (pc * x).ravel())
+    np.testing.assert_allclose(xbar, xb_host, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(xb_host).max()))
+    xb_s = xbar[slot]
+    W = ph.Ws().copy()
+    np.testing.assert_allclose(W - W0, 1.0 * (x - xb_s), rtol=1e-12, atol=1e-12 * max(1.0, np.abs(x).max()))
+    wsum = np.zeros(b.N_tot)
+    np.add.at(wsum, slot.ravel(), (pc * W).ravel())
+    assert np.abs(wsum).max() <= 1e-9 * max(1.0, np.abs(W).max())
+
+    ph.solve_loop()
+    # hydro's prox objective nearly cancels against its constant (rho/2 sum xbar^2 ~ 1e4 against
+    # objectives of order 1 in some scenarios), so obj - bound relative to 1 + |obj| is no measure
+    # of the solve there: every layout shows up to 1.05e-5 on the same 120 scenarios at relative KKT
+    # <= 1e-9 (tools/hydro_gap_diag.py).  Checked instead: status 0 and each solve's relative KKT
+    # error (primal, dual residuals and the gap relative to the terms' own magnitude, the kernel's
+    # termination test) <= eps; the objective against the oracle relative to that magnitude.
+    assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+    assert ph.engine.get(_lib.F_KKT).max() <= EPS
+    scale = 1.0 + 0.5 * (xb_s ** 2).sum(1)
+    rng = np.random.default_rng(1134)
+    sample = sorted(rng.choice(S, size=6, replace=False).tolist()) + [2802]   # 2802: the largest gap
+    o = oph.OraclePH(_opts(), [names[k] for k in sample], None,
+                     scenarios=[om.hydro_tree(names[k], fanouts=fan) for k in sample])
+    o.W = W[sample].copy()
+    o.xbar = xb_s[sample].copy()
+    o.W_on, o.prox_on = 1, 1
+    xg = ph.nonants()[sample]
+    og = ph.engine.get(_lib.F_OBJ)[sample]
+    for i in range(len(sample)):
+        o.solve_one(i)
+        xo = o.nonants(i)
+        np.testing.assert_allclose(xg[i], xo, rtol=1e-6, atol=1e-6 * max(1.0, np.abs(xo).max()))
+        assert abs(og[i] - o.obj[i]) <= 1e-6 * (abs(o.obj[i]) + scale[sample[i]]), (sample[i], og[i], o.obj[i])
