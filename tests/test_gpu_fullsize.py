@@ -1,5 +1,6 @@
 """Parity at the bench's full sizes (BASELINE.json configs): farmer cm=10 x 10 000 scenarios
-(local kernel), sslp_15_45_10 x 2 048 and netdes x 1 024 (block kernel).
+(local kernel), sslp_15_45_10 x 2 048 and netdes x 1 024 (block kernel), hydro 3-stage tree x 20 000
+(shared-matrix MFMA kernel).
 
 The whole batch is too large for the oracle, so the checks are
 * size-independent properties of every scenario: status 0 (relative KKT <= eps), primal objective
