@@ -54,7 +54,15 @@ hipError_t ph_head_launch(const PhArgs& a, double* packed, double thr, int first
 hipError_t ph_step_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st);
 hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double* gate_host, double seq,
                             hipStream_t st);
-constexpr int kSchedEvery = 4;
+// solves between launch-schedule recomputations (PHG_SCHED_EVERY overrides, for A/B runs)
+static int sched_every() {
+    static const int v = [] {
+        const char* e = getenv("PHG_SCHED_EVERY");
+        const int k = e ? atoi(e) : 0;
+        return k > 0 ? k : 4;
+    }();
+    return v;
+}
 hipError_t eval_obj_launch(int S, int n, int N, const double* x, const double* c, const double* obj_off,
                            const int* nonant_col, const double* xN, const double* W, const double* rho,
                            const double* xbar, const int* xidx, int w_on, int prox_on, double sense,
@@ -169,7 +177,7 @@ struct phg_handle {
     double* gate_host = nullptr;     // fine-grained pinned host copy + sequence word [3]
     long long gate_seq = 0;          // sequence number of the last enqueued gate computation
     bool gate_fused = false;         // the last phg_apply_xbar already computed the gate
-    // the launch schedule is recomputed after every kSchedEvery-th solve (iteration counts move
+    // the launch schedule is recomputed after every sched_every()-th solve (iteration counts move
     // slowly under warm starts; the sort is a latency-bound single-workgroup launch)
     int solves = 0;
     double* rho_k = nullptr;   // [N] copy of rho when it is the same in every scenario (PhArgs::rho_k)
@@ -1786,7 +1794,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     if (timing_event(h, 0, 1)) return -1;
     swap_state(h);
     ++h->swaps;
-    if (o->schedule && (h->solves % kSchedEvery == 0 || !h->have_order)) {
+    if (o->schedule && (h->solves % sched_every() == 0 || !h->have_order)) {
         CK(schedule_launch(h->iters, h->S, a.check_every, h->order, h->stream));
         h->have_order = true;
     }
