@@ -104,6 +104,17 @@ typedef struct phg_opts {
      * round-off (an xbar of first-order solves: farmer 10k sums to 5000 + 2e-7 acres); an exactly
      * fixed infeasible box sends PDHG's dual iterates off along the infeasibility ray instead.     */
     double  fix_tol;
+    /* 1: after the solve, replace every scenario's dual bound (PHG_F_BOUND) by a bound that is valid
+     * whatever the solve's status -- the Lagrangian dual function of the scenario's subproblem at the
+     * solve's dual iterate, made feasible: row duals of the wrong sign for an infinite row bound
+     * zeroed; columns charged against their bounds, infinite ones replaced by bounds implied by the
+     * rows (computed once per batch from the caller's data); reduced-cost infeasibility on a column
+     * with no finite bound either way repaired by shrinking the duals of its rows.  -inf (+inf when
+     * maximising) only when no finite certificate results.  For the bound consumers of spopt.py:
+     * 225-230 (Iter0's trivial bound, spopt.py:377-422 Ebound; the Lagrangian spoke,
+     * lagrangian_bounder.py:21-44) at scenarios that stopped at the iteration limit.  Not with
+     * fix_nonants.                                                                              */
+    int32_t safe_bound;
 } phg_opts;
 
 /* solve modes (mpisppy/phbase.py:670-760: W_on / prox_on toggles) */
@@ -169,6 +180,11 @@ int  phg_plan(const phg_batch* b, int32_t* out8);
  * phg_set of PHG_F_Y keep the caller's row numbering; folded rows read back 0.
  * phg_presolve_info: out2 = {rows folded, rows kept}                                          */
 int  phg_set_presolve(phg_handle* h, int32_t on);
+/* host-only (no device): the column bounds phg_opts.safe_bound uses -- every infinite bound of
+ * scenario s that a row implies replaced by that implied bound (bound propagation over the rows,
+ * widened against round-off), finite ones unchanged; lo, hi are [S*n]; *n_free (may be NULL) = the
+ * columns left with an infinite side in some scenario.  On the batch as given (no presolve).     */
+int  phg_implied_bounds(const phg_batch* b, double* lo, double* hi, int32_t* n_free);
 int  phg_presolve_info(phg_handle* h, int32_t* out2);
 int  phg_load_batch(phg_handle* h, const phg_batch* b);
 int  phg_set(phg_handle* h, int32_t field, const double* host_in);
@@ -260,7 +276,8 @@ int  phg_query(phg_handle* h, int32_t* idle);
 /* launch timing without per-launch synchronisation: phg_timing_reset clears the counters and
  * selects what gets HIP events (enable bit 0: solves, bit 1: PH updates; 0 = none, the
  * production default);
- * phg_timing sums the HIP-event durations of every solve (which = 0) or PH update (which = 1)
+ * phg_timing sums the HIP-event durations of every solve (which = 0), PH update (which = 1: from the
+ * node sums' begin to the W update's end), node-sum launch (2) or W-update / head launch (3)
  * launched since, and the PDHG iterations of all scenarios over those solves              */
 int  phg_timing_reset(phg_handle* h, int32_t enable);
 int  phg_timing(phg_handle* h, int32_t which, double* total_ms, int32_t* launches, int64_t* pdhg_iters);

@@ -35,7 +35,7 @@ class PhgOpts(C.Structure):
                 ("warm_start", C.c_int32), ("fix_nonants", C.c_int32), ("schedule", C.c_int32),
                 ("beta_sufficient", C.c_double), ("beta_necessary", C.c_double),
                 ("beta_artificial", C.c_double), ("primal_weight_theta", C.c_double),
-                ("skip_if_conv_below", C.c_double), ("fix_tol", C.c_double)]
+                ("skip_if_conv_below", C.c_double), ("fix_tol", C.c_double), ("safe_bound", C.c_int32)]
 
 
 (F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART, F_OMEGA,
@@ -55,6 +55,7 @@ SIGNATURES = {
     "phg_sync": (C.c_int, [C.c_void_p]),
     "phg_set_layout": (C.c_int, [C.c_void_p, C.c_int32]),
     "phg_plan": (C.c_int, [C.POINTER(PhgBatch), i32p]),
+    "phg_implied_bounds": (C.c_int, [C.POINTER(PhgBatch), f64p, f64p, i32p]),
     "phg_load_batch": (C.c_int, [C.c_void_p, C.POINTER(PhgBatch)]),
     "phg_set": (C.c_int, [C.c_void_p, C.c_int32, f64p]),
     "phg_get": (C.c_int, [C.c_void_p, C.c_int32, f64p]),

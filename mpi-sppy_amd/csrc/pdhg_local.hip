@@ -38,7 +38,8 @@ struct Cold {
     static constexpr int YDR = 0, IDRD = DD, DLO = 2 * DD, DHI = 3 * DD, SC = 4 * DD;
     // KRST / KPREV hold SQUARED weighted KKT errors; TP / TD the squared termination thresholds
     // (eps (1 + ||b||))^2, (eps (1 + ||c||))^2; W2 / IW2 = omega^2, 1 / omega^2
-    enum { CNORM = 0, BNORM, ETA, PROX, OMEGA, KRST, KPREV, TP, TD, W2, IW2, NSC };
+    // KOFF: the objective constant of the gap test (PdhgArgs::gap_const)
+    enum { CNORM = 0, BNORM, ETA, PROX, OMEGA, KRST, KPREV, TP, TD, W2, IW2, KOFF, NSC };
     static constexpr int NG = SC + NSC;
 };
 template <int LPS, int CPL, int RPL, int D>
@@ -276,13 +277,13 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     auto rel_of = [&](const double* o) {
         const double p = sqrt(o[2]) / (1.0 + GS(CI::SC + CI::BNORM));
         const double d = sqrt(o[3]) / (1.0 + GS(CI::SC + CI::CNORM));
-        const double g = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
+        const double g = fabs(o[4] - o[5]) / gap_den(o[4], o[5], GS(CI::SC + CI::KOFF));
         return fmax(fmax(p, d), g);
     };
     // rel_of(o) <= eps without square roots or divisions
     auto converged = [&](const double* o) {
         return o[2] <= GS(CI::SC + CI::TP) && o[3] <= GS(CI::SC + CI::TD) &&
-               fabs(o[4] - o[5]) <= a.eps * (1.0 + fabs(o[4]) + fabs(o[5]));
+               fabs(o[4] - o[5]) <= a.eps * gap_den(o[4], o[5], GS(CI::SC + CI::KOFF));
     };
     // squared primal-weighted KKT error (PDLP's restart metric)
     auto wkkt2_of = [&](const double* o) {
@@ -391,6 +392,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             rr[3] += b2d;
             GS(CI::SC + CI::CNORM) = sqrt(rr[0]);
             GS(CI::SC + CI::PROX) = rr[1];
+            GS(CI::SC + CI::KOFF) = a.gap_const ? a.obj_off[s] + (a.prox_on ? rr[1] : 0.0) : 0.0;
             const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
             omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
             if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];

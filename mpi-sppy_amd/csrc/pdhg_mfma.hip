@@ -44,7 +44,7 @@ struct MCold {
     static constexpr int KC = 4 * TN, KR = 4 * TM;
     static constexpr int XR = 0, Q = KC, IDC = 2 * KC, C = 3 * KC, YR = 4 * KC, IDR = YR + KR, BLO = IDR + KR,
                          BHI = BLO + KR, SC = BHI + KR;
-    enum { CNORM = 0, BNORM, ETA, PROX, OMEGA, KRST, KPREV, TP, TD, W2, IW2, NSC };
+    enum { CNORM = 0, BNORM, ETA, PROX, OMEGA, KRST, KPREV, TP, TD, W2, IW2, KOFF, NSC };   // KOFF: gap_den's K
     static constexpr int N = SC + NSC;
 };
 
@@ -178,6 +178,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
         ssum_many<4>(rr);
         SS(CI::CNORM) = sqrt(rr[0]);
         SS(CI::PROX) = rr[1];
+        SS(CI::KOFF) = a.gap_const ? a.obj_off[s] + (a.prox_on ? rr[1] : 0.0) : 0.0;
         const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
         omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
         if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
@@ -271,12 +272,12 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
     auto rel_of = [&](const double* o) {
         const double p = sqrt(o[2]) / (1.0 + SS(CI::BNORM));
         const double d = sqrt(o[3]) / (1.0 + SS(CI::CNORM));
-        const double gg = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
+        const double gg = fabs(o[4] - o[5]) / gap_den(o[4], o[5], SS(CI::KOFF));
         return fmax(fmax(p, d), gg);
     };
     auto converged = [&](const double* o) {
         return o[2] <= SS(CI::TP) && o[3] <= SS(CI::TD) &&
-               fabs(o[4] - o[5]) <= a.eps * (1.0 + fabs(o[4]) + fabs(o[5]));
+               fabs(o[4] - o[5]) <= a.eps * gap_den(o[4], o[5], SS(CI::KOFF));
     };
     auto wkkt2_of = [&](const double* o) {
         const double gg = o[4] - o[5];

@@ -235,7 +235,8 @@ __global__ __launch_bounds__(NT) void pdhg_stream_kernel(PdhgArgs a) {
     auto rel_of = [&](const double* o) {
         const double p = sqrt(o[2]) / (1.0 + bnorm);
         const double d = sqrt(o[3]) / (1.0 + cnorm);
-        const double g = fabs(o[4] - o[5]) / (1.0 + fabs(o[4]) + fabs(o[5]));
+        const double g = fabs(o[4] - o[5]) /
+                         gap_den(o[4], o[5], a.gap_const ? a.obj_off[s] + (a.prox_on ? prox_const : 0.0) : 0.0);
         return fmax(fmax(p, d), g);
     };
     auto wkkt_of = [&](const double* o, double w) {

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/phg.h"
@@ -54,6 +55,7 @@ hipError_t ph_head_launch(const PhArgs& a, double* packed, double thr, int first
 hipError_t ph_step_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st);
 hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double* gate_host, double seq,
                             hipStream_t st);
+hipError_t safe_bound_launch(const PdhgArgs& a, const SafeBoundArgs& b, hipStream_t st);
 // solves between launch-schedule recomputations (PHG_SCHED_EVERY overrides, for A/B runs)
 static int sched_every() {
     static const int v = [] {
@@ -165,9 +167,12 @@ struct phg_handle {
     // timing of the last launches (HIP events on the handle's stream)
     // per-launch timing since the last phg_timing_reset: event pairs of every solve (0) and every
     // PH update (1), read only when phg_timing is called -- no per-launch host synchronisation
-    std::vector<hipEvent_t> tev[2];
-    int tcount[2] = {0, 0};
-    int timing_mask = 0;       // bit 0: time solves, bit 1: time PH updates
+    // (2: node sums alone, 3: the W update / head alone; a PH update = node sums + W update, timed
+    // from the node sums' begin to the W update's end, which = 1)
+    std::vector<hipEvent_t> tev[4];
+    int tcount[4] = {0, 0, 0, 0};
+    bool t_open = false;       // a PH update's begin event is recorded, its end not yet
+    int timing_mask = 0;       // bit 0: time solves, bit 1: time PH updates (and their two kernels)
     long long* iters_acc = nullptr;
     // singleton-row presolve (presolve_singletons): rows of the caller's batch -> kept rows
     int presolve = 1;
@@ -182,6 +187,11 @@ struct phg_handle {
     int solves = 0;
     double* rho_k = nullptr;   // [N] copy of rho when it is the same in every scenario (PhArgs::rho_k)
     std::vector<int> row_map;  // original row -> kept row, or -1 (folded into a column bound)
+    // phg_opts.safe_bound (bound.hip): pattern, implied column bounds, repair candidates; the
+    // scratch (SafeBoundArgs::Y, R) is allocated at the first safe-bound solve
+    SafeBoundArgs sb{};
+    // relative-gap test on the whole objective (PdhgArgs::gap_const); PHG_GAP_RAW=1 turns it off
+    int gap_const = 1;
 };
 
 template <class T>
@@ -203,7 +213,7 @@ static int dput(phg_handle* h, T** p, const T* src, size_t count) {
 }
 
 static int timing_event(phg_handle* h, int which, int half) {
-    if (!(h->timing_mask & (1 << which))) return 0;
+    if (!(h->timing_mask & (1 << (which >= 2 ? 1 : which)))) return 0;
     std::vector<hipEvent_t>& v = h->tev[which];
     const size_t idx = 2 * (size_t)h->tcount[which] + half;
     while (v.size() <= idx) {
@@ -258,6 +268,7 @@ int phg_create(int device, phg_handle** out) {
     if (const char* ev = std::getenv("PHG_LOCAL_PERSIST")) h->persist = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("PHG_AVG_EVERY")) h->avg_every = std::max(1, std::atoi(ev));
     if (const char* ev = std::getenv("PHG_FUSE")) h->no_fuse = std::atoi(ev) == 0;
+    if (const char* ev = std::getenv("PHG_GAP_RAW")) h->gap_const = std::atoi(ev) == 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return fail("phg_create: hipStreamCreate failed");
@@ -1419,6 +1430,97 @@ static void presolve_singletons(const phg_batch* in, Presolved& P) {
     P.b.col_hi = P.cu.data();
 }
 
+// Column bounds implied by the rows (for phg_opts.safe_bound, bound.hip), per scenario on the caller's
+// (presolved, unscaled) data: every INFINITE column bound that a row with a finite side and finite
+// activity bounds on its other columns caps is replaced by that cap, widened by a relative 1e-9 of the
+// terms involved (round-off of the activity sums: the box must contain every feasible point; a looser
+// box only weakens the bound by its reduced cost times the slack).  Passes repeat while a bound turned
+// finite (at most 8).  Finite bounds are kept as given.  free_cols: columns left with an infinite side
+// in at least one scenario.
+static void implied_bounds(const phg_batch* b, std::vector<double>& L, std::vector<double>& U,
+                           std::vector<int>& free_cols) {
+    const int S = b->S, n = b->n, m = b->m, nnz = b->nnz;
+    L.assign(b->col_lo, b->col_lo + (size_t)S * n);
+    U.assign(b->col_hi, b->col_hi + (size_t)S * n);
+    std::vector<char> free_any(n, 0);
+    auto one = [&](int s, std::vector<char>& fr) {
+        double* l = L.data() + (size_t)s * n;
+        double* u = U.data() + (size_t)s * n;
+        const double* v = b->vals + (size_t)s * nnz;
+        const double* rlo = b->row_lo + (size_t)s * m;
+        const double* rhi = b->row_hi + (size_t)s * m;
+        auto fin_ = [](double x) { return std::fabs(x) < 1e300; };
+        for (int pass = 0; pass < 8; ++pass) {
+            bool changed = false;
+            for (int i = 0; i < m; ++i) {
+                const double lo = rlo[i], hi = rhi[i];
+                if (!fin_(lo) && !fin_(hi)) continue;
+                double mn = 0.0, mx = 0.0, mag = 0.0;
+                int nmn = 0, nmx = 0;
+                for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) {
+                    const double a = v[p];
+                    const int j = b->colidx[p];
+                    if (a == 0.0) continue;
+                    const double lmin = a > 0 ? l[j] : u[j], lmax = a > 0 ? u[j] : l[j];
+                    if (fin_(lmin)) { mn += a * lmin; mag += std::fabs(a * lmin); } else ++nmn;
+                    if (fin_(lmax)) { mx += a * lmax; mag += std::fabs(a * lmax); } else ++nmx;
+                }
+                if ((nmn > 1 || !fin_(hi)) && (nmx > 1 || !fin_(lo))) continue;
+                for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) {
+                    const double a = v[p];
+                    const int j = b->colidx[p];
+                    if (a == 0.0 || (fin_(l[j]) && fin_(u[j]))) continue;
+                    const double lmin = a > 0 ? l[j] : u[j], lmax = a > 0 ? u[j] : l[j];
+                    // a x_j <= hi - min activity of the other columns
+                    if (fin_(hi) && nmn - (fin_(lmin) ? 0 : 1) == 0) {
+                        const double rest = mn - (fin_(lmin) ? a * lmin : 0.0);
+                        const double cap = (hi - rest) / a;
+                        const double sl = 1e-9 * (std::fabs(cap) + (std::fabs(hi) + mag) / std::fabs(a)) + 1e-12;
+                        if (a > 0 && !fin_(u[j]) && fin_(cap)) { u[j] = cap + sl; changed = true; }
+                        if (a < 0 && !fin_(l[j]) && fin_(cap)) { l[j] = cap - sl; changed = true; }
+                    }
+                    // a x_j >= lo - max activity of the other columns
+                    if (fin_(lo) && nmx - (fin_(lmax) ? 0 : 1) == 0) {
+                        const double rest = mx - (fin_(lmax) ? a * lmax : 0.0);
+                        const double cap = (lo - rest) / a;
+                        const double sl = 1e-9 * (std::fabs(cap) + (std::fabs(lo) + mag) / std::fabs(a)) + 1e-12;
+                        if (a > 0 && !fin_(l[j]) && fin_(cap)) { l[j] = cap - sl; changed = true; }
+                        if (a < 0 && !fin_(u[j]) && fin_(cap)) { u[j] = cap + sl; changed = true; }
+                    }
+                }
+            }
+            if (!changed) break;
+        }
+        for (int j = 0; j < n; ++j)
+            if (!fin_(l[j]) || !fin_(u[j])) fr[j] = 1;
+    };
+    const int nt = std::max(1, std::min<int>(16, std::min<int>((int)std::thread::hardware_concurrency(), S / 64 + 1)));
+    std::vector<std::vector<char>> fr(nt, std::vector<char>(n, 0));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] { for (int s2 = t; s2 < S; s2 += nt) one(s2, fr[t]); });
+    for (auto& x : th) x.join();
+    for (int t = 0; t < nt; ++t)
+        for (int j = 0; j < n; ++j) free_any[j] |= fr[t][j];
+    free_cols.clear();
+    for (int j = 0; j < n; ++j)
+        if (free_any[j]) free_cols.push_back(j);
+}
+
+int phg_implied_bounds(const phg_batch* b, double* lo, double* hi, int32_t* n_free) {
+    if (!b || !lo || !hi) return fail("phg_implied_bounds: null argument");
+    if (b->S <= 0 || b->n <= 0 || b->m <= 0 || !b->rowptr || !b->colidx || !b->vals || !b->col_lo ||
+        !b->col_hi || !b->row_lo || !b->row_hi)
+        return fail("phg_implied_bounds: incomplete batch");
+    std::vector<double> L, U;
+    std::vector<int> fc;
+    implied_bounds(b, L, U, fc);
+    std::memcpy(lo, L.data(), L.size() * sizeof(double));
+    std::memcpy(hi, U.data(), U.size() * sizeof(double));
+    if (n_free) *n_free = (int32_t)fc.size();
+    return 0;
+}
+
 int phg_set_presolve(phg_handle* h, int32_t on) {
     if (!h) return fail("phg_set_presolve: null handle");
     if (h->loaded) return fail("phg_set_presolve: call before phg_load_batch");
@@ -1629,6 +1731,19 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     pa.vals = h->vals; pa.dc = h->dc; pa.dr = h->dr; pa.cl = h->cl; pa.cu = h->cu; pa.rl = h->rl;
     pa.ru = h->ru; pa.eta = h->eta; pa.bnorm = h->bnorm; pa.scratch = scratch;
     CK(prep_launch(pa, h->stream));
+    {   // safe bounds (bound.hip): pattern in CSR / CSC, implied column bounds, repair candidates
+        std::vector<double> il, ih;
+        std::vector<int> fc;
+        implied_bounds(b, il, ih, fc);
+        SafeBoundArgs& sb = h->sb;
+        sb.rowptr = pa.rowptr; sb.colidx = pa.colidx; sb.colptr = pa.colptr; sb.csc_p = pa.csc_p;
+        if (dput(h, &ip, csc_row.data(), nnz)) return -1; sb.rowidx = ip;
+        double* dp;
+        if (dput(h, &dp, il.data(), il.size())) return -1; sb.ilo = dp;
+        if (dput(h, &dp, ih.data(), ih.size())) return -1; sb.ihi = dp;
+        sb.nf = (int)fc.size();
+        if (dput(h, &ip, fc.data(), std::max<size_t>(1, fc.size()))) return -1; sb.free_col = ip;
+    }
     if (h->block_variant >= 0 && build_block_values(h)) return -1;
     if (h->mfma_variant >= 0 && build_mfma_fragments(h, b)) return -1;
     if (h->stream_layout && build_stream_values(h)) return -1;
@@ -1785,6 +1900,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.queue = h->persist ? h->queue : nullptr;
     a.avg_every = h->avg_every;
     a.bd = h->bd;
+    a.gap_const = h->gap_const;
     if (h->border_layout) CK(pdhg_border_launch(a, h->stream));
     else if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));
     else if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
@@ -1792,6 +1908,13 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
     if (timing_event(h, 0, 1)) return -1;
+    if (o->safe_bound && !o->fix_nonants) {   // bound.hip: certificates whatever the statuses
+        if (!h->sb.Y) {
+            if (dalloc(h, &h->sb.Y, (size_t)h->S * h->m)) return -1;
+            if (dalloc(h, &h->sb.R, (size_t)h->S * h->n)) return -1;
+        }
+        CK(safe_bound_launch(a, h->sb, h->stream));
+    }
     swap_state(h);
     ++h->swaps;
     if (o->schedule && (h->solves % sched_every() == 0 || !h->have_order)) {
@@ -1805,8 +1928,11 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
 int phg_node_sums(phg_handle* h, double* dev_nodesum) {
     if (!h || !h->loaded) return fail("phg_node_sums: no batch loaded");
     CK(hipSetDevice(h->device));
-    if (timing_event(h, 1, 0)) return -1;
+    if (!h->t_open && timing_event(h, 1, 0)) return -1;
+    h->t_open = (h->timing_mask & 2) != 0;
+    if (timing_event(h, 2, 0)) return -1;
     CK(node_sums_launch(h->ph, dev_nodesum ? dev_nodesum : h->nodesum, h->stream));
+    if (timing_event(h, 2, 1)) return -1;
     return 0;
 }
 
@@ -1820,9 +1946,13 @@ int phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpar
         a.gate_host = h->gate_host;
         a.gate_seq = (double)(++h->gate_seq);
     }
+    if (!h->t_open && timing_event(h, 1, 0)) return -1;
+    if (timing_event(h, 3, 0)) return -1;
     CK(w_update_launch(a, dev_nodesum ? dev_nodesum : h->nodesum,
                        dev_convpart ? dev_convpart : h->convpart, h->stream));
+    if (timing_event(h, 3, 1)) return -1;
     if (timing_event(h, 1, 1)) return -1;
+    h->t_open = false;
     return 0;
 }
 
@@ -1833,9 +1963,12 @@ int phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t fi
     a.gate = h->gate;
     a.gate_host = h->gate_host;
     a.gate_seq = (double)(++h->gate_seq);
-    if (timing_event(h, 1, 0)) return -1;
+    if (!h->t_open && timing_event(h, 1, 0)) return -1;
+    if (timing_event(h, 3, 0)) return -1;
     CK(ph_head_launch(a, dev_packed ? dev_packed : h->packed, convthresh, first, h->stream));
+    if (timing_event(h, 3, 1)) return -1;
     if (timing_event(h, 1, 1)) return -1;
+    h->t_open = false;
     h->gate_fused = false;
     return 0;
 }
@@ -1854,9 +1987,10 @@ int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fu
     a.gate = h->gate;
     a.gate_host = h->gate_host;
     a.gate_seq = (double)(++h->gate_seq);
-    if (timing_event(h, 1, 0)) return -1;
+    if (!h->t_open && timing_event(h, 1, 0)) return -1;
     CK(ph_step_launch(a, h->packed, convthresh, first, h->stream));
     if (timing_event(h, 1, 1)) return -1;
+    h->t_open = false;
     h->gate_fused = false;
     return 0;
 }
@@ -2021,7 +2155,8 @@ int phg_exchange_buffers(phg_handle* h, double** ns, double** cp) {
 int phg_timing_reset(phg_handle* h, int32_t enable) {
     if (!h || !h->loaded) return fail("phg_timing_reset: no batch loaded");
     CK(hipStreamSynchronize(h->stream));
-    h->tcount[0] = h->tcount[1] = 0;
+    for (int& c : h->tcount) c = 0;
+    h->t_open = false;
     h->timing_mask = enable & 3;
     CK(hipMemsetAsync(h->iters_acc, 0, (size_t)h->S * sizeof(long long), h->stream));
     CK(hipStreamSynchronize(h->stream));
@@ -2030,7 +2165,8 @@ int phg_timing_reset(phg_handle* h, int32_t enable) {
 
 int phg_timing(phg_handle* h, int32_t which, double* total_ms, int32_t* launches, int64_t* pdhg_iters) {
     if (!h || !h->loaded) return fail("phg_timing: no batch loaded");
-    if (which < 0 || which > 1) return fail("phg_timing: which must be 0 (solves) or 1 (PH updates)");
+    if (which < 0 || which > 3)
+        return fail("phg_timing: which must be 0 (solves), 1 (PH updates), 2 (node sums) or 3 (W updates)");
     CK(hipStreamSynchronize(h->stream));
     double tot = 0.0;
     for (int k = 0; k < h->tcount[which]; ++k) {

@@ -190,6 +190,31 @@ struct PdhgArgs {
     // between launches), or nullptr: one work item per lane group
     unsigned* queue;
     int avg_every;          // lane-local kernel: the average iterate's KKT at every avg_every-th check (1: all)
+    // 1: the relative gap is taken on the subproblem's whole objective, constant included
+    // (obj_off + the prox constant rho/2 ||xbar||^2), as PDLP counts an objective offset:
+    //     |p - d| <= eps (1 + |p + K| + |d + K|)
+    // -- without K the test is relative to |p|, |d| of the constant-free objective, which the prox
+    // term inflates to ~rho/2 ||xbar||^2 (hydro: 1e4 against objectives of order 1); 0: the
+    // constant-free form (PHG_GAP_RAW=1, A/B runs)
+    int gap_const;
+};
+
+// relative-gap denominator of the termination test (PdhgArgs::gap_const): K = the objective constant
+__device__ __forceinline__ double gap_den(double p, double d, double K) {
+    return 1.0 + fabs(p + K) + fabs(d + K);
+}
+
+// Safe per-scenario dual bound after a solve (bound.hip, phg_opts.safe_bound): the shared pattern in
+// CSR and CSC, the column bounds with every infinite side replaced by one implied by the rows (raw,
+// built once per batch on the host: phg_api.hip implied_bounds), the columns that keep an infinite
+// side in some scenario (the repair candidates), and per-scenario scratch for the duals / reduced costs
+struct SafeBoundArgs {
+    const int *rowptr, *colidx;          // [m+1], [nnz]
+    const int *colptr, *rowidx, *csc_p;  // [n+1], [nnz] row of CSC entry, [nnz] its CSR position
+    const double *ilo, *ihi;             // [S*n] unscaled
+    const int* free_col;                 // [nf]
+    int nf;
+    double *Y, *R;                       // [S*m], [S*n]
 };
 
 struct PrepArgs {

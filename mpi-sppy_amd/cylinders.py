@@ -107,7 +107,8 @@ class _BoundSpoke:
 
 class LagrangianOuterBound(_BoundSpoke):
     """``lagrangian_bounder.py``: solve every scenario with the hub's W, prox off; the outer bound
-    is sum_s p_s (dual bound_s) -- the PDHG dual objective, a valid Lagrangian bound."""
+    is sum_s p_s (dual bound_s) -- each a weak-duality certificate of the scenario's Lagrangian
+    subproblem from its dual iterate (``phg_opts.safe_bound``), valid whatever the solve's status."""
     converger_spoke_char = "L"
     bound_kind = "outer"
 
@@ -116,20 +117,19 @@ class LagrangianOuterBound(_BoundSpoke):
         o = self._solve_opts()
         self.engine.solve(1, 0, eps=o["pdhg_eps"], max_iter=o["pdhg_max_iter"],
                           check_every=o["pdhg_check_every"], warm_start=1 if self.launches else 0,
-                          schedule=o["pdhg_schedule"])
+                          schedule=o["pdhg_schedule"], safe_bound=True)
         return True
 
     def _collect(self):
-        # the PDHG dual objective is a valid Lagrangian bound only where the solve reached the KKT
-        # tolerance: an iteration-limited (status 1) or failed (2) scenario's dual iterate can be
-        # infeasible, and its "bound" could overshoot -- then this spoke reports nothing this round
+        # every scenario's bound is a certificate (safe_bound); only a scenario whose dual iterate
+        # gives none (-inf, or a NaN solve) voids this round's bound
         st = self.engine.get_i32(_lib.I_STATUS)
-        ok = float((st != 0).sum() == 0)
+        b = self.engine.get(_lib.F_BOUND)
+        ok = float(bool(np.isfinite(b).all() and (st != 2).all()))
         if self.hub_opt.n_proc > 1:
             ok = float(self.hub_opt.mpicomm.allreduce_scalar(1.0 - ok) == 0.0)
         if not ok:
             return None
-        b = self.engine.get(_lib.F_BOUND)
         p = self.engine.batch.prob
         return self._rank_fsum([p[k] * b[k] for k in range(len(b))])
 
@@ -279,11 +279,12 @@ def evaluate_xhat(opt, xhat, eps=None, max_iter=200000, fix_tol=0.0, feas_tol=1e
         eng.close()
 
 
-def evaluate_lagrangian(opt, eps=None, max_iter=1000000):
+def evaluate_lagrangian(opt, eps=None, max_iter=200000):
     """Lagrangian outer bound with ``opt``'s current W (``lagrangian_bounder.py:21-44``): every
     local scenario with W on and prox off, one batched solve on a temporary handle; sum_s p_s
-    bound_s (the PDHG dual objective, valid at KKT-optimal points), or None if any scenario did
-    not reach the tolerance."""
+    bound_s, each a weak-duality certificate from the scenario's dual iterate (``phg_opts.
+    safe_bound``: valid also where a solve stops at ``max_iter``), or None if some scenario's
+    iterate certifies nothing (-inf)."""
     he = opt.engine
     dev = 0
     try:
@@ -298,16 +299,16 @@ def evaluate_lagrangian(opt, eps=None, max_iter=1000000):
         eng.copy_from(he, _lib.F_W)
         o = opt._solver_opts()
         eng.solve(1, 0, eps=eps or o["pdhg_eps"], max_iter=max_iter, check_every=o["pdhg_check_every"],
-                  warm_start=0, schedule=False)
+                  warm_start=0, schedule=False, safe_bound=True)
         eng.sync()
         st = eng.get_i32(_lib.I_STATUS)
         evaluate_lagrangian.last_status_counts = np.bincount(st, minlength=3).tolist()
-        bad = float((st != 0).sum())
+        b = eng.get(_lib.F_BOUND)
+        bad = float((~np.isfinite(b)).sum() + (st == 2).sum())
         if opt.n_proc > 1:
             bad = opt.mpicomm.allreduce_scalar(bad)
         if bad:
             return None
-        b = eng.get(_lib.F_BOUND)
         p = eng.batch.prob
         return opt._rank_fsum([p[k] * b[k] for k in range(len(b))])
     finally:

@@ -132,6 +132,19 @@ def plan_layout(batch):
             "lanes_used": int(out[6])}
 
 
+def implied_bounds(batch):
+    """Host-only: the column bounds the safe outer bounds use (``phg_implied_bounds``): (lo, hi) as
+    [S, n] arrays and the number of columns left with an infinite side."""
+    lib = _lib.load()
+    b, keep = batch.c_struct()
+    lo = np.empty(batch.S * batch.n)
+    hi = np.empty(batch.S * batch.n)
+    nf = np.zeros(1, np.int32)
+    _lib.check(lib.phg_implied_bounds(__import__("ctypes").byref(b), ptr(lo), ptr(hi), ptr(nf)))
+    del keep
+    return lo.reshape(batch.S, batch.n), hi.reshape(batch.S, batch.n), int(nf[0])
+
+
 class Engine:
     """One libphg handle on one GPU (no CPU fallback: raises if the library or device is missing)."""
 
@@ -219,10 +232,14 @@ class Engine:
 
     # ------------------------------------------------------------------ hot path
     def solve(self, w_on, prox_on, eps=1e-9, max_iter=100000, check_every=32, warm_start=3,
-              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0), theta=0.0, skip_below=0.0, fix_tol=0.0):
+              fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0), theta=0.0, skip_below=0.0, fix_tol=0.0,
+              safe_bound=False):
+        """safe_bound: every scenario's F_BOUND is a valid outer bound whatever its status (bound.hip;
+        -inf / +inf only where the dual iterate yields no finite certificate)."""
         o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(warm_start),
                          int(bool(fix_nonants)), int(bool(schedule)), *[float(v) for v in beta],
-                         float(theta), float(skip_below), float(fix_tol))
+                         float(theta), float(skip_below), float(fix_tol), int(bool(safe_bound)))
+        self.last_safe_bound = bool(safe_bound) and not fix_nonants
         import ctypes
         _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))
 

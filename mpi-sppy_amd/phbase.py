@@ -188,10 +188,15 @@ class PHBase(SPBase):
     # ------------------------------------------------------------------------------- solves
     def solve_loop(self, solver_options=None, use_scenarios_not_subproblems=False, dtiming=False,
                    dis_W=False, dis_prox=False, gripe=False, disable_pyomo_signal_handling=False,
-                   tee=False, verbose=False, need_solution=True, warm_start=True, skip_below=0.0):
+                   tee=False, verbose=False, need_solution=True, warm_start=True, skip_below=0.0,
+                   safe_bound=None):
         """``phbase.py:522-603`` + ``spopt.py:250-341``: one batched launch for all local scenarios.
         skip_below > 0 makes the launch a device-side no-op when the conv of the last
-        ``engine.conv_start`` is below it (see :meth:`update_and_solve`)."""
+        ``engine.conv_start`` is below it (see :meth:`update_and_solve`).  safe_bound (default: the
+        ``pdhg_safe_bound`` option, on) makes every scenario's outer bound valid whatever its status
+        (``phg_opts.safe_bound``); the pipelined hub solves leave it off (nothing reads their bounds)."""
+        if safe_bound is None:
+            safe_bound = bool(self.options.get("pdhg_safe_bound", True))
         saved = (self.W_on, self.prox_on)
         if dis_W:
             self._disable_W()
@@ -210,7 +215,7 @@ class PHBase(SPBase):
                           warm_start=(1 | _omega_bits(o["pdhg_keep_omega"])) if warm_start else 0,
                           schedule=o["pdhg_schedule"],
                           beta=(o["pdhg_beta_sufficient"], o["pdhg_beta_necessary"], o["pdhg_beta_artificial"]),
-                          theta=o["pdhg_primal_weight_theta"], skip_below=skip_below)
+                          theta=o["pdhg_primal_weight_theta"], skip_below=skip_below, safe_bound=safe_bound)
         self.solve_count += self.engine.S
         # The launch is asynchronous: the statuses reach the host with the next convergence
         # readback (phg_solve_summary, checked in convergence_diff), so a PH iteration costs one
@@ -308,7 +313,7 @@ class PHBase(SPBase):
         else:   # one GPU: node sums and the gated W update in one launch (phg_ph_step)
             eng.ph_step(thr, first)
         self.solve_loop(solver_options=self.current_solver_options, gripe=verbose, verbose=verbose,
-                        skip_below=thr if thr > 0 else 0.0)
+                        skip_below=thr if thr > 0 else 0.0, safe_bound=False)
         self._spec_pending = True
         conv = eng.conv_wait()
         if not first:
@@ -356,14 +361,18 @@ class PHBase(SPBase):
         return self.mpicomm.allreduce_scalar(local) if self.n_proc > 1 else local
 
     def _valid_bounds(self):
-        """Per-scenario outer bounds of the last solve, model sense.  The PDHG dual objective is a
-        valid bound only at a KKT-optimal point (status 0): at an iteration-limited or failed
-        scenario the dual iterate may be infeasible on infinite-bound columns, so its bound is
-        replaced by the trivial one (-inf when minimising, +inf when maximising), as a solver that
-        reports no Lower_bound would leave it (spopt.py:225-230)."""
+        """Per-scenario outer bounds of the last solve, model sense.  With safe bounds (the default
+        for every solve whose bounds are read, ``phg_opts.safe_bound``) each is a weak-duality
+        certificate whatever the scenario's status -- -inf / +inf where none exists, as a solver that
+        reports no Lower_bound would leave it (spopt.py:225-230).  Without, the PDHG dual objective
+        counts only at a KKT-optimal point (status 0): an iteration-limited or failed scenario's dual
+        iterate may be infeasible on infinite-bound columns, so its bound is the trivial one."""
         b = self.engine.get(_lib.F_BOUND)
         self._statuses()
-        bad = self._status != 0
+        if getattr(self.engine, "last_safe_bound", False):
+            bad = (self._status == 2) | ~np.isfinite(b)
+        else:
+            bad = self._status != 0
         if bad.any():
             b = b.copy()
             b[bad] = -math.inf if self.is_minimizing else math.inf

@@ -81,20 +81,104 @@ def test_wheel_hub_and_spokes_gap():
     assert wheel.spcomm.opt._PHIter < 200
 
 
-def test_bounds_invalid_at_iteration_cap():
-    """An iteration-limited PDHG solve gives no bound (ADVICE: a dual iterate that has not reached
-    the KKT tolerance can overshoot): Iter0's trivial bound is -inf (farmer minimises) and the
-    Lagrangian spoke reports nothing, when the solves are capped at 64 PDHG iterations."""
-    cap = {"pdhg_max_iter": 64}
-    ph = _ph(3, 1, iter0_solver_options=cap, iterk_solver_options=cap, PHIterLimit=2)
+def _np_safe_bound(batch, y, c_min, lo, hi, sense, off):
+    """numpy restatement of bound.hip for an LP (no prox), unscaled: the duals sign-projected onto
+    the finite row bounds, r = c - A^T y, the free columns' reduced costs repaired by moving their
+    rows' duals toward 0 (free columns ascending, each column's rows ascending), then the
+    certificate sum_i y_i (lo_i | hi_i) + sum_j min over [lo_j, hi_j] of r_j x_j."""
+    m, n = batch.m, batch.n
+    rp, ci = batch.rowptr, batch.colidx
+    rows = np.repeat(np.arange(m), np.diff(rp))
+    out = []
+    for s in range(batch.S):
+        v = batch.vals[s]
+        Y = y[s].copy()
+        Y[(Y > 0) & ~np.isfinite(batch.rl[s])] = 0.0
+        Y[(Y < 0) & ~np.isfinite(batch.ru[s])] = 0.0
+        R = c_min[s] - np.bincount(ci, weights=v * Y[rows], minlength=n)
+        free = [j for j in range(n) if not (np.isfinite(lo[:, j]).all() and np.isfinite(hi[:, j]).all())]
+        for _ in range(4):
+            anyv = False
+            for j in free:
+                r = R[j]
+                if r < 0 and not np.isfinite(hi[s, j]):
+                    need, d = -r, 1
+                elif r > 0 and not np.isfinite(lo[s, j]):
+                    need, d = r, -1
+                else:
+                    continue
+                anyv = True
+                for p in np.nonzero(ci == j)[0]:
+                    if need <= 0:
+                        break
+                    i, av = rows[p], v[p]
+                    cap = d * av * Y[i]
+                    if not cap > 0:
+                        continue
+                    dl = min(need, cap)
+                    y1 = 0.0 if dl == cap else Y[i] - d * dl / av
+                    dy = y1 - Y[i]
+                    Y[i] = y1
+                    R[ci[rp[i]:rp[i + 1]]] -= v[rp[i]:rp[i + 1]] * dy
+                    need -= dl
+            if not anyv:
+                break
+        t = np.sum(np.where(Y > 0, Y * np.where(Y > 0, batch.rl[s], 0), np.where(Y < 0, Y * batch.ru[s], 0)))
+        with np.errstate(invalid="ignore"):
+            t += np.sum(np.where(R > 0, R * lo[s], np.where(R < 0, R * hi[s], 0.0)))
+        out.append(sense * (t + off[s]))
+    return np.array(out)
+
+
+@pytest.mark.parametrize("cap", [16, 64, 256])
+def test_safe_bounds_at_iteration_cap(cap):
+    """Solves stopped at the PDHG iteration cap still give VALID bounds (phg_opts.safe_bound,
+    bound.hip): Iter0's trivial bound and the Lagrangian spoke's bound are finite and at or below
+    the exact LP values (the oracle's HiGHS), and equal to the numpy restatement of the certificate
+    built from the device's dual iterate (presolve off, so the rows are the caller's).  With the
+    safe bounds switched off the old behaviour holds: no bound at the cap."""
+    from mpisppy_amd.engine import implied_bounds
+    cp = {"pdhg_max_iter": cap}
+    ph = _ph(3, 1, iter0_solver_options=cp, iterk_solver_options=cp, PHIterLimit=3, pdhg_presolve=False)
     ph.PH_Prep()
     tb = ph.Iter0()
     assert (ph.engine.get_i32(_lib.I_STATUS) == 1).all()
-    assert tb == -np.inf
-    sp = LagrangianOuterBound(ph)
+    o = oph.OraclePH(_opts(), om.farmer_names(3), om.farmer, dict(crops_multiplier=1, num_scens=3))
+    otb = o.Iter0()
+    assert np.isfinite(tb) and tb <= otb + 1e-9 * abs(otb), (tb, otb)
+    b = ph.engine.batch
+    lo, hi, _ = implied_bounds(b)
+    y = ph.engine.get(_lib.F_Y).reshape(b.S, b.m)
+    want = _np_safe_bound(b, y, b.sense * b.c, lo, hi, b.sense, b.sense * b.off)
+    got = ph.engine.get(_lib.F_BOUND)
+    np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-9)
+    ph.iterk_loop()
+    sp = LagrangianOuterBound(ph, options={"pdhg_max_iter": cap})
     sp.update()
-    assert sp.finalize() is None
+    lb = sp.finalize()
+    olb = o.lagrangian_bound(ph.Ws())
+    assert lb is not None and lb <= olb + 1e-9 * abs(olb), (lb, olb)
     sp.close()
+    # safe bounds off: an iteration-limited solve certifies nothing
+    ph2 = _ph(3, 1, iter0_solver_options=cp, PHIterLimit=1, pdhg_safe_bound=False)
+    ph2.PH_Prep()
+    assert ph2.Iter0() == -np.inf
+
+
+def test_safe_bounds_converged_match_exact():
+    """At convergence the safe certificate is the LP optimum: Iter0 trivial bound of farmer 30
+    scenarios (cm=1) within 1e-7 of the oracle's, and the reference's pinned -137846 (3 s.f.,
+    test_aph.py:249-253)."""
+    names = [f"Scenario{k}" for k in range(1, 31)]
+    ph = PH(_opts(PHIterLimit=1), names, farmer.scenario_creator,
+            scenario_creator_kwargs={"crops_multiplier": 1, "num_scens": 30})
+    ph.PH_Prep()
+    tb = ph.Iter0()
+    o = oph.OraclePH(_opts(), names, om.farmer, dict(crops_multiplier=1, num_scens=30))
+    otb = o.Iter0()
+    assert tb <= otb + 1e-9 * abs(otb)
+    assert abs(tb - otb) <= 1e-7 * abs(otb), (tb, otb)
+    assert round(tb, -3) == -138000.0
 
 
 def test_spoke_copy_ordered_against_queued_hub_updates():

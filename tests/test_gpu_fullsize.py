@@ -134,17 +134,13 @@ def test_hydro_mfma_full_size_properties_and_sampled_parity():
     assert np.abs(wsum).max() <= 1e-9 * max(1.0, np.abs(W).max())
 
     ph.solve_loop()
-    # hydro's prox objective nearly cancels against its constant (rho/2 sum xbar^2 ~ 1e4 against
-    # objectives of order 1 in some scenarios), so obj - bound relative to 1 + |obj| is no measure
-    # of the solve there: every layout shows up to 1.05e-5 on the same 120 scenarios at relative KKT
-    # <= 1e-9 (tools/hydro_gap_diag.py).  Checked instead: status 0 and each solve's relative KKT
-    # error (primal, dual residuals and the gap relative to the terms' own magnitude, the kernel's
-    # termination test) <= eps; the objective against the oracle relative to that magnitude.
-    assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+    # each prox-QP's own certificate: the relative gap of the termination test is on the whole
+    # objective, the prox constant rho/2 ||xbar||^2 (~1e4 against objectives of order 1 in some
+    # scenarios) included (PdhgArgs::gap_const) -- so obj - bound is 1e-6-tight relative to 1 + |obj|
+    _certificates(ph)
     assert ph.engine.get(_lib.F_KKT).max() <= EPS
-    scale = 1.0 + 0.5 * (xb_s ** 2).sum(1)
     rng = np.random.default_rng(1134)
-    sample = sorted(rng.choice(S, size=6, replace=False).tolist()) + [2802]   # 2802: the largest gap
+    sample = sorted(rng.choice(S, size=6, replace=False).tolist()) + [2802]   # 2802: the largest gap in r02
     o = oph.OraclePH(_opts(), [names[k] for k in sample], None,
                      scenarios=[om.hydro_tree(names[k], fanouts=fan) for k in sample])
     o.W = W[sample].copy()
@@ -156,4 +152,4 @@ def test_hydro_mfma_full_size_properties_and_sampled_parity():
         o.solve_one(i)
         xo = o.nonants(i)
         np.testing.assert_allclose(xg[i], xo, rtol=1e-6, atol=1e-6 * max(1.0, np.abs(xo).max()))
-        assert abs(og[i] - o.obj[i]) <= 1e-6 * (abs(o.obj[i]) + scale[sample[i]]), (sample[i], og[i], o.obj[i])
+        assert abs(og[i] - o.obj[i]) <= 1e-6 * max(1.0, abs(o.obj[i])), (sample[i], og[i], o.obj[i])

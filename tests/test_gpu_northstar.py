@@ -14,8 +14,8 @@ bench's options) to conv < 1e-4 through the C ABI, then:
 * the converged root xbar fixed in every scenario (the xhat evaluation, ``xhat_eval.py:102-170``;
   first-stage rows checked to 1e-7 relative, see ``cylinders.evaluate_xhat``) gives an inner bound
   >= EF - 1e-7 relative (first-order solves at eps 1e-9) and within 1e-6;
-* the Lagrangian bound with the converged W (``lagrangian_bounder.py:21-44``) is valid (<= EF);
-  its gap is reported (W is only as converged as PH at 1e-4);
+* the Lagrangian bound with the converged W (``lagrangian_bounder.py:21-44``) exists, is valid
+  (<= EF) and is within 1e-4 of it at S = 1 000 and 10 000 (2e-4 at S = 30);
 * the converged xbar against the EF's first-stage solution (reported; asserted loosely: the EF
   optimum's first stage need not be unique).
 
@@ -78,13 +78,12 @@ def test_farmer_converged_ph_vs_ef(S):
     assert tb <= efo                                   # the trivial bound is an outer bound
     # inner bound: at or above the EF optimum up to the solves' tolerance
     assert inner is not None and -1e-7 <= rin <= 1e-6
-    # Lagrangian bound with the W of conv < 1e-4: valid (<= EF) but not tight to 1e-6 -- W is only
-    # as converged as PH (S=30: 1e-4 relative below EF).  None = some scenario's LP did not reach
-    # the KKT tolerance within the cap, so no valid bound is claimed (cylinders.evaluate_lagrangian)
-    if outer is None:
-        print("Lagrangian: no bound (statuses", cylinders.evaluate_lagrangian.last_status_counts, ")")
-    else:
-        assert -1e-3 <= rout <= 1e-7
+    # Lagrangian bound with the W of conv < 1e-4: valid (<= EF) whatever the LP statuses (every
+    # scenario's bound is a weak-duality certificate of its dual iterate, phg_opts.safe_bound), and
+    # within 1e-4 of the EF -- W is only as converged as PH at 1e-4
+    print("Lagrangian statuses", cylinders.evaluate_lagrangian.last_status_counts)
+    assert outer is not None
+    assert -(1e-4 if S >= 1000 else 2e-4) <= rout <= 1e-9
     assert dx <= 1.0                                    # acres; reported above at full precision
 
 

@@ -175,25 +175,28 @@ def test_prox_qp_solves_vs_oracle(S, cm, layout):
         np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6)
 
 
+@pytest.mark.parametrize("check_every", [32, 64])
 @pytest.mark.parametrize("layout", ["gather", "block", "mfma"])
 @pytest.mark.parametrize("tree", ["bf33", (2, 1, 4), (5, 15, 30)])
-def test_hydro_prox_qp_solves_vs_oracle(tree, layout):
+def test_hydro_prox_qp_solves_vs_oracle(tree, layout, check_every):
     """Multistage prox-QPs with identical W and per-NODE xbar in both solvers (the xbar slot of each
     nonant comes from its scenario's node at that stage, xidx): strictly convex in x_N, so the
-    nonants are unique -- 1e-6 -- and so are the objectives (1e-6).  Covers the uniform 3x3 tree of
-    the reference (hydro.py) and non-uniform synthetic trees."""
+    nonants are unique -- 1e-6 -- and so are the objectives (1e-6), at either restart-check cadence
+    (the relative gap is measured on the whole objective, prox constant included:
+    PdhgArgs::gap_const), and each solve's own certificate obj - bound <= 1e-6 (1 + |obj|).  Covers
+    the uniform 3x3 tree of the reference (hydro.py) and non-uniform synthetic trees."""
     if tree == "bf33":
         bf = [3, 3]
         names, nodenames = hydro.scenario_names_creator(9), create_nodenames_from_branching_factors(bf)
-        ph = PH(_opts(pdhg_layout=layout), names, hydro.scenario_creator, all_nodenames=nodenames,
-                scenario_creator_kwargs={"branching_factors": bf})
+        ph = PH(_opts(pdhg_layout=layout, pdhg_check_every=check_every), names, hydro.scenario_creator,
+                all_nodenames=nodenames, scenario_creator_kwargs={"branching_factors": bf})
         o = oph.OraclePH(_opts(PHIterLimit=3), om.hydro_names(9), om.hydro, {})
     else:
         S = sum(tree)
         kw = {"fanouts": tree}
         nodenames = hydro.synthetic_nodenames(tree)
-        ph = PH(_opts(pdhg_layout=layout), hydro.scenario_names_creator(S), hydro.synthetic_scenario_creator,
-                all_nodenames=nodenames, scenario_creator_kwargs=kw)
+        ph = PH(_opts(pdhg_layout=layout, pdhg_check_every=check_every), hydro.scenario_names_creator(S),
+                hydro.synthetic_scenario_creator, all_nodenames=nodenames, scenario_creator_kwargs=kw)
         o = oph.OraclePH(_opts(PHIterLimit=3), om.hydro_names(S), om.hydro_tree, kw)
     ph.PH_Prep()
     ph.Iter0()
@@ -211,6 +214,8 @@ def test_hydro_prox_qp_solves_vs_oracle(tree, layout):
         xo = np.array([o.nonants(k) for k in range(S)])
         np.testing.assert_allclose(xg, xo, rtol=1e-6, atol=1e-6 * max(1.0, np.abs(xo).max()))
         np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6, atol=1e-6)
+        obj, bnd = ph.engine.get(_lib.F_OBJ), ph.engine.get(_lib.F_BOUND)
+        assert (np.abs(obj - bnd) / (1.0 + np.abs(obj))).max() <= 1e-6
 
 
 # ----------------------------------------------------------------------------- full PH vs fixtures

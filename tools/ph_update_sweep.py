@@ -4,9 +4,11 @@ for the >= 60 % claim").
 A synthetic two-stage batch -- S scenarios with N nonants each, one dense row (sum x <= N) -- is
 loaded through the C ABI (no solves), the nonants are set to seeded random values, and
 node_sums + W update + conv (phg_node_sums / phg_apply_xbar / phg_conv_start+wait) are timed with
-the library's HIP events over R repetitions.  Algorithmic bytes per update:
-8 S N (x read, W read, W write, rho read) + 8 S + 16 N_tot.  The result is checked on the host
-(xbar = mean of the nonants, W = rho (x - xbar)) before timing.
+the library's HIP events over R repetitions (the update from the node sums' begin to the W update's
+end, and each kernel alone).  Algorithmic bytes per update:
+8 S N (x read, W read, W write, [rho per scenario ? 1 : 0] rho read) + 8 S + 16 N_tot -- rho is the
+same in every scenario here (defaultPHrho), so the W update reads its [N] copy: 3 streams.  The
+result is checked on the host (xbar = mean of the nonants, W = rho (x - xbar)) before timing.
 
 Usage: python tools/ph_update_sweep.py [OUT_JSON]
 """
@@ -87,13 +89,21 @@ def run(S, N, reps=20):
         eng.conv_start()
         eng.conv_wait()
     ms, n_upd, _ = eng.timing(1)
+    ns_ms, n_ns, _ = eng.timing(2)
+    wu_ms, n_wu, _ = eng.timing(3)
     eng.timing_reset(solves=False, updates=False)
     eng.close()
     avg_s = ms / n_upd / 1e3
-    alg = 8 * S * N * 4 + 8 * S + 16 * N
+    alg = 8 * S * N * 3 + 8 * S + 16 * N
     gbs = alg / avg_s / 1e9
+    ns_s, wu_s = ns_ms / max(1, n_ns) / 1e3, wu_ms / max(1, n_wu) / 1e3
     return {"S": S, "N": N, "SN": S * N, "avg_us": round(avg_s * 1e6, 2), "bytes_per_update": alg,
             "achieved_GBs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4), "updates": n_upd,
+            "node_sums_us": round(ns_s * 1e6, 2), "w_update_us": round(wu_s * 1e6, 2),
+            # each kernel on its own algorithmic bytes: node sums read x (8 S N), the W update reads x
+            # and W and writes W (24 S N)
+            "node_sums_GBs": round(8 * S * N / ns_s / 1e9, 1) if n_ns else None,
+            "w_update_GBs": round(24 * S * N / wu_s / 1e9, 1) if n_wu else None,
             "check_ok": bool(ok), "err_xbar": err_xbar, "err_w": err_w, "setup_s": round(setup, 2)}
 
 
@@ -110,7 +120,7 @@ def main():
         out.append(r)
     if len(sys.argv) > 1:
         json.dump({"kernel": "node_sums_kernel + w_update_kernel (+ fused conv gate)",
-                   "bytes_formula": "8*S*N*4 + 8*S + 16*N_tot (SURVEY 8(d)3)",
+                   "bytes_formula": "8*S*N*3 + 8*S + 16*N_tot (SURVEY 8(d)3, rho shared: no rho stream)",
                    "timing": "HIP events on the library stream around each update (phg_timing(1))",
                    "results": out}, open(sys.argv[1], "w"), indent=1)
 
