@@ -104,8 +104,9 @@ typedef struct phg_opts {
      * round-off (an xbar of first-order solves: farmer 10k sums to 5000 + 2e-7 acres); an exactly
      * fixed infeasible box sends PDHG's dual iterates off along the infeasibility ray instead.     */
     double  fix_tol;
-    /* 1: after the solve, replace every scenario's dual bound (PHG_F_BOUND) by a bound that is valid
-     * whatever the solve's status -- the Lagrangian dual function of the scenario's subproblem at the
+    /* 1: after the solve, replace the dual bound (PHG_F_BOUND) of every scenario that did not reach
+     * the KKT tolerance (status 1 / 2; the others keep the solve's dual objective) by a bound that is
+     * valid whatever the status -- the Lagrangian dual function of the scenario's subproblem at the
      * solve's dual iterate, made feasible: row duals of the wrong sign for an infinite row bound
      * zeroed; columns charged against their bounds, infinite ones replaced by bounds implied by the
      * rows (computed once per batch from the caller's data); reduced-cost infeasibility on a column
@@ -140,7 +141,11 @@ enum {
     PHG_F_OMEGA = 13,   /* [S] PDHG primal weight carried between solves                    */
     PHG_F_Z = 14,       /* [S*N] smoothing centre z (smoothed PH)                          */
     PHG_F_SMOOTH_P = 15,/* [S*N] smoothing weight p                                        */
-    PHG_F_SMOOTH_BETA = 16 /* [S*N] smoothing step beta                                    */
+    PHG_F_SMOOTH_BETA = 16,/* [S*N] smoothing step beta                                    */
+    PHG_F_WARM = 17     /* phg_copy_from only: src's last solution (scaled x, y and primal weights)
+                           as dst's warm start -- e.g. a Lagrangian spoke starting from the hub's
+                           prox-QP solution, whose duals are near-optimal for the Lagrangian LP once
+                           x is near xbar                                                       */
 };
 enum {
     PHG_I_ITERS = 0,    /* [S] PDHG iterations of the last solve                           */
@@ -265,7 +270,8 @@ int  phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on);
 
 /* Cylinders on one GPU (hub.py:462-616 send_ws / send_nonants, spoke.py; here device-to-device,
  * ordered after src's queued work by an event, enqueued on dst's stream):
- *   phg_copy_from : dst.field <- src.field (W for a Lagrangian spoke, phbase.py:397-413)
+ *   phg_copy_from : dst.field <- src.field (W for a Lagrangian spoke, phbase.py:397-413; PHG_F_WARM:
+ *                   src's last solution becomes dst's warm start)
  *   phg_fix_from  : dst.fixed[s, :] <- src.xN[scen, :] for all s (xhat candidate = scenario scen's
  *                   nonants, xhatshufflelooper_bounder.py; two-stage batches)
  *   phg_query     : *idle = 1 when everything queued on h's stream has finished (non-blocking)  */

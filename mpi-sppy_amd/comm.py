@@ -104,6 +104,15 @@ class TorchComm:
         return out
 
 
+def _device_count():
+    """Visible HIP devices, without initialising one (torch's count does not, on this image)."""
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except ImportError:
+        return 1 << 30
+
+
 class PhgGroupComm:
     """Device all-reduces through libphg.so's own RCCL communicator (``phg_create_group``,
     include/phg.h), everything else through ``host`` (any communicator of this module).
@@ -115,19 +124,31 @@ class PhgGroupComm:
     over once the engine exists (``attach``)."""
 
     def __init__(self, host, device):
-        from ._lib import PhgGroup
+        from . import _lib
         self.host = host
         self.rank, self.size = host.Get_rank(), host.Get_size()
-        uid, err = None, None
-        if self.rank == 0:
-            try:
-                uid = PhgGroup.unique_id()
-            except Exception as e:    # every rank still joins the broadcast, then all raise
-                err = e
+        # ncclCommInitRank is collective and blocking: a rank that fails BEFORE its call (library
+        # load, device, the id) would leave its peers inside it.  So the steps up to the call are
+        # agreed first through ``host``: every rank reports, and all proceed or all raise.  (The call
+        # itself is non-blocking with a deadline in libphg, PHG_GROUP_TIMEOUT.)
+        uid, err, ok = None, None, True
+        try:
+            _lib.load()
+            if not 0 <= int(device) < _device_count():
+                raise RuntimeError(f"device {device} not present")
+            if self.rank == 0:
+                uid = _lib.PhgGroup.unique_id()
+        except Exception as e:    # every rank still joins the broadcast and the vote
+            ok, err = False, e
         uid = host.bcast_object(uid, root=0)
-        if uid is None:
-            raise RuntimeError(f"phg_group_unique_id failed on rank 0{f': {err}' if err else ''}")
-        self.group = PhgGroup(self.size, self.rank, uid, device)
+        ok = ok and isinstance(uid, (bytes, bytearray)) and len(uid) == 128
+        n_ok = host.allreduce_scalar(1.0 if ok else 0.0) if self.size > 1 else (1.0 if ok else 0.0)
+        if n_ok != self.size:
+            if uid is None and err is None:
+                err = "phg_group_unique_id failed on rank 0"
+            raise RuntimeError(f"libphg RCCL group: set-up failed on {self.size - int(n_ok)} rank(s) before "
+                               f"ncclCommInitRank{f': {err}' if err else ''}")
+        self.group = _lib.PhgGroup(self.size, self.rank, uid, device)
         self.handle = None
 
     def attach(self, engine):

@@ -18,7 +18,8 @@
 // changes other columns' reduced costs only by finite charges against their bounds).  If that cannot
 // zero it, the scenario's bound is -inf: no finite certificate from this iterate.
 //
-// One 256-thread workgroup per scenario; duals and reduced costs in per-scenario scratch; the repair
+// Applied to the scenarios that did NOT reach the KKT tolerance (status 1 / 2); the others keep the
+// PDHG epilogue's dual objective.  One 256-thread workgroup per scenario; duals and reduced costs in per-scenario scratch; the repair
 // (a handful of columns on farmer: the Purchased columns, whose only row is the cattle-feed row) is
 // sequential in one thread; sums are fixed-order block reductions (deterministic).
 #include "phg_internal.h"
@@ -41,6 +42,11 @@ __global__ __launch_bounds__(256) void safe_bound_kernel(PdhgArgs a, SafeBoundAr
     if (a.gate && a.gate[0] < a.gate_below) return;   // the solve was gated off: nothing to bound
     __shared__ double red[4];
     const int s = blockIdx.x, tid = threadIdx.x;
+    // a scenario that reached the KKT tolerance keeps the solve's own dual objective -- a solver's
+    // bound at optimality, as a CPU solver reports it at its tolerances; charging that iterate's
+    // tolerance-level reduced costs against implied bounds would only loosen it (farmer: up to
+    // 1.5e-6 relative, sold quantities capped at ~1e5)
+    if (a.status[s] == 0) return;
     const int n = a.n, m = a.m;
     const long sn = (long)s * n, sm = (long)s * m, snz = (long)s * a.nnz, sN = (long)s * a.N;
     double* Y = b.Y + sm;

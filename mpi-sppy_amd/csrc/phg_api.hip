@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -322,6 +323,19 @@ static int cross_stream_wait(phg_handle* dst, phg_handle* src) {
 int phg_copy_from(phg_handle* dst, phg_handle* src, int32_t field) {
     if (!dst || !src || !dst->loaded || !src->loaded) return fail("phg_copy_from: handles not loaded");
     if (dst->device != src->device) return fail("phg_copy_from: handles on different devices");
+    if (field == PHG_F_WARM) {
+        // src's last solution as dst's warm start: the scaled front state (same batch -> the same
+        // deterministic scaling on both handles) and its primal weights
+        if (dst->S != src->S || dst->n != src->n || dst->m != src->m)
+            return fail("phg_copy_from: PHG_F_WARM needs the same batch on both handles");
+        CK(hipSetDevice(dst->device));
+        if (cross_stream_wait(dst, src)) return -1;
+        CK(hipMemcpyAsync(dst->xs, src->xs, (size_t)dst->S * dst->n * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
+        CK(hipMemcpyAsync(dst->ys, src->ys, (size_t)dst->S * dst->m * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
+        CK(hipMemcpyAsync(dst->omega, src->omega, (size_t)dst->S * sizeof(double), hipMemcpyDeviceToDevice, dst->stream));
+        dst->out_stale = true;
+        return cross_stream_wait(src, dst);
+    }
     size_t nd = 0, ns = 0;
     double* pd = field_ptr(dst, field, &nd);
     double* ps = field_ptr(src, field, &ns);
@@ -2107,10 +2121,33 @@ int phg_create_group(int32_t nranks, int32_t rank, const uint8_t* id128, int32_t
     g->nranks = nranks;
     g->rank = rank;
     g->device = device;
-    const ncclResult_t r = ncclCommInitRank(&g->comm, nranks, id, rank);
+    // non-blocking init, polled with a deadline: a peer that never joins (it failed before its own
+    // call) must not leave this rank blocked inside the collective -- on timeout the half-made
+    // communicator is aborted and the call fails, so every rank returns and the caller's vote
+    // (comm.group_or_host) can fall back.  PHG_GROUP_TIMEOUT seconds (default 300).
+    double limit = 300.0;
+    if (const char* ev = std::getenv("PHG_GROUP_TIMEOUT")) limit = std::max(1.0, std::atof(ev));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&g->comm, nranks, id, rank, &cfg);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress || (r == ncclSuccess && g->comm)) {
+        ncclResult_t st = ncclInProgress;
+        if (ncclCommGetAsyncError(g->comm, &st) != ncclSuccess) { r = ncclSystemError; break; }
+        if (st != ncclInProgress) { r = st; break; }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+            r = ncclInProgress;
+            break;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
     if (r != ncclSuccess) {
+        if (g->comm) (void)ncclCommAbort(g->comm);
         delete g;
-        return fail(std::string("phg_create_group: ncclCommInitRank: ") + ncclGetErrorString(r));
+        return fail(r == ncclInProgress
+                        ? std::string("phg_create_group: ncclCommInitRankConfig did not complete within ") +
+                              std::to_string((int)limit) + " s (a peer never joined?); aborted"
+                        : std::string("phg_create_group: ncclCommInitRankConfig: ") + ncclGetErrorString(r));
     }
     *out = g;
     return 0;

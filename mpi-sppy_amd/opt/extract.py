@@ -10,8 +10,14 @@ then lives in the batch.  Three sources:
 * a Pyomo ``ConcreteModel`` when Pyomo is importable: the active variables, the active linear
   constraints and the single active objective, through ``pyomo.repn.generate_standard_repn``.
   Pyomo is absent on the build container and on the GPU box, so this path is written against
-  Pyomo's public API and is PARITY UNPINNED (never executed here); a nonlinear or quadratic body
-  raises.
+  Pyomo's public API and is PARITY UNPINNED (never executed here); a nonlinear constraint body, or
+  an objective with off-diagonal quadratic terms, raises.
+
+The objective may carry a DIAGONAL quadratic part -- what the reference's PH puts on every scenario
+at iteration >= 1: ``W_on * sum W_i x_i + prox_on * sum rho_i/2 (x_i^2 - 2 xbar_i x_i + xbar_i^2)``
+(``phbase.py:724-750``, ``ProxExpr``), expanded by ``generate_standard_repn`` into linear terms plus
+``rho_i/2 x_i^2``.  It is kept as ``qdiag`` (objective = c^T x + 1/2 sum_j qdiag_j x_j^2 + c0); the
+plugin (``opt/phg.py``) maps it onto the C ABI's prox term (rho = qdiag, xbar = 0).
 
 Duck-typed protocol (``extract`` checks for ``variables``):
   ``model.variables()``   -> sequence of variable objects (``.name``, ``.lb``, ``.ub`` with None = unbounded,
@@ -19,7 +25,9 @@ Duck-typed protocol (``extract`` checks for ``variables``):
   ``model.constraints()`` -> sequence of rows (``.name``, ``.terms`` = [(variable, coef), ...],
                              ``.lower`` / ``.upper`` with None = unbounded, optional ``.constant`` moved
                              to the bounds)
-  ``model.objective()``   -> object with ``.terms``, optional ``.constant``, ``.sense`` (1 min, -1 max)
+  ``model.objective()``   -> object with ``.terms``, optional ``.constant``, ``.sense`` (1 min, -1 max),
+                             optional ``.quadratic`` = [(variable, variable, coef), ...] for coef * x * y
+                             (diagonal only: both the same variable)
 """
 import numpy as np
 
@@ -31,8 +39,10 @@ class StandardForm:
     """CSR standard form of one model; ``variables`` are the source objects in column order."""
 
     def __init__(self, name, variables, names, c, c0, sense, rowptr, colidx, vals, row_lo, row_hi, row_names,
-                 col_lo, col_hi):
+                 col_lo, col_hi, qdiag=None):
         self.name = name
+        # objective = c^T x + 1/2 sum_j qdiag_j x_j^2 + c0 (model sense)
+        self.qdiag = np.zeros(len(c)) if qdiag is None else np.asarray(qdiag, np.float64)
         self.variables = variables
         self.names = names
         self.c, self.c0, self.sense = c, c0, sense
@@ -70,7 +80,8 @@ def _from_linear_model(m):
     a = m.arrays()
     cols = [VarData(m, j, nm) for j, nm in enumerate(m.column_names())]
     sf = StandardForm(m.name, cols, m.column_names(), a["c"], m.obj_offset, m.sense, a["rowptr"], a["colidx"],
-                      a["vals"], a["row_lo"], a["row_hi"], [r[3] for r in m._rows], a["col_lo"], a["col_hi"])
+                      a["vals"], a["row_lo"], a["row_hi"], [r[3] for r in m._rows], a["col_lo"], a["col_hi"],
+                      qdiag=getattr(m, "_qdiag", None))
     sf.col_of = {}   # LinearModel variables map by column index (VarData objects are made on demand)
     return sf
 
@@ -101,10 +112,23 @@ def _from_duck(model):
     c = np.zeros(n)
     for v, a in ob.terms:
         c[col[id(v)]] += float(a)
+    q = _qdiag(((col[id(v1)], col[id(v2)], a) for v1, v2, a in (getattr(ob, "quadratic", None) or [])), n,
+               getattr(model, "name", ""))
     rp, ci, vals = _csr(rows, n)
     return StandardForm(getattr(model, "name", ""), variables, [getattr(v, "name", f"x{j}") for j, v in enumerate(variables)],
                         c, float(getattr(ob, "constant", 0.0) or 0.0), int(getattr(ob, "sense", 1)), rp, ci, vals,
-                        np.array(rlo), np.array(rhi), rnames, lo, hi)
+                        np.array(rlo), np.array(rhi), rnames, lo, hi, qdiag=q)
+
+
+def _qdiag(terms, n, name):
+    """coef * x_j * x_k terms -> qdiag (objective 1/2 sum qdiag_j x_j^2): diagonal only."""
+    q = np.zeros(n)
+    for j, k, a in terms:
+        if j != k:
+            raise ValueError(f"model {name}: off-diagonal quadratic objective term (columns {j}, {k}); "
+                             "the engine solves diagonal quadratics (PH's prox term) only")
+        q[j] += 2.0 * float(a)
+    return q
 
 
 def _from_pyomo(model):   # parity unpinned: Pyomo is not importable here (module docstring)
@@ -135,16 +159,19 @@ def _from_pyomo(model):   # parity unpinned: Pyomo is not importable here (modul
     objs = list(model.component_data_objects(pyo.Objective, active=True, descend_into=True))
     if len(objs) != 1:
         raise ValueError(f"expected one active objective, found {len(objs)}")
-    repn = generate_standard_repn(objs[0].expr, compute_values=True)
-    if not repn.is_linear():
-        raise ValueError("only a linear objective is supported (PH adds its own prox term)")
+    # linear, or quadratic with diagonal terms only: PH's W and prox terms (phbase.py:724-750)
+    repn = generate_standard_repn(objs[0].expr, compute_values=True, quadratic=True)
+    if repn.nonlinear_expr is not None:
+        raise ValueError("the objective has a nonlinear part; only linear + diagonal quadratic is supported")
     c = np.zeros(n)
     for v, a in zip(repn.linear_vars, repn.linear_coefs):
         c[col[id(v)]] += float(a)
+    q = _qdiag(((col[id(v1)], col[id(v2)], a) for (v1, v2), a in
+                zip(repn.quadratic_vars or [], repn.quadratic_coefs or [])), n, model.name)
     rp, ci, vals = _csr(rows, n)
     sense = 1 if objs[0].sense == pyo.minimize else -1
     return StandardForm(model.name, variables, [v.name for v in variables], c, float(repn.constant), sense, rp, ci,
-                        vals, np.array(rlo), np.array(rhi), rnames, lo, hi)
+                        vals, np.array(rlo), np.array(rhi), rnames, lo, hi, qdiag=q)
 
 
 def extract(model):
@@ -169,6 +196,7 @@ def to_linear_model(sf, name=None):
         m._rows.append((d, float(sf.row_lo[i]), float(sf.row_hi[i]), str(sf.row_names[i])))
     m.sense = sf.sense
     m.obj_offset = float(sf.c0)
+    m._qdiag = np.asarray(sf.qdiag, np.float64).copy()   # diagonal quadratic objective (opt/phg.py)
     return m
 
 

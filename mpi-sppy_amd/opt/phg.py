@@ -17,8 +17,16 @@ plugin surface ``SPOpt`` uses on its solvers (``mpisppy/spopt.py:876-913`` creat
 
 The batch needs no scenario tree for a plain solve: a model without ``_mpisppy_node_list`` gets a
 one-column ROOT node whose PH terms are switched off (w_on = prox_on = 0), so the solve is the
-model's own LP.  The GPU engine is the only solver: there is no CPU fallback (the library loads
-or the plugin raises).
+model's own LP.  A model whose objective has a DIAGONAL quadratic part (``extract.qdiag``) -- the
+reference PH's subproblem from iteration 1 on, ``f(x) + W.x + rho/2 (x - xbar)^2``
+(``phbase.py:724-750``) as ``SPOpt.solve_one`` hands it to its plugin (``spopt.py:147-231``) --
+is solved as the C ABI's prox-QP: the batch's nonants are the quadratic columns, rho = the
+min-form diagonal, xbar = 0, W off (the linear part, W.x - rho xbar.x included, is already in c),
+prox on.  A concave (min-form negative) diagonal raises.  The GPU engine is the only solver: there
+is no CPU fallback (the library loads or the plugin raises).
+
+Reported bounds (``Problem[0].Lower_bound`` of a min problem) are weak-duality certificates of the
+solve's dual iterate (``phg_opts.safe_bound``), valid also at ``maxIterations``.
 """
 import numpy as np
 
@@ -78,6 +86,22 @@ class Results:
                 return self[i]
 
         return _SolList(res._solutions)
+
+
+class _PluginScenario:
+    """The plugin's view of one model: its standard form (attributes forwarded) with the batch's own
+    tree -- the quadratic columns as ROOT nonants -- and unit probability coefficients, without
+    touching the caller's model."""
+
+    def __init__(self, lm, nodes):
+        self._lm = lm
+        self._mpisppy_node_list = nodes
+        self._mpisppy_data = type("MpisppyData", (), {})()
+        self._mpisppy_data.prob_coeff = {nd.name: 1.0 for nd in nodes}
+        self._mpisppy_data.has_variable_probability = False
+
+    def __getattr__(self, k):
+        return getattr(self._lm, k)
 
 
 class PHGSolver:
@@ -143,30 +167,37 @@ class PHGSolver:
         lms = []
         for md in self._models:
             lm = as_scenario_model(md)
-            if not hasattr(lm, "_mpisppy_node_list"):
-                # no tree: one dummy ROOT nonant (column 0), PH terms off in the solve
-                if not isinstance(lm, LinearModel) or lm.n == 0:
-                    raise ValueError("PHGSolver: empty model")
-                lm._mpisppy_node_list = [ScenarioNode("ROOT", 1.0, 1, None, [VarData(lm, 0, lm.column_names()[0])], lm)]
+            if not isinstance(lm, LinearModel) or lm.n == 0:
+                raise ValueError("PHGSolver: empty model")
             lms.append(lm)
         S = len(lms)
+        # min-form diagonal of each model's quadratic objective; the batch's nonants are the columns
+        # quadratic in any model (one shared column list), else the dummy column 0 with PH terms off
+        qmin = []
         for lm in lms:
-            if not hasattr(lm, "_mpisppy_data"):
-                lm._mpisppy_data = type("MpisppyData", (), {})()
-            lm._mpisppy_data.prob_coeff = {nd.name: 1.0 for nd in lm._mpisppy_node_list}
-            lm._mpisppy_data.has_variable_probability = False
-        nodenames = []
-        for nd in lms[0]._mpisppy_node_list:
-            nodenames.append(nd.name)
-        for lm in lms[1:]:
-            for nd in lm._mpisppy_node_list:
-                if nd.name not in nodenames:
-                    nodenames.append(nd.name)
-        batch = BatchArrays(lms, nodenames, [1.0 / S] * S, 0, S, 1)
+            q = getattr(lm, "_qdiag", None)
+            q = np.zeros(lm.n) if q is None else lm.sense * np.asarray(q, np.float64)
+            if (q < 0).any():
+                raise ValueError(f"PHGSolver: model {lm.name}: the quadratic objective is not convex "
+                                 "(min-form diagonal < 0)")
+            qmin.append(q)
+        qcols = sorted(set(int(j) for q in qmin for j in np.nonzero(q)[0]))
+        self._quadratic = bool(qcols)
+        cols = qcols or [0]
+        views = []
+        for lm in lms:
+            names = lm.column_names()
+            nodes = [ScenarioNode("ROOT", 1.0, 1, None, [VarData(lm, j, names[j]) for j in cols], lm)]
+            views.append(_PluginScenario(lm, nodes))
+        batch = BatchArrays(views, ["ROOT"], [1.0 / S] * S, 0, S, 1)
         if self._engine is not None:
             self._engine.close()
         dev = torch.cuda.current_device()
         self._engine = Engine(batch, device=dev, layout=self.options.get("pdhg_layout", "auto"))
+        if self._quadratic:
+            # prox term rho/2 (x - xbar)^2 with xbar = 0: exactly the diagonal quadratic
+            self._engine.set(_lib.F_RHO, np.stack([q[cols] for q in qmin]).ravel())
+            self._engine.set(_lib.F_XBAR, np.zeros(len(cols)))
         self._lms = lms
         self._dirty = False
 
@@ -174,9 +205,9 @@ class PHGSolver:
         if self._dirty or self._engine is None:
             self._build()
         eng = self._engine
-        eng.solve(0, 0, eps=float(self.options.get("pdhg_eps", 1e-9)),
+        eng.solve(0, 1 if self._quadratic else 0, eps=float(self.options.get("pdhg_eps", 1e-9)),
                   max_iter=int(self.options.get("pdhg_max_iter", 200000)),
-                  check_every=int(self.options.get("pdhg_check_every", 32)), warm_start=0)
+                  check_every=int(self.options.get("pdhg_check_every", 32)), warm_start=0, safe_bound=True)
         eng.sync()
         st = eng.get_i32(_lib.I_STATUS)
         it = eng.get_i32(_lib.I_ITERS)

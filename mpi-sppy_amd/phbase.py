@@ -529,10 +529,12 @@ class PHBase(SPBase):
                 # run this one statement by statement (its own time check breaks below)
                 if self._spec_pending:
                     c, undone = self._drain_speculation()
+                    # either way conv of the previous iteration's update is part of the history
+                    # (the sequential loop appended it there)
+                    self.conv = c
+                    self.conv_history.append(c)
                     if undone:
                         self._PHIter -= 1
-                        self.conv = c
-                        self.conv_history.append(c)
                         break
                 pipelined = False
             if pipelined:
@@ -575,6 +577,11 @@ class PHBase(SPBase):
         else:
             self.mpicomm.Barrier()
         if self._spec_pending:      # PHIterLimit or the hub ended a pipelined loop
+            # conv_K of the last update K; below convthresh the reference broke at THIS iteration K
+            # before solve K, so the undo restores its state and _PHIter stays K (the in-loop paths
+            # decrement because they learn conv one iteration late).  Documented deviation: when a
+            # hub sync ran at iteration K it already handed the spokes that speculative solve's
+            # nonants (the reference would not have synced at K); the spokes' bounds stay valid.
             c, _undone = self._drain_speculation()
             self.conv = c
             self.conv_history.append(c)

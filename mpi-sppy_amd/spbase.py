@@ -79,8 +79,11 @@ class SPBase:
         bundles then take the scenarios' place in the batch (named ``rank<r>bundle<b>`` as in the
         reference, probability = the members' sum): the members of a bundle share one nonant copy,
         so their W / x-bar updates coincide and PH over the bundles is PH over the scenarios with
-        every member's nonants equal (the conv metric weighs each bundle once -- the reference's
-        per-scenario count when the bundles are equal-sized).  Two-stage trees only."""
+        every member's nonants equal.  The reference's convergence metric counts SCENARIOS
+        (``phbase.py:349-371`` loops over local_scenarios, not the bundles); weighing each bundle once
+        is that count only when the bundles are equal-sized, so unequal bundle sizes are rejected
+        (ValueError) rather than silently changing conv and the convthresh stopping iteration.
+        Two-stage trees only."""
         from .utils.ef import create_EF_from_scen_dict
         from .utils.proper_bundler import bundle_scenarios
         from .scenario_tree import attach_root_node
@@ -95,6 +98,12 @@ class SPBase:
             groups = bundle_scenarios([self.all_scenario_names[i] for i in slc], bpr)
             self.names_in_bundles[r] = dict(enumerate(groups))
             bundle_names += [f"rank{r}bundle{b}" for b in range(bpr)]
+        sizes = {len(g) for r in self.names_in_bundles for g in self.names_in_bundles[r].values()}
+        if len(sizes) > 1:
+            raise ValueError(f"bundles_per_rank={bpr} over {S} scenarios and {self.n_proc} rank(s) gives "
+                             f"bundles of unequal sizes {sorted(sizes)}: the convergence metric would weigh "
+                             "them differently from the reference's per-scenario count; choose "
+                             "bundles_per_rank * n_proc dividing the scenario count")
         members = {nm: grp for r in range(self.n_proc) for nm, grp in
                    zip(bundle_names[r * bpr:(r + 1) * bpr], self.names_in_bundles[r].values())}
         self.all_scenario_names_unbundled = self.all_scenario_names

@@ -81,6 +81,16 @@ def test_loose_bundles_per_rank():
     assert tot <= ef_obj + 1e-6 * abs(ef_obj)     # wait-and-see over bundles bounds the EF (min)
 
 
+def test_loose_bundles_unequal_sizes_rejected():
+    """bundles of unequal sizes would weigh the convergence metric differently from the reference's
+    per-scenario count (phbase.py:349-371): rejected."""
+    opts = {"solver_name": "phg", "PHIterLimit": 1, "defaultPHrho": 1, "convthresh": 0,
+            "verbose": False, "display_progress": False, "bundles_per_rank": 3}
+    with pytest.raises(ValueError, match="unequal sizes"):
+        SPBase(opts, farmer.scenario_names_creator(7), farmer.scenario_creator,
+               scenario_creator_kwargs={"num_scens": 7})
+
+
 class _V:
     def __init__(self, name, lb=None, ub=None, fixed=False, value=None):
         self.name, self.lb, self.ub, self.fixed, self.value = name, lb, ub, fixed, value
@@ -92,8 +102,10 @@ class _R:
 
 
 class _O:
-    def __init__(self, terms, constant=0.0, sense=1):
+    def __init__(self, terms, constant=0.0, sense=1, quadratic=None):
         self.terms, self.constant, self.sense = terms, constant, sense
+        if quadratic is not None:
+            self.quadratic = quadratic
 
 
 class _Duck:
@@ -140,3 +152,70 @@ def test_linear_model_extraction_round_trip():
         np.testing.assert_array_equal(lm.arrays()[k], m.arrays()[k])
     assert as_scenario_model(m) is m
     assert isinstance(lm, LinearModel)
+
+
+class PHDuck:
+    """A scenario model as the reference's PH hands it to its solver plugin at iteration >= 1
+    (``phbase.py:724-750``, min sense): f(x) + W.x_N + rho/2 (x_N^2 - 2 xbar x_N + xbar^2), built
+    from a LinearModel's arrays through the duck-typed protocol, the prox term expanded as
+    ``generate_standard_repn`` expands ProxExpr (linear terms + diagonal quadratics + constant).
+    sense=-1 states the same problem as a max of the negated objective."""
+
+    def __init__(self, lm, W, xbar, rho, sense=1):
+        a = lm.arrays()
+        self.name = lm.name + "_ph"
+        self.vars = [_V(nm, None if not np.isfinite(lo) else lo, None if not np.isfinite(hi) else hi)
+                     for nm, lo, hi in zip(lm.column_names(), a["col_lo"], a["col_hi"])]
+        self.rows = []
+        for i in range(len(a["row_lo"])):
+            p0, p1 = a["rowptr"][i], a["rowptr"][i + 1]
+            lo, hi = a["row_lo"][i], a["row_hi"][i]
+            self.rows.append(_R(f"r{i}", [(self.vars[j], v) for j, v in zip(a["colidx"][p0:p1], a["vals"][p0:p1])],
+                                None if not np.isfinite(lo) else lo, None if not np.isfinite(hi) else hi))
+        cols = [v.col for nd in lm._mpisppy_node_list for v in nd.nonant_vardata_list]
+        c = lm.sense * a["c"].copy()                # min form
+        lin = {j: c[j] for j in range(len(c)) if c[j] != 0.0}
+        quad = []
+        const = lm.sense * lm.obj_offset
+        for k, j in enumerate(cols):
+            lin[j] = lin.get(j, 0.0) + W[k] - rho[k] * xbar[k]
+            quad.append((self.vars[j], self.vars[j], rho[k] / 2.0))
+            const += rho[k] / 2.0 * xbar[k] ** 2
+        sg = float(sense)
+        self.obj = _O([(self.vars[j], sg * v) for j, v in lin.items()], constant=sg * const, sense=sense,
+                      quadratic=[(v1, v2, sg * q) for v1, v2, q in quad])
+        self.cols = cols
+
+    def variables(self):
+        return self.vars
+
+    def constraints(self):
+        return self.rows
+
+    def objective(self):
+        return self.obj
+
+
+def test_quadratic_objective_extraction():
+    m = farmer.scenario_creator("scen1", num_scens=3)
+    N = 3
+    W, xbar, rho = np.array([1.0, -2.0, 0.5]), np.array([100.0, 200.0, 150.0]), np.array([1.0, 2.0, 0.5])
+    d = PHDuck(m, W, xbar, rho)
+    sf = extract(d)
+    q = np.zeros(sf.n)
+    q[d.cols] = rho
+    np.testing.assert_allclose(sf.qdiag, q)
+    c = m.sense * m.arrays()["c"].copy()
+    c[d.cols] += W - rho * xbar
+    np.testing.assert_allclose(sf.c, c)
+    assert sf.c0 == pytest.approx(float(np.sum(rho / 2 * xbar ** 2)))
+    lm = to_linear_model(sf)
+    np.testing.assert_allclose(lm._qdiag, q)
+    assert len(d.cols) == N
+
+
+def test_off_diagonal_quadratic_raises():
+    d = _Duck()
+    d.objective = lambda: _O([(d.x, 1.0)], quadratic=[(d.x, d.y, 1.0)])
+    with pytest.raises(ValueError, match="off-diagonal"):
+        extract(d)

@@ -18,7 +18,9 @@ from mpisppy_amd.ph import PH  # noqa: E402
 from mpisppy_amd.utils.ef import create_EF  # noqa: E402
 from mpisppy_amd.utils.proper_bundler import ProperBundler  # noqa: E402
 from oracle import highs  # noqa: E402
-from test_bundles_extract import _Duck  # noqa: E402
+from oracle import models as om  # noqa: E402
+from oracle import ph as oph  # noqa: E402
+from test_bundles_extract import PHDuck, _Duck  # noqa: E402
 
 
 def _oracle_obj(m):
@@ -53,6 +55,92 @@ def test_plugin_solve_batch_matches_oracle():
         assert r.Problem[0].Upper_bound == pytest.approx(o, rel=1e-7)
         assert m.objective_value() == pytest.approx(o, rel=1e-7)
     opt.close()
+
+
+def _oracle_qp(m, W, xbar, rho):
+    """The oracle's HiGHS QP of the PH subproblem (min form): objective and x."""
+    a = m.arrays()
+    cols = [v.col for nd in m._mpisppy_node_list for v in nd.nonant_vardata_list]
+    c = m.sense * a["c"].copy()
+    c[cols] += W - rho * xbar
+    q = np.zeros_like(c)
+    q[cols] = rho
+    r = highs.solve(c, a["rowptr"], a["colidx"], a["vals"], a["row_lo"], a["row_hi"], a["col_lo"], a["col_hi"],
+                    qdiag=q, offset=m.sense * m.obj_offset + float(np.sum(rho / 2 * xbar ** 2)))
+    return r.obj, r.x
+
+
+@pytest.mark.parametrize("sense", [1, -1])
+def test_plugin_solves_ph_prox_objective(sense):
+    """The reference's PH hands its plugin a model whose objective carries W.x + rho/2 (x - xbar)^2
+    (phbase.py:724-750) -- a diagonal quadratic.  SolverFactory("phg").solve extracts it and solves
+    it as the C ABI's prox-QP: objective and solution at 1e-7 against the oracle's HiGHS QP, in both
+    senses (a max model states the negated objective)."""
+    names = farmer.scenario_names_creator(3)
+    rng = np.random.default_rng(5)
+    opt = SolverFactory("phg")
+    for nm in names:
+        m = farmer.scenario_creator(nm, crops_multiplier=2, num_scens=3)
+        N = len(m._mpisppy_node_list[0].nonant_vardata_list)
+        W = rng.normal(scale=20.0, size=N)
+        xbar = rng.uniform(50.0, 250.0, size=N)
+        rho = rng.uniform(0.5, 2.0, size=N)
+        d = PHDuck(m, W, xbar, rho, sense=sense)
+        res = opt.solve(d, load_solutions=True)
+        oobj, ox = _oracle_qp(m, W, xbar, rho)
+        assert res.solver.termination_condition == "optimal"
+        pobj = res.Problem[0].Upper_bound if sense == 1 else -res.Problem[0].Lower_bound
+        dbnd = res.Problem[0].Lower_bound if sense == 1 else -res.Problem[0].Upper_bound
+        assert pobj == pytest.approx(oobj, rel=1e-7), (pobj, oobj)
+        assert dbnd <= pobj + 1e-9 * abs(pobj) and dbnd == pytest.approx(oobj, rel=1e-7)
+        x = np.array([v.value for v in d.vars])
+        np.testing.assert_allclose(x[d.cols], ox[d.cols], rtol=1e-6, atol=1e-6 * np.abs(ox).max())
+    opt.close()
+
+
+class _PluginPH(oph.OraclePH):
+    """The reference's PH loop (restated by the oracle: Compute_Xbar, Update_W, convergence_diff,
+    the W_on / prox_on toggles) with every subproblem solve dispatched, as SPOpt.solve_one does
+    (spopt.py:147-231), to SolverFactory("phg") on the model PH builds: f(x) + W_on W.x +
+    prox_on rho/2 (x - xbar)^2."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.plugin = SolverFactory("phg")
+        self.models = [farmer.scenario_creator(nm, num_scens=self.S) for nm in self.names]
+
+    def solve_one(self, k):
+        m = self.models[k]
+        W = self.W[k] if self.W_on else np.zeros(self.N)
+        rho = self.rho[k] if self.prox_on else np.zeros(self.N)
+        d = PHDuck(m, W, self.xbar[k], rho)
+        res = self.plugin.solve(d, load_solutions=True)
+        assert res.solver.termination_condition == "optimal"
+        self.x[k] = np.array([v.value for v in d.vars])
+        self.obj[k] = res.Problem[0].Upper_bound
+        self.outer[k] = res.Problem[0].Lower_bound
+        self.feasible[k] = True
+
+
+def test_reference_ph_loop_through_plugin_reproduces_w_file():
+    """Drop-in check: the reference's PH with the phg plugin as its subproblem solver reproduces the
+    reference's own golden W / xbar files (mpisppy/tests/examples/w_test_data, farmer 3 scenarios,
+    rho 1, 5 iterations; test_w_writer.py:83-112 at places=5)."""
+    import csv
+    import os
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    o = _PluginPH(dict(defaultPHrho=1.0, PHIterLimit=5, convthresh=1e-10), om.farmer_names(3), om.farmer,
+                  dict(crops_multiplier=1, num_scens=3))
+    o.Iter0()
+    o.iterk_loop()
+    sc = om.farmer("scen0", num_scens=3)
+    nonant_names = [sc.colnames[c] for c in sc.nonant_cols()]
+    for sname, vname, wval in list(csv.reader(open(os.path.join(gold, "ref_w_file.csv"))))[:9]:
+        k, i = om.farmer_names(3).index(sname), nonant_names.index(vname)
+        assert abs(o.W[k, i] - float(wval)) < 5e-6, (sname, vname, o.W[k, i], wval)
+    for vname, xval in list(csv.reader(open(os.path.join(gold, "ref_xbar_file.csv"))))[:3]:
+        assert abs(o.xbar[0, nonant_names.index(vname)] - float(xval)) < 5e-6
+    o.plugin.close()
 
 
 def _ph(names, creator, kw, **extra):
