@@ -175,9 +175,9 @@ int  phg_sync(phg_handle* h);
 enum { PHG_LAYOUT_AUTO = 0, PHG_LAYOUT_GATHER = 1, PHG_LAYOUT_LOCAL = 2, PHG_LAYOUT_BLOCK = 3,
        PHG_LAYOUT_MFMA = 4, PHG_LAYOUT_STREAM = 5, PHG_LAYOUT_BORDER = 6 };
 int  phg_set_layout(phg_handle* h, int32_t policy);
-/* host-only dry run of the lane-local planner (no device needed): out8 = {local variant or -1,
+/* host-only dry run of the lane-local planner (no device needed): out8 = {local shape or -1,
  * lanes per scenario, columns per lane, rows per lane, coupling-row slots, coupling rows used,
- * lanes used, 0}                                                                               */
+ * lanes used, the kernel variant phg_load_batch runs (pattern / infinite-bound specialised)}      */
 int  phg_plan(const phg_batch* b, int32_t* out8);
 
 /* singleton-row presolve, on by default (call before phg_load_batch): rows with one nonzero on a

@@ -15,6 +15,7 @@
 // So one PDHG iteration is ~100 fp64 VALU instructions and one short DPP chain per wave, with no
 // memory traffic at all between the prologue (load the scenario) and the epilogue (store x, y).
 #include <algorithm>
+#include <type_traits>
 
 #include "phg_internal.h"
 #include "wave_ops.h"
@@ -68,7 +69,7 @@ constexpr size_t local_lds_bytes() {
 template <int LPS, int CPL, int RPL, int D>
 constexpr int local_waves() { return 2; }
 
-template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC>
+template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC, unsigned long long BI>
 __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
     constexpr int G = 64 / LPS;                    // scenarios per wave
@@ -87,6 +88,11 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     // 2 instead of 3 fp64 ops per column, for 2 more registers per column -- only where they
     // fit (the widest variants would spill; they keep x+ = clamp((x + tau (A^T y - c)) ip))
     constexpr bool FOLD = RPL * CPL + D * CPL <= 12;
+    // FOLDT (pattern-specialised kernels with <= 8 occupied slots): tau ip folded into the matrix as
+    // well -- blkt = blk tip, cft = cf tip, re-derived with the step coefficients -- so the primal
+    // step is one FMA chain clamp(fma(x, ip, -ctip) + sum blkt y) per column: A^T y itself is no
+    // longer formed in the iteration (the checks re-form it), 1 fp64 instruction less per column
+    constexpr bool FOLDT = FOLD && (__builtin_popcount(MB) + __builtin_popcount(MC) <= 8);
 
     // ------------------------------------------------------------------ per-group state
     int s = 0;                                     // scenario of the group's current work item
@@ -94,8 +100,10 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     double x[CPL], aty[CPL], c[CPL], lo[CPL], hi[CPL], ip[CPL], tip[CPL], ctip[CPL], xsum[CPL];
     double y[RPL], ax[RPL], rlo[RPL], rhi[RPL], ysum[RPL];
     double blk[RPL][CPL];
+    double blkt[FOLDT ? RPL : 1][FOLDT ? CPL : 1];
     double yd[DD], axd[DD], dlo[DD], dhi[DD], ydsum[DD];
     double cf[DD][CPL];
+    double cft[FOLDT ? DD : 1][FOLDT ? CPL : 1];
 #pragma unroll
     for (int k = 0; k < CPL; ++k) { cj[k] = -1; x[k] = aty[k] = c[k] = lo[k] = hi[k] = ip[k] = tip[k] = ctip[k] = xsum[k] = 0.0; }
 #pragma unroll
@@ -117,6 +125,26 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     // (loops fully unrolled: the mask tests fold to constants)
     auto bon = [](int r, int k) { return ((MB >> (r * CPL + k)) & 1u) != 0u; };
     auto con = [](int d, int k) { return ((MC >> (d * CPL + k)) & 1u) != 0u; };
+    // BI: bound sides infinite in every occupied lane slot of every scenario (host-verified,
+    // local_inf_mask in phg_api.hip): the projection onto them is the identity, so its v_max / v_min
+    // is dropped at compile time (bit-identical: max(v, -inf) = v, min(v, +inf) = v).  Bits: column
+    // slot k lower 0 + k, upper 16 + k; row slot r lower 32 + r, upper 40 + r; coupling row d lower
+    // 48 + d, upper 52 + d.  Farmer: 5 of the 14 clamps per PDHG iteration (sold / purchased
+    // quantities have no upper bound, every row one infinite side)
+    auto binf = [](int bit) { return ((BI >> bit) & 1ull) != 0ull; };
+    auto clampx = [&](int k, double v) {
+        if (!binf(k)) v = vmax(v, lo[k]);
+        if (!binf(16 + k)) v = vmin(v, hi[k]);
+        return v;
+    };
+    // g - clamp(g, -sig hi, -sig lo) with the infinite sides' no-op dropped (rlo / rhi hold -sig
+    // times the bounds: an infinite upper bound is -inf there, an infinite lower one +inf)
+    auto dproj = [&](double g, double nhi, double nlo, int blo, int bhi) {
+        double t = g;
+        if (!binf(bhi)) t = vmax(t, nhi);
+        if (!binf(blo)) t = vmin(t, nlo);
+        return g - t;
+    };
     // row r of the block times a column vector f(k) (first term a product, then FMAs)
     auto brow = [&](int r, auto f) {
         double acc = 0.0;
@@ -177,6 +205,12 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             if constexpr (FOLD) {
                 tip[k] = tau * ip[k];
                 ctip[k] = CS(CI::C + k) * tip[k];
+            }
+            if constexpr (FOLDT) {
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) blkt[r][k] = blk[r][k] * tip[k];
+#pragma unroll
+                for (int d = 0; d < D; ++d) cft[d][k] = cf[d][k] * tip[k];
             }
         }
     };
@@ -510,15 +544,28 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         if (!wave_any(live)) break;
         // two PDHG iterations per trip (check_every is even): the A x / A x+ hand-over is a
         // register rename instead of copies
-        auto step = [&]() {
+        auto step = [&](auto sumc) {
+            constexpr bool SUM = decltype(sumc)::value;
             // primal step: exact prox of the diagonal quadratic + box (1/(1+tau q) precomputed)
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 double xn;
-                if constexpr (FOLD) xn = vmin(vmax(fma(aty[k], tip[k], fma(x[k], ip[k], -ctip[k])), lo[k]), hi[k]);
-                else xn = vmin(vmax(fma(tau, aty[k] - c[k], x[k]) * ip[k], lo[k]), hi[k]);
+                if constexpr (FOLDT) {
+                    double acc = fma(x[k], ip[k], -ctip[k]);
+#pragma unroll
+                    for (int r = 0; r < RPL; ++r)
+                        if (bon(r, k)) acc = fma(blkt[r][k], y[r], acc);
+#pragma unroll
+                    for (int d = 0; d < D; ++d)
+                        if (con(d, k)) acc = fma(cft[d][k], yd[d], acc);
+                    xn = clampx(k, acc);
+                } else if constexpr (FOLD) {
+                    xn = clampx(k, fma(aty[k], tip[k], fma(x[k], ip[k], -ctip[k])));
+                } else {
+                    xn = clampx(k, fma(tau, aty[k] - c[k], x[k]) * ip[k]);
+                }
                 x[k] = xn;
-                xsum[k] += xn;
+                if constexpr (SUM) xsum[k] += xn;
             }
             // dual step with extrapolation A(2x+ - x) = 2 A x+ - A x (empty row slots stay 0:
             // zero block row and zero bounds)
@@ -528,27 +575,39 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             for (int r = 0; r < RPL; ++r) {
                 // y+ = max(g + sig lo, 0) + min(g + sig hi, 0) = g - clamp(g, -sig hi, -sig lo)
                 const double g = y[r] - sig * (2.0 * axn[r] - ax[r]);
-                y[r] = g - vmin(vmax(g, rhi[r]), rlo[r]);
+                y[r] = dproj(g, rhi[r], rlo[r], 32 + r, 40 + r);
                 ax[r] = axn[r];
-                ysum[r] += y[r];
+                if constexpr (SUM) ysum[r] += y[r];
             }
 #pragma unroll
             for (int d = 0; d < D; ++d) {
                 const double g = yd[d] - sig * (2.0 * axdn[d] - axd[d]);
-                yd[d] = g - vmin(vmax(g, dhi[d]), dlo[d]);
+                yd[d] = dproj(g, dhi[d], dlo[d], 48 + d, 52 + d);
                 axd[d] = axdn[d];
-                ydsum[d] += yd[d];
+                if constexpr (SUM) ydsum[d] += yd[d];
             }
-            mv_aty(y, yd, aty);
+            if constexpr (!FOLDT) mv_aty(y, yd, aty);
         };
+        // sum_stride 2 (PdhgArgs::sum_stride): the running sums of the average iterate take every
+        // second iterate only (the average of the even iterates: still an ergodic PDHG average, and
+        // a restart candidate like any other point) -- 7 of ~72 fp64 instructions per PDHG
+        // iteration on farmer saved in the other step
+        if (a.sum_stride == 2) {
 #pragma unroll 1
-        for (int kk = 0; kk < chk; kk += 2) {
-            step();
-            step();
+            for (int kk = 0; kk < chk; kk += 2) {
+                step(std::false_type{});
+                step(std::true_type{});
+            }
+        } else {
+#pragma unroll 1
+            for (int kk = 0; kk < chk; kk += 2) {
+                step(std::true_type{});
+                step(std::true_type{});
+            }
         }
         it += chk;
         since += chk;
-        cnt += chk;
+        cnt += a.sum_stride == 2 ? chk / 2 : chk;
 
         // ---------------------------------------------------------- restart / termination check
         const double inv = 1.0 / (double)cnt;
@@ -557,6 +616,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         // avg_every-th check of the group -- uniform over the wave, the check's reductions are
         // group-local but the products are wave-wide
         const bool avg = wave_any(live && (a.avg_every <= 1 || ((it / chk) % a.avg_every) == 0));
+        if constexpr (FOLDT) mv_aty(y, yd, aty);   // not formed in the iterations
         kkt_both(avg, inv, oc, oa);
         if (!avg)
 #pragma unroll
@@ -644,16 +704,20 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
 struct LocalVariant {
     int LPS, CPL, RPL, D;
     unsigned MB, MC;           // compiled-in block / coupling slot masks (all ones: generic)
+    unsigned long long BI;     // compiled-in infinite bound sides (0: generic)
     size_t lds;                // dynamic LDS per wave (Cold layout)
     void (*fn)(PdhgArgs);
     void (*fn_persist)(PdhgArgs);
 };
 
-#define PHG_LM(a_, b_, c_, d_, mb_, mc_)                                                        \
-    {a_, b_, c_, d_, mb_, mc_, local_lds_bytes<a_, b_, c_, d_>(),                                \
-     pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_>,                                         \
-     pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_>}
-#define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u)
+#define PHG_LM(a_, b_, c_, d_, mb_, mc_, bi_)                                                   \
+    {a_, b_, c_, d_, mb_, mc_, bi_, local_lds_bytes<a_, b_, c_, d_>(),                             \
+     pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_, bi_>,                                      \
+     pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_, bi_>}
+#define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u, 0ull)
+// farmer's infinite sides: columns 2, 3 (QuantitySuperQuotaSold, QuantityPurchased) above; row 0
+// (cattle feed, >=) above, row 1 (limit sold, <= 0) below; the total-acreage row (<=) below
+#define PHG_FARMER_BI ((1ull << 18) | (1ull << 19) | (1ull << 40) | (1ull << 33) | (1ull << 48))
 // shapes ordered by preference: fewest lanes per scenario first, then smallest register footprint;
 // the generic kernel of every shape first, then pattern-specialised ones
 static const LocalVariant kLocalVariants[] = {
@@ -669,10 +733,15 @@ static const LocalVariant kLocalVariants[] = {
     // farmer (examples/farmer/farmer.py:157-203): per crop lane, columns DevotedAcreage, SubQuota,
     // SuperQuota, Purchased; rows cattle feed (all four) and limit sold (no Purchased); the
     // total-acreage coupling row on DevotedAcreage only
-    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u),
-    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u),
-    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u),
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, 0ull),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, 0ull),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, 0ull),
+    // ... and its infinite bound sides
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI),
 };
+#undef PHG_FARMER_BI
 #undef PHG_L
 #undef PHG_LM
 constexpr int kLocalShapes = 9;   // the generic entries; the planner walks these
@@ -681,16 +750,18 @@ int pdhg_local_num_variants() { return kLocalShapes; }
 
 // the variant to run for shape v and the layout's slot masks: the specialised entry of that shape
 // with the fewest slots that still covers every occupied one, else the generic kernel
-int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc) {
+int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi) {
     const LocalVariant& S0 = kLocalVariants[v];
     int best = v, bits = __builtin_popcount(S0.MB) + __builtin_popcount(S0.MC);
+    int inf = 0;
     const int total = (int)(sizeof(kLocalVariants) / sizeof(kLocalVariants[0]));
     for (int u = kLocalShapes; u < total; ++u) {
         const LocalVariant& V = kLocalVariants[u];
         if (V.LPS != S0.LPS || V.CPL != S0.CPL || V.RPL != S0.RPL || V.D != S0.D) continue;
-        if ((mb & ~V.MB) || (mc & ~V.MC)) continue;
+        if ((mb & ~V.MB) || (mc & ~V.MC) || (V.BI & ~bi)) continue;   // every dropped clamp must be a no-op
         const int b = __builtin_popcount(V.MB) + __builtin_popcount(V.MC);
-        if (b < bits) { best = u; bits = b; }
+        const int f = __builtin_popcountll(V.BI);
+        if (b < bits || (b == bits && f > inf)) { best = u; bits = b; inf = f; }
     }
     return best;
 }

@@ -29,7 +29,7 @@ hipError_t prep_launch(const PrepArgs& a, hipStream_t stream);
 hipError_t schedule_launch(const int* iters, int S, int unit, int* order, hipStream_t st);
 int pdhg_local_num_variants();
 void pdhg_local_variant_shape(int v, int* out4);
-int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc);
+int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi);
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_block_num_variants();
@@ -193,6 +193,7 @@ struct phg_handle {
     SafeBoundArgs sb{};
     // relative-gap test on the whole objective (PdhgArgs::gap_const); PHG_GAP_RAW=1 turns it off
     int gap_const = 1;
+    int sum_stride = 1;        // PdhgArgs::sum_stride (PHG_SUM_STRIDE)
 };
 
 template <class T>
@@ -270,6 +271,7 @@ int phg_create(int device, phg_handle** out) {
     if (const char* ev = std::getenv("PHG_AVG_EVERY")) h->avg_every = std::max(1, std::atoi(ev));
     if (const char* ev = std::getenv("PHG_FUSE")) h->no_fuse = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_GAP_RAW")) h->gap_const = std::atoi(ev) == 0;
+    if (const char* ev = std::getenv("PHG_SUM_STRIDE")) h->sum_stride = std::atoi(ev) == 2 ? 2 : 1;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return fail("phg_create: hipStreamCreate failed");
@@ -615,6 +617,65 @@ static int plan_local(const phg_batch* b, int LPS, int CPL, int RPL, int D, Loca
     return 0;
 }
 
+// Bound sides that are infinite in EVERY occupied slot of every scenario (the kernel drops their
+// no-op clamps, pdhg_local.hip BI).  Columns that are nonants are excluded (fixing the nonants, the
+// xhat evaluation, gives them finite boxes); rows can only gain infinite sides when fixed (row_bounds).
+static unsigned long long local_inf_mask(const phg_batch* b, const LocalPlan& P, int LPS, int CPL, int RPL, int D) {
+    std::vector<char> isn(b->n, 0);
+    for (int k = 0; k < b->N; ++k) isn[b->nonant_col[k]] = 1;
+    auto all_inf = [&](const double* v, int stride, int idx) {
+        for (int s = 0; s < b->S; ++s)
+            if (std::fabs(v[(size_t)s * stride + idx]) < 1e300) return false;
+        return true;
+    };
+    unsigned long long m = 0;
+    for (int k = 0; k < CPL && k < 16; ++k) {
+        bool lo = true, hi = true, any = false;
+        for (int l = 0; l < LPS; ++l) {
+            const int j = P.col_of[l * CPL + k];
+            if (j < 0) continue;
+            any = true;
+            if (isn[j]) { lo = hi = false; break; }
+            lo = lo && all_inf(b->col_lo, b->n, j);
+            hi = hi && all_inf(b->col_hi, b->n, j);
+        }
+        if (any && lo) m |= 1ull << k;
+        if (any && hi) m |= 1ull << (16 + k);
+    }
+    for (int r = 0; r < RPL && r < 8; ++r) {
+        bool lo = true, hi = true, any = false;
+        for (int l = 0; l < LPS; ++l) {
+            const int i = P.row_of[l * RPL + r];
+            if (i < 0) continue;
+            any = true;
+            lo = lo && all_inf(b->row_lo, b->m, i);
+            hi = hi && all_inf(b->row_hi, b->m, i);
+        }
+        if (any && lo) m |= 1ull << (32 + r);
+        if (any && hi) m |= 1ull << (40 + r);
+    }
+    for (int d = 0; d < D && d < 4; ++d) {
+        const int i = P.cpl_row[d];
+        if (i < 0) continue;
+        if (all_inf(b->row_lo, b->m, i)) m |= 1ull << (48 + d);
+        if (all_inf(b->row_hi, b->m, i)) m |= 1ull << (52 + d);
+    }
+    return m;
+}
+
+static void local_slot_masks(const LocalPlan& plan, const int* sh, unsigned* mb, unsigned* mc) {
+    const int LPS = sh[0], CPL = sh[1], RPL = sh[2], D = sh[3];
+    *mb = *mc = 0;
+    for (int l = 0; l < LPS; ++l) {
+        for (int rr = 0; rr < RPL; ++rr)
+            for (int k = 0; k < CPL; ++k)
+                if (plan.blk_p[(l * RPL + rr) * CPL + k] >= 0) *mb |= 1u << (rr * CPL + k);
+        for (int d = 0; d < D; ++d)
+            for (int k = 0; k < CPL; ++k)
+                if (plan.cpl_p[(d * LPS + l) * CPL + k] >= 0) *mc |= 1u << (d * CPL + k);
+    }
+}
+
 static int pick_local_variant(const phg_batch* b, LocalPlan& plan, int* sh) {
     for (int v = 0; v < pdhg_local_num_variants(); ++v) {
         pdhg_local_variant_shape(v, sh);
@@ -636,17 +697,11 @@ static int build_local_layout(phg_handle* h, const phg_batch* b) {
         // slots occupied in at least one lane -> the pattern-specialised kernel of this shape
         const int LPS = sh[0], CPL = sh[1], RPL = sh[2], D = sh[3];
         unsigned mb = 0, mc = 0;
-        for (int l = 0; l < LPS; ++l) {
-            for (int rr = 0; rr < RPL; ++rr)
-                for (int k = 0; k < CPL; ++k)
-                    if (plan.blk_p[(l * RPL + rr) * CPL + k] >= 0) mb |= 1u << (rr * CPL + k);
-            for (int d = 0; d < D; ++d)
-                for (int k = 0; k < CPL; ++k)
-                    if (plan.cpl_p[(d * LPS + l) * CPL + k] >= 0) mc |= 1u << (d * CPL + k);
-        }
+        local_slot_masks(plan, sh, &mb, &mc);
         // PHG_LOCAL_GENERIC=1 keeps the generic kernel (A/B of the specialisation)
         const char* gen = std::getenv("PHG_LOCAL_GENERIC");
-        h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc);
+        const unsigned long long bi = local_inf_mask(b, plan, LPS, CPL, RPL, D);
+        h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc, bi);
         h->local_masks[0] = mb;
         h->local_masks[1] = mc;
         std::memcpy(h->lshape, sh, sizeof sh);
@@ -1572,6 +1627,9 @@ int phg_plan(const phg_batch* b_in, int32_t* out8) {
             lanes += used;
         }
         out8[6] = lanes;
+        unsigned mb, mc;
+        local_slot_masks(plan, sh, &mb, &mc);
+        out8[7] = pdhg_local_pick_masked(v, mb, mc, local_inf_mask(b, plan, sh[0], sh[1], sh[2], sh[3]));
     }
     return 0;
 }
@@ -1915,6 +1973,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.avg_every = h->avg_every;
     a.bd = h->bd;
     a.gap_const = h->gap_const;
+    a.sum_stride = h->sum_stride;
     if (h->border_layout) CK(pdhg_border_launch(a, h->stream));
     else if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));
     else if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));

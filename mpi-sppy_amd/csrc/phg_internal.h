@@ -197,6 +197,9 @@ struct PdhgArgs {
     // term inflates to ~rho/2 ||xbar||^2 (hydro: 1e4 against objectives of order 1); 0: the
     // constant-free form (PHG_GAP_RAW=1, A/B runs)
     int gap_const;
+    // lane-local kernel: 1 = the average iterate's running sums take every PDHG iterate, 2 = every
+    // second one (PHG_SUM_STRIDE)
+    int sum_stride;
 };
 
 // relative-gap denominator of the termination test (PdhgArgs::gap_const): K = the objective constant

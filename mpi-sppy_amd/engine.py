@@ -129,7 +129,7 @@ def plan_layout(batch):
         return None
     return {"variant": int(out[0]), "lanes_per_scenario": int(out[1]), "cols_per_lane": int(out[2]),
             "rows_per_lane": int(out[3]), "coupling_slots": int(out[4]), "coupling_rows": int(out[5]),
-            "lanes_used": int(out[6])}
+            "lanes_used": int(out[6]), "kernel_variant": int(out[7])}
 
 
 def implied_bounds(batch):
