@@ -15,6 +15,7 @@ DevotedAcreage keys), HiGHS status / iterations / time, instance}.
 
     python tests/golden/make_ef_fixtures.py 1000 10000
     python tests/golden/make_ef_fixtures.py ph 30       # the oracle's PH to conv < 1e-4
+    python tests/golden/make_ef_fixtures.py first 30 1000 10000   # first-stage uniqueness / stiffness
 """
 import json
 import os
@@ -178,6 +179,87 @@ def farmer_ef_separable(S, cm=10):
     return obj, [a[cn] for cn in order]
 
 
+def farmer_ef_first_stage(S, cm=10):
+    """Uniqueness of the farmer EF's first stage, from the separable structure of
+    farmer_ef_separable.  With mu = the land price (minus the slope of the last segment the greedy
+    fill used, 0 if the budget is slack) every feasible a satisfies, by convexity of the f_c and
+    Sum a <= B,
+        f(a) - f* >= Sum_c [(s_c^+ + mu) (a_c - a*_c)^+ + (-mu - s_c^-) (a*_c - a_c)^+]
+    with s_c^-, s_c^+ the left / right slopes of f_c at a*_c (-inf / +inf at 0 / B).  So a crop with
+    stiffness kappa_c = min(s_c^+ + mu, -mu - s_c^-) > 0 can move by at most (f(a) - f*) / kappa_c;
+    a crop on the marginal segment (kappa_c = 0) moves only with the others or with idle land:
+    |a_m - a*_m| <= Sum_{c != m} |a_c - a*_c| + (f(a) - f*) / mu.  The first stage is unique iff at
+    most one crop is marginal (exact slope ties: relative 1e-12).  Returns the dict stored as the
+    fixture's "first_stage"."""
+    scens = [om.farmer(nm, crops_multiplier=cm, num_scens=S) for nm in om.farmer_names(S)]
+    crops = [f"{cb}{i}" for i in range(cm) for cb in om._FARMER_BASE]
+    base = {f"{cb}{i}": cb for i in range(cm) for cb in om._FARMER_BASE}
+    B = 500.0 * cm
+    p = 1.0 / S
+    segs = {}
+    for cn in crops:
+        cb = base[cn]
+        Y = np.array([sc.yields[cn] for sc in scens])
+        cfr, quota = om._CATTLE[cb], om._PRICE_QUOTA[cb]
+        pp, sub, sup, plant = om._PURCHASE[cb], om._SUB_PRICE[cb], om._SUPER_PRICE[cb], om._PLANT[cb]
+        bps = np.unique(np.clip(np.concatenate([cfr / Y, (cfr + quota) / Y, [0.0, B]]), 0.0, B))
+        mid = 0.5 * (bps[:-1] + bps[1:])
+        ya = np.outer(mid, Y)
+        sl = np.where(ya < cfr, -pp, np.where(ya < cfr + quota, -sub, -sup)) * Y
+        segs[cn] = (bps, plant + p * sl.sum(axis=1))
+    allseg = sorted((float(sl[k]), cn, float(bps[k]), float(bps[k + 1])) for cn, (bps, sl) in segs.items()
+                    for k in range(len(sl)))
+    a = {cn: 0.0 for cn in crops}
+    left, last = B, 0.0
+    for slope, cn, lo, hi in allseg:
+        if slope >= 0.0 or left <= 0.0:
+            break
+        take = min(hi - lo, left)
+        a[cn] = lo + take
+        left -= take
+        last = slope
+    mu = -last if left <= 1e-9 * B else 0.0
+    out = {}
+    tol = 1e-12 * max(1.0, max(abs(v[0]) for v in allseg))
+    marginal = []
+    for cn in crops:
+        bps, sl = segs[cn]
+        x = a[cn]
+        # left slope: segment ending at or containing x; right slope: segment starting at or containing x
+        k = int(np.searchsorted(bps, x, side="left"))
+        inside = 0 < k < len(bps) and bps[k] != x and bps[k - 1] < x
+        if inside:
+            s_lo = s_hi = float(sl[k - 1])
+        else:
+            kk = int(np.argmin(np.abs(bps - x)))
+            s_lo = float(sl[kk - 1]) if kk > 0 else -np.inf
+            s_hi = float(sl[kk]) if kk < len(sl) else np.inf
+        kap = min(s_hi + mu, -mu - s_lo)
+        if kap <= tol:
+            marginal.append(cn)
+        out[cn] = {"a": x, "slope_left": s_lo, "slope_right": s_hi, "kappa": kap}
+    order = sorted(crops)
+    return {"land_price_mu": mu, "budget_slack": left, "marginal_crops": marginal,
+            "unique": len(marginal) <= 1,
+            "kappa": [out[cn]["kappa"] for cn in order], "a": [out[cn]["a"] for cn in order],
+            "crops": order,
+            "bound": "f(a) - f* >= sum_c kappa_c |a_c - a*_c| over non-marginal crops (make_ef_fixtures."
+                     "farmer_ef_first_stage)"}
+
+
+def first_stage_fixture(sizes, cm=10):
+    for S in sizes:
+        fn = os.path.join(HERE, f"farmer_cm{cm}_ef_S{S}.json")
+        d = json.load(open(fn))
+        fs = farmer_ef_first_stage(S, cm)
+        assert max(abs(x - y) for x, y in zip(fs["a"], d["root_nonants"])) < 1e-9 * 500 * cm
+        d["first_stage"] = fs
+        with open(fn, "w") as fh:
+            json.dump(d, fh, indent=1)
+        print(fn, "unique" if fs["unique"] else "NOT unique", "marginal", fs["marginal_crops"],
+              "min kappa (non-marginal)", min(k for k in fs["kappa"] if k > 0), flush=True)
+
+
 def separable_fixture(sizes, cm=10):
     for S in sizes:
         t0 = time.perf_counter()
@@ -337,6 +419,8 @@ def oracle_ph_iters(S=30, cm=10, iters=100, procs=8):
 if __name__ == "__main__":
     if sys.argv[1:2] == ["sep"]:
         separable_fixture([int(a) for a in sys.argv[2:]])
+    elif sys.argv[1:2] == ["first"]:
+        first_stage_fixture([int(a) for a in sys.argv[2:]])
     elif sys.argv[1:2] == ["phit"]:
         oracle_ph_iters(*[int(a) for a in sys.argv[2:5]])
     elif sys.argv[1:2] == ["ph"]:

@@ -16,8 +16,11 @@ bench's options) to conv < 1e-4 through the C ABI, then:
   >= EF - 1e-7 relative (first-order solves at eps 1e-9) and within 1e-6;
 * the Lagrangian bound with the converged W (``lagrangian_bounder.py:21-44``) exists, is valid
   (<= EF) and is within 1e-4 of it at S = 1 000 and 10 000 (2e-4 at S = 30);
-* the converged xbar against the EF's first-stage solution (reported; asserted loosely: the EF
-  optimum's first stage need not be unique).
+* the converged xbar against the EF's first-stage solution: the EF first stage is unique but flat
+  (tests/golden/make_ef_fixtures.py farmer_ef_first_stage: one marginal crop, stiffness kappa_c of
+  the others down to 6e-4 $/acre at S = 10 000), so xbar must lie within G / kappa_c acres of it
+  per crop, G = the xhat inner bound's gap to the EF -- the deviation its own objective accuracy
+  allows.
 
 And against the oracle's own PH to convergence on S = 30 (``oracle_ph_farmer_cm10_S30.json``):
 E[obj] within 1e-6 relative.
@@ -84,6 +87,23 @@ def test_farmer_converged_ph_vs_ef(S):
     print("Lagrangian statuses", cylinders.evaluate_lagrangian.last_status_counts)
     assert outer is not None
     assert -(1e-4 if S >= 1000 else 2e-4) <= rout <= 1e-9
+    # first stage: the EF's is unique (one marginal crop) but flat (fixture "first_stage", from
+    # make_ef_fixtures.farmer_ef_first_stage): every crop off the marginal segment can sit at most
+    # G / kappa_c acres from the EF's, G = EF objective at xbar minus the optimum = the xhat inner
+    # bound's gap; the marginal crop at most the others' total plus G / mu
+    fs = ef.get("first_stage")
+    if fs is not None:
+        assert fs["unique"]
+        G = max(inner - efo, 0.0) + 1e-9 * abs(efo)
+        dev = np.abs(xhat - np.array(fs["a"]))
+        kap = np.array(fs["kappa"])
+        marg = kap <= 0
+        bound = np.where(marg, 0.0, G / np.where(marg, 1.0, kap))
+        assert (dev[~marg] <= bound[~marg] + 1e-9).all(), (dev, bound)
+        mu = fs["land_price_mu"]
+        assert (dev[marg] <= dev[~marg].sum() + (G / mu if mu > 0 else np.inf) + 1e-9).all()
+        print(f"first stage: max |xbar - a*| {dx:.3e} acres, allowed by the objective gap: "
+              f"{bound[~marg].min():.3e} .. {bound[~marg].max():.3e} (non-marginal crops)")
     assert dx <= 1.0                                    # acres; reported above at full precision
 
 
