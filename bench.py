@@ -253,22 +253,27 @@ def main():
     el = time.perf_counter() - t0
     pdhg_ms, n_solves, pdhg_iters = eng.timing(0)
     assert n_solves == args.steps, n_solves
-    # the PH update timed separately (HIP events only on it) over extra iterations: on one GPU the
-    # step the timed loop ran (phg_ph_step: node sums + W update, one launch where fusable), on
-    # several the sequential statements (node sums, all-reduce, W update)
+    # the PH update timed separately (HIP events only on it) over extra pipelined iterations, as the
+    # timed loop ran them: node sums (+ the previous folded update's conv segments) and the head --
+    # with the fold (include/phg.h phg_fold_partials) the head only forms xbar and the W update runs
+    # in the next solve's prologue; then the standalone two-kernel update (node sums + W update,
+    # the sequential statements) for its own roofline
     W_saved = eng.get(_lib.F_W)
+    fold = eng.set_fold(os.environ.get("PHG_FOLD", "1") != "0")
     eng.timing_reset(solves=False, updates=True)
-    upd_fused = False
     for _ in range(args.steps):
-        if comm is None:
-            upd_fused = eng.ph_step(0.0, False)
-        else:
-            ph.Compute_Xbar()
-            ph.Update_W()
-            ph.convergence_diff()
+        step()
     upd_ms, n_upd, _ = eng.timing(1)
-    ns_ms, n_ns, _ = eng.timing(2)       # node sums alone (0 launches when fused)
-    wu_ms, n_wu, _ = eng.timing(3)       # W update / head alone
+    ns_ms, n_ns, _ = eng.timing(2)
+    hd_ms, n_hd, _ = eng.timing(3)
+    eng.timing_reset(solves=False, updates=True)
+    for _ in range(args.steps):
+        ph.Compute_Xbar()
+        ph.Update_W()
+        ph.convergence_diff()
+    sa_ms, n_sa, _ = eng.timing(1)
+    sa_ns_ms, n_sa_ns, _ = eng.timing(2)
+    sa_wu_ms, n_sa_wu, _ = eng.timing(3)
     eng.timing_reset(solves=False, updates=False)
     eng.set(_lib.F_W, W_saved)
     iters_last = eng.get_i32(_lib.I_ITERS)
@@ -321,13 +326,18 @@ def main():
                 traffic = tj.get("pdhg_bytes_per_launch")
         except Exception:
             traffic = None
-    # PH update (node sums + W update): algorithmic bytes, SURVEY 8(d)3:
+    # PH update, algorithmic bytes:
     #   8 S N (1 x read + 1 W read + 1 W write + [rho per scenario ? 1 : 0]) + 8 S + 16 N_tot
     # rho is read from an [N] copy when it is the same in every scenario (PhArgs::rho_k), as here
     rho_now = eng.get(_lib.F_RHO).reshape(S_loc, b.N)
     rho_streams = int(not (rho_now == rho_now[0]).all())
     ph_bytes = 8 * S_loc * b.N * (3 + rho_streams) + 8 * S_loc + 16 * b.N_tot
-    ph_gbs = ph_bytes / (upd_ms / args.steps / 1e3) / 1e9
+    sa_gbs = ph_bytes / (sa_ms / max(1, n_sa) / 1e3) / 1e9
+    # the node-sum pass on its own bytes: x read (8 S N), prob coefficients (8 S L), the folded
+    # update's per-scenario partials and statuses (12 S), node sums written (16 N_tot)
+    ns_bytes = 8 * S_loc * b.N + 8 * S_loc * b.L + (12 * S_loc if fold else 0) + 16 * b.N_tot
+    ns_s = ns_ms / max(1, n_ns) / 1e3
+    ns_gbs = ns_bytes / ns_s / 1e9 if n_ns else 0.0
     # the block kernel on a SHARED matrix (sslp) holds its pieces in registers and x / y in LDS: no
     # per-iteration HBM stream exists to price against the HBM roofline, so it is reported like the
     # register-resident kernels (fp64 flops against the fp64 peak), with the PMC-measured HBM rate beside
@@ -408,15 +418,29 @@ def main():
                      "pdhg_iters_per_scen_per_step": round(pdhg_iters / args.steps / S_loc, 2),
                      "max_pdhg_iters": max_iters,
                      "avg_launch_ms": round(avg_launch_s * 1e3, 4)},
-        "roofline_ph_update": {"bound": "hbm", "achieved": round(ph_gbs, 2), "peak": HBM_PEAK_GBS,
-                               "unit": "GB/s", "frac": round(ph_gbs / HBM_PEAK_GBS, 5),
-                               "bytes_per_update": ph_bytes, "rho_streams": rho_streams,
-                               "avg_ms": round(upd_ms / args.steps, 4),
+        # the PH update as the timed steps run it.  Folded (default on the lane-local layout): the
+        # node-sum pass and the xbar head are the only launches -- the W update's x and W reads are
+        # the next solve's own warm-start / cost loads and its W write happens there too (measured
+        # against the unfolded solve by tools/ph_update_sweep.py); the roofline is the node-sum
+        # pass on its own bytes.  "standalone": the two-kernel update (node sums + W update) on
+        # the SURVEY 8(d)3 bytes.  At farmer size (10k x 30) every launch here is latency-bound.
+        "roofline_ph_update": {"bound": "hbm", "achieved": round(ns_gbs, 2), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(ns_gbs / HBM_PEAK_GBS, 5),
+                               "kernel": "node_sums_kernel" + (" (+ the folded update's conv segments)" if fold else ""),
+                               "bytes_per_launch": ns_bytes,
+                               "path": ("folded: node sums + xbar head; W += rho (x - xbar) in the next PDHG "
+                                        "prologue" if fold else "node sums + W update (two launches)"),
+                               "avg_ms": round(upd_ms / max(1, n_upd), 4),
                                "node_sums_avg_ms": round(ns_ms / max(1, n_ns), 4) if n_ns else None,
-                               "w_update_avg_ms": round(wu_ms / max(1, n_wu), 4) if n_wu else None,
-                               "timed": "HIP events: node sums begin -> W update end, and each kernel alone",
-                               "kernels": ("ph_step_kernel (node sums + W update, one launch)" if upd_fused
-                                           else "node sums + W update (two launches per PH iteration)")},
+                               "head_avg_ms": round(hd_ms / max(1, n_hd), 4) if n_hd else None,
+                               "survey_bytes_per_update": ph_bytes, "rho_streams": rho_streams,
+                               "timed": "HIP events on the library stream over extra pipelined iterations",
+                               "standalone": {"kernels": "node_sums_kernel + w_update_kernel",
+                                              "avg_ms": round(sa_ms / max(1, n_sa), 4),
+                                              "node_sums_avg_ms": round(sa_ns_ms / max(1, n_sa_ns), 4),
+                                              "w_update_avg_ms": round(sa_wu_ms / max(1, n_sa_wu), 4),
+                                              "bytes_per_update": ph_bytes, "achieved": round(sa_gbs, 2),
+                                              "frac": round(sa_gbs / HBM_PEAK_GBS, 5)}},
         "per_rank": per_rank,
         "host_and_exchange_ms_per_step": round(ms_per_step - max(per_rank["pdhg_ms_per_step"]), 4),
         "setup_s": round(t_setup, 3),

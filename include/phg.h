@@ -250,6 +250,21 @@ int  phg_ph_update(phg_handle* h, double* host_conv);
  * solve k-1 (x_{k-2}, W_{k-1}, xbar_{k-1}).  After the last iteration, phg_conv_start on the
  * partials gives conv of the last update; if it is below thr, phg_solve_undo restores the state
  * before the last solve.                                                                         */
+/* Folded update (default for the lane-local layout without smoothing / variable probability;
+ * PHG_FOLD=0 turns it off): phg_ph_head then only publishes conv_{k-1} and forms xbar_k; the next
+ * phg_solve applies W += rho (x - xbar) in its prologue -- it loads x (its warm start) and W (its
+ * objective) anyway, so the update's second read of x and its own launch disappear -- and leaves
+ * the per-scenario partials of update k on the device.  The next phg_node_sums reduces them into the
+ * partials region of the packed buffer it is given (dev_nodesum + 2*N_tot: pass the packed buffer),
+ * so the one all-reduce still carries them; after the last pipelined iteration
+ * phg_fold_partials(h, dev_convpart) does that reduction alone (before the caller's all-reduce of the
+ * partials; phg_conv_start does it itself when nothing is to be all-reduced, dev_convpart NULL).
+ * Reading or writing W / xbar, phg_apply_xbar or a second head before a solve apply a pending
+ * update first, so the state stays the reference's.                                           */
+int  phg_fold_partials(phg_handle* h, double* dev_convpart);
+/* fold on / off for this handle (a pending folded update is applied first); *active (may be NULL)
+ * = 1 if the loaded batch's solves take the folded update                                      */
+int  phg_set_fold(phg_handle* h, int32_t on, int32_t* active);
 int  phg_exchange_layout(phg_handle* h, int32_t* out3);
 int  phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t first);
 int  phg_solve_undo(phg_handle* h);

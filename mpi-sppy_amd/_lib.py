@@ -78,6 +78,8 @@ SIGNATURES = {
     "phg_exchange_layout": (C.c_int, [C.c_void_p, i32p]),
     "phg_ph_head": (C.c_int, [C.c_void_p, C.c_void_p, C.c_double, C.c_int32]),
     "phg_solve_undo": (C.c_int, [C.c_void_p]),
+    "phg_fold_partials": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "phg_set_fold": (C.c_int, [C.c_void_p, C.c_int32, i32p]),
     "phg_ph_step": (C.c_int, [C.c_void_p, C.c_double, C.c_int32, i32p]),
     "phg_mfma_info": (C.c_int, [C.c_void_p, i32p]),
     "phg_group_unique_id": (C.c_int, [C.c_void_p]),

@@ -330,7 +330,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     auto load = [&](int sc) {
         s = sc;
         const long sn = (long)s * a.n, sN = (long)s * a.N;
-        double prox_const = 0.0, c2 = 0.0;
+        double prox_const = 0.0, c2 = 0.0, dsum = 0.0;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             seq();
@@ -347,7 +347,14 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                 const int kk = col_nonant[j];
                 if (kk >= 0) {
                     const long t = sN + kk;
-                    ph_terms(a, t, cc, qq, prox_const);
+                    double w = a.W[t];
+                    if (a.fold_w) {   // Update_W (phbase.py:301-326) of the x this solve starts from
+                        const double dv = a.xs_in[b] * dd - a.xbar[a.xidx[t]];
+                        w = fma(a.rho[t], dv, w);
+                        a.W_rw[t] = w;
+                        dsum += fabs(dv);
+                    }
+                    ph_terms_w(a, t, w, cc, qq, prox_const);
                     if (a.fix_nonants) fixed_box(a, t, dd, lo_, hi_);
                 }
                 c2 += cc * cc;
@@ -419,10 +426,14 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         }
         // ||c'|| (unscaled, incl. PH terms), prox constant, initial primal weight ||c_hat||/||b_hat||
         {
-            double rr[4] = {c2, prox_const, 0.0, b2};
+            double rr[5] = {c2, prox_const, 0.0, b2, dsum};
 #pragma unroll
             for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
-            gsum_many<LPS, 4>(rr);
+            gsum_many<LPS, 5>(rr);
+            if (a.fold_w && gl == 0) {
+                a.conv_s[s] = rr[4];
+                a.fold_st[s] = a.status_in[s];
+            }
             rr[3] += b2d;
             GS(CI::SC + CI::CNORM) = sqrt(rr[0]);
             GS(CI::SC + CI::PROX) = rr[1];

@@ -9,6 +9,7 @@
 // inside one node) and then, by the last workgroup, per node in segment order; the cross-GPU
 // all-reduce (RCCL) of the 2*N_tot node sums and of the 2*P+2 convergence partials happens
 // between / after the kernels (see include/phg.h).
+#include <algorithm>
 #include <type_traits>
 
 #include "phg_internal.h"
@@ -294,12 +295,54 @@ __device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum,
     }
 }
 
+// Folded W update (PdhgArgs::fold_w): the solve prologue left each scenario's sum |x - xbar|
+// (conv_s) and the status of the solve that produced x (fold_st).  Conv segment b's partials:
+// fixed-order sums over its scenario range, published for conv_partials_final.
+__device__ void fold_conv_segment(const PhArgs& a, int b) {
+    __shared__ double red[4];
+    __shared__ int bad[8];
+    const int tid = threadIdx.x;
+    const int s0 = a.cseg_s0[b], s1 = a.cseg_s1[b];
+    double acc = 0.0;
+    int nb = 0, nn = 0;
+    for (int s = s0 + tid; s < s1; s += 256) {
+        acc += a.conv_s[s];
+        const int st = a.fold_st[s];
+        nb += st != 0;
+        nn += st == 2;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        acc += __shfl_xor(acc, o, 64);
+        nb += __shfl_xor(nb, o, 64);
+        nn += __shfl_xor(nn, o, 64);
+    }
+    if ((tid & 63) == 0) { red[tid >> 6] = acc; bad[tid >> 6] = nb; bad[4 + (tid >> 6)] = nn; }
+    __syncthreads();
+    if (tid == 0) {
+        publish(&a.csegpart[b], ((red[0] + red[1]) + red[2]) + red[3]);
+        publish(&a.csegbad[2 * b], bad[0] + bad[1] + bad[2] + bad[3]);
+        publish(&a.csegbad[2 * b + 1], bad[4] + bad[5] + bad[6] + bad[7]);
+    }
+    __syncthreads();
+}
+
+// the last workgroup's part of convergence_diff (declared here, defined below)
+__device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart);
+
 __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
+    // folded update pending: its conv segments ride along (the packed buffer's partials region)
+    if (a.fold_conv && blockIdx.y == 0)
+        for (int b = blockIdx.x; b < a.n_cseg; b += gridDim.x) fold_conv_segment(a, b);
     node_sum_partials(a);
     const int K = min(a.n_final, (int)(gridDim.x * gridDim.y));
     const int rank = last_k_workgroups(a.ticket, K);
     if (rank < 0) return;
     node_sum_final<false>(a, nodesum, rank, K);
+    if (a.fold_conv && rank == K - 1) {
+        __syncthreads();
+        conv_partials_final(a, nodesum + 2 * (long)a.N_tot);
+    }
     finish_k(a.ticket, a.ticket + 2, K);
 }
 
@@ -466,6 +509,7 @@ __device__ __forceinline__ void w_update_segment(const PhArgs& a, int b, const d
 // the last workgroup's part of convergence_diff: segment partials per virtual rank (fixed order)
 // into convpart[2v], convpart[2v+1] = (sum, count); the status counts; the flag
 __device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart) {
+    __syncthreads();
     __shared__ double red[4];
     __shared__ int bad[8];
     const int tid = threadIdx.x;
@@ -584,6 +628,41 @@ __global__ __launch_bounds__(256) void ph_step_kernel(PhArgs a, double* packed, 
         __hip_atomic_store(a.fticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.fticket + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// Folded PH iteration, the part before the solve (phg_ph_head with the fold on): conv of the
+// previous update from the all-reduced partials (the same tree as everywhere: same bits), published
+// by workgroup 0; unless it is below thr, xbar / xsqbar from the all-reduced node sums.  The W update
+// itself runs in the next solve's prologue (PdhgArgs::fold_w).  Grid: N_tot / 2048 workgroups.
+__global__ __launch_bounds__(256) void xbar_head_kernel(PhArgs a, const double* packed, double thr, int first) {
+    __shared__ double red256[256];
+    const double conv = first ? INFINITY : conv_value_block(packed + 2 * (long)a.N_tot, a.P, red256);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        publish_gate(conv, packed + 2 * (long)a.N_tot, a.P, a.gate, a.gate_host, a.gate_seq);
+    if (conv < thr) return;
+    for (long j = (long)blockIdx.x * 256 + threadIdx.x; j < a.N_tot; j += (long)gridDim.x * 256) {
+        a.xbar[j] = packed[j];
+        a.xsqbar[j] = packed[a.N_tot + j];
+    }
+}
+
+hipError_t xbar_head_launch(const PhArgs& a, const double* packed, double thr, int first, hipStream_t st) {
+    const int g = (int)std::min<long>(64, std::max<long>(1, ((long)a.N_tot + 2047) / 2048));
+    hipLaunchKernelGGL(xbar_head_kernel, dim3(g), dim3(256), 0, st, a, packed, thr, first);
+    return hipGetLastError();
+}
+
+// the conv partials of a folded update on their own (the drain after the last pipelined iteration,
+// phg_fold_partials): conv segments, then the last workgroup's per-virtual-rank reduction
+__global__ __launch_bounds__(256) void fold_conv_kernel(PhArgs a, double* convpart) {
+    fold_conv_segment(a, blockIdx.x);
+    if (!last_workgroup(a.ticket + 1)) return;
+    conv_partials_final(a, convpart);
+}
+
+hipError_t fold_conv_launch(const PhArgs& a, double* convpart, hipStream_t st) {
+    hipLaunchKernelGGL(fold_conv_kernel, dim3(a.n_cseg), dim3(256), 0, st, a, convpart);
+    return hipGetLastError();
 }
 
 hipError_t ph_step_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st) {

@@ -57,6 +57,8 @@ hipError_t ph_step_launch(const PhArgs& a, double* packed, double thr, int first
 hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double* gate_host, double seq,
                             hipStream_t st);
 hipError_t safe_bound_launch(const PdhgArgs& a, const SafeBoundArgs& b, hipStream_t st);
+hipError_t xbar_head_launch(const PhArgs& a, const double* packed, double thr, int first, hipStream_t st);
+hipError_t fold_conv_launch(const PhArgs& a, double* convpart, hipStream_t st);
 // solves between launch-schedule recomputations (PHG_SCHED_EVERY overrides, for A/B runs)
 static int sched_every() {
     static const int v = [] {
@@ -194,6 +196,14 @@ struct phg_handle {
     // relative-gap test on the whole objective (PdhgArgs::gap_const); PHG_GAP_RAW=1 turns it off
     int gap_const = 1;
     int sum_stride = 1;        // PdhgArgs::sum_stride (PHG_SUM_STRIDE)
+    // folded PH update (phg_ph_head -> the next phg_solve's prologue does Update_W; PHG_FOLD=0 off):
+    // on for the lane-local layout without smoothing / variable probability
+    int fold = 1;
+    bool fold_w_pending = false;      // xbar of update k is in place, its W update not yet applied
+    bool fold_conv_pending = false;   // the last solve did a folded update: its conv partials are
+                                      // per scenario (conv_s / fold_st), not yet in any partials buffer
+    double* conv_s = nullptr;
+    int* fold_st = nullptr;
 };
 
 template <class T>
@@ -239,6 +249,24 @@ static int materialize_outputs(phg_handle* h) {
     return 0;
 }
 
+// the folded update applies to this handle's solves (PdhgArgs::fold_w): lane-local layout, W kept
+// for every nonant (no variable-probability mask), no smoothing centre to update
+static bool fold_active(const phg_handle* h) {
+    return h->fold && h->local_variant >= 0 && !h->smooth_on && !h->ph.pcv;
+}
+
+// a folded W update whose solve has not run (xbar of update k in place, phg_ph_head done): apply it
+// now with the standalone kernel (W, and its conv partials into the handle's own buffer) -- for
+// anything that reads or rewrites W, or a second head before a solve
+static int flush_fold(phg_handle* h) {
+    if (!h->fold_w_pending) return 0;
+    PhArgs a = h->ph;
+    CK(w_update_launch(a, h->xbar, h->convpart, h->stream));
+    h->fold_w_pending = false;
+    h->fold_conv_pending = false;
+    return 0;
+}
+
 // front <-> back copy of the solve state (see phg_handle::SolveState)
 static void swap_state(phg_handle* h) {
     std::swap(h->xs, h->back.xs);
@@ -272,6 +300,7 @@ int phg_create(int device, phg_handle** out) {
     if (const char* ev = std::getenv("PHG_FUSE")) h->no_fuse = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_GAP_RAW")) h->gap_const = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_SUM_STRIDE")) h->sum_stride = std::atoi(ev) == 2 ? 2 : 1;
+    if (const char* ev = std::getenv("PHG_FOLD")) h->fold = std::atoi(ev) != 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return fail("phg_create: hipStreamCreate failed");
@@ -338,6 +367,7 @@ int phg_copy_from(phg_handle* dst, phg_handle* src, int32_t field) {
         dst->out_stale = true;
         return cross_stream_wait(src, dst);
     }
+    if (flush_fold(src) || flush_fold(dst)) return -1;
     size_t nd = 0, ns = 0;
     double* pd = field_ptr(dst, field, &nd);
     double* ps = field_ptr(src, field, &ns);
@@ -861,6 +891,8 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     if (dput(h, &ip, vfirst.data(), vfirst.size())) return -1; a.vr_first = ip;
     if (dput(h, &ip, xidx.data(), xidx.size())) return -1; h->xidx = ip;
     a.xidx = h->xidx;
+    if (dalloc(h, &h->conv_s, (size_t)S)) return -1;
+    if (dalloc(h, &h->fold_st, (size_t)S)) return -1;
     if (dalloc(h, &h->packed, 2 * (size_t)b->N_tot + 2 * (size_t)P + 3)) return -1;
     h->nodesum = h->packed;
     h->convpart = h->packed + 2 * (size_t)b->N_tot;
@@ -1871,6 +1903,7 @@ static double* field_ptr(phg_handle* h, int f, size_t* count) {
 
 int phg_set(phg_handle* h, int32_t f, const double* in) {
     if (!h || !h->loaded) return fail("phg_set: no batch loaded");
+    if ((f == PHG_F_W || f == PHG_F_XBAR || f == PHG_F_CONV_PART) && flush_fold(h)) return -1;
     size_t cnt = 0;
     double* p = field_ptr(h, f, &cnt);
     if (!p) return fail("phg_set: unknown field");
@@ -1905,6 +1938,7 @@ int phg_set(phg_handle* h, int32_t f, const double* in) {
 
 int phg_get(phg_handle* h, int32_t f, double* out) {
     if (!h || !h->loaded) return fail("phg_get: no batch loaded");
+    if ((f == PHG_F_W || f == PHG_F_XBAR || f == PHG_F_CONV_PART) && flush_fold(h)) return -1;
     size_t cnt = 0;
     double* p = field_ptr(h, f, &cnt);
     if (!p) return fail("phg_get: unknown field");
@@ -1974,6 +2008,19 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.bd = h->bd;
     a.gap_const = h->gap_const;
     a.sum_stride = h->sum_stride;
+    if (h->fold_w_pending) {
+        if (!fold_active(h)) {
+            if (flush_fold(h)) return -1;
+        } else {
+            a.fold_w = 1;
+            a.W_rw = h->W;
+            a.conv_s = h->conv_s;
+            a.fold_st = h->fold_st;
+            a.status_in = h->status;   // front: the solve whose x the update uses
+            h->fold_w_pending = false;
+            h->fold_conv_pending = true;
+        }
+    }
     if (h->border_layout) CK(pdhg_border_launch(a, h->stream));
     else if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));
     else if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
@@ -2001,10 +2048,17 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
 int phg_node_sums(phg_handle* h, double* dev_nodesum) {
     if (!h || !h->loaded) return fail("phg_node_sums: no batch loaded");
     CK(hipSetDevice(h->device));
+    if (h->fold_w_pending && flush_fold(h)) return -1;   // x changes only by a solve: keep W in step
     if (!h->t_open && timing_event(h, 1, 0)) return -1;
     h->t_open = (h->timing_mask & 2) != 0;
     if (timing_event(h, 2, 0)) return -1;
-    CK(node_sums_launch(h->ph, dev_nodesum ? dev_nodesum : h->nodesum, h->stream));
+    PhArgs a = h->ph;
+    // a folded update's conv partials ride along into the packed buffer's partials region
+    a.fold_conv = h->fold_conv_pending ? 1 : 0;
+    a.conv_s = h->conv_s;
+    a.fold_st = h->fold_st;
+    CK(node_sums_launch(a, dev_nodesum ? dev_nodesum : h->nodesum, h->stream));
+    h->fold_conv_pending = false;
     if (timing_event(h, 2, 1)) return -1;
     return 0;
 }
@@ -2012,6 +2066,7 @@ int phg_node_sums(phg_handle* h, double* dev_nodesum) {
 int phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpart) {
     if (!h || !h->loaded) return fail("phg_apply_xbar: no batch loaded");
     CK(hipSetDevice(h->device));
+    if (flush_fold(h)) return -1;
     PhArgs a = h->ph;
     h->gate_fused = dev_convpart == nullptr;   // one GPU: the last workgroup finishes conv too
     if (h->gate_fused) {
@@ -2038,7 +2093,14 @@ int phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t fi
     a.gate_seq = (double)(++h->gate_seq);
     if (!h->t_open && timing_event(h, 1, 0)) return -1;
     if (timing_event(h, 3, 0)) return -1;
-    CK(ph_head_launch(a, dev_packed ? dev_packed : h->packed, convthresh, first, h->stream));
+    if (fold_active(h)) {
+        // folded: xbar only; W += rho (x - xbar) and its partials in the next solve's prologue
+        if (flush_fold(h)) return -1;
+        CK(xbar_head_launch(a, dev_packed ? dev_packed : h->packed, convthresh, first, h->stream));
+        h->fold_w_pending = true;
+    } else {
+        CK(ph_head_launch(a, dev_packed ? dev_packed : h->packed, convthresh, first, h->stream));
+    }
     if (timing_event(h, 3, 1)) return -1;
     if (timing_event(h, 1, 1)) return -1;
     h->t_open = false;
@@ -2049,7 +2111,7 @@ int phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t fi
 int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fused) {
     if (!h || !h->loaded) return fail("phg_ph_step: no batch loaded");
     const PhArgs& p = h->ph;
-    const bool fusable = p.root_only && p.P == 1 && !p.smooth_on && !p.pcv && !h->no_fuse;
+    const bool fusable = p.root_only && p.P == 1 && !p.smooth_on && !p.pcv && !h->no_fuse && !fold_active(h);
     if (out_fused) *out_fused = fusable ? 1 : 0;
     if (!fusable) {
         if (phg_node_sums(h, nullptr)) return -1;
@@ -2089,6 +2151,11 @@ int phg_exchange_layout(phg_handle* h, int32_t* out3) {
 int phg_conv_start(phg_handle* h, const double* dev_convpart) {
     if (!h || !h->loaded) return fail("phg_conv_start: no batch loaded");
     CK(hipSetDevice(h->device));
+    if (h->fold_conv_pending) {   // the last solve's folded update: its partials first
+        CK(fold_conv_launch(h->ph, dev_convpart ? const_cast<double*>(dev_convpart) : h->convpart, h->stream));
+        h->fold_conv_pending = false;
+        h->gate_fused = false;
+    }
     if (!(h->gate_fused && dev_convpart == nullptr))   // after an all-reduce: a small kernel
         CK(conv_gate_launch(dev_convpart ? dev_convpart : h->convpart, h->P, h->gate, h->gate_host,
                             (double)(++h->gate_seq), h->stream));
@@ -2121,6 +2188,26 @@ int phg_conv_finish(phg_handle* h, const double* dev_convpart, double* host_conv
     return phg_conv_wait(h, host_conv);
 }
 
+int phg_set_fold(phg_handle* h, int32_t on, int32_t* active) {
+    if (!h) return fail("phg_set_fold: null handle");
+    if (h->loaded) {
+        CK(hipSetDevice(h->device));
+        if (flush_fold(h)) return -1;
+    }
+    h->fold = on ? 1 : 0;
+    if (active) *active = h->loaded && fold_active(h) ? 1 : 0;
+    return 0;
+}
+
+int phg_fold_partials(phg_handle* h, double* dev_convpart) {
+    if (!h || !h->loaded) return fail("phg_fold_partials: no batch loaded");
+    CK(hipSetDevice(h->device));
+    if (!h->fold_conv_pending) return 0;
+    CK(fold_conv_launch(h->ph, dev_convpart ? dev_convpart : h->convpart, h->stream));
+    h->fold_conv_pending = false;
+    return 0;
+}
+
 int phg_solve_summary(phg_handle* h, int32_t* out2) {
     if (!h || !h->loaded) return fail("phg_solve_summary: no batch loaded");
     out2[0] = h->summary[0];
@@ -2136,6 +2223,7 @@ int phg_ph_update(phg_handle* h, double* host_conv) {
 
 int phg_eval_objective(phg_handle* h, int32_t w_on, int32_t prox_on) {
     if (!h || !h->loaded) return fail("phg_eval_objective: no batch loaded");
+    if (flush_fold(h)) return -1;
     if (materialize_outputs(h)) return -1;
     CK(hipSetDevice(h->device));
     CK(eval_obj_launch(h->S, h->n, h->N, h->x_out, h->c, h->obj_off, h->nonant_col_d, h->xN, h->W,

@@ -200,6 +200,15 @@ struct PdhgArgs {
     // lane-local kernel: 1 = the average iterate's running sums take every PDHG iterate, 2 = every
     // second one (PHG_SUM_STRIDE)
     int sum_stride;
+    // folded PH update (phg_ph_head with the fold on, include/phg.h): the prologue first applies
+    // Update_W of the x it warm-starts from -- W += rho (x - xbar), x = xs_in dc, the bits the last
+    // epilogue stored as xN -- writing W in place (W_rw), the scenario's sum |x - xbar| (conv_s) and
+    // the status of the solve that produced x (status_in -> fold_st), then solves with the new W
+    int fold_w;
+    double* W_rw;           // [S*N] = W
+    double* conv_s;         // [S]
+    int* fold_st;           // [S]
+    const int* status_in;   // [S] statuses of the solve being warm-started from (front copy)
 };
 
 // relative-gap denominator of the termination test (PdhgArgs::gap_const): K = the objective constant
@@ -285,13 +294,20 @@ struct PhArgs {
     double* gate;
     double* gate_host;
     double gate_seq;
+    // folded PH update (PdhgArgs::fold_w): per-scenario sums |x - xbar| and statuses left by the solve
+    // prologue; fold_conv: node_sums_kernel also reduces them into the conv partials of the packed
+    // exchange buffer (nodesum + 2 N_tot)
+    const double* conv_s;
+    const int* fold_st;
+    int fold_conv;
 };
 
 
 // PH terms of nonant t = s*N + k in the min-form subproblem objective (phbase.py:670-760):
 //   c += w_on W;  prox_on: c -= rho xbar (+ p z), q = rho (+ p), const += rho/2 xbar^2 (+ p/2 z^2)
-__device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, double& cc, double& qq, double& pc) {
-    if (a.w_on) cc += a.W[t];
+// (ph_terms_w: with the value of W given -- the folded update's new W)
+__device__ __forceinline__ void ph_terms_w(const PdhgArgs& a, long t, double w, double& cc, double& qq, double& pc) {
+    if (a.w_on) cc += w;
     if (a.prox_on) {
         const double r = a.rho[t];
         const double xb = a.xbar[a.xidx[t]];
@@ -305,6 +321,9 @@ __device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, double& cc, 
             pc += 0.5 * p * z * z;
         }
     }
+}
+__device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, double& cc, double& qq, double& pc) {
+    ph_terms_w(a, t, a.w_on ? a.W[t] : 0.0, cc, qq, pc);
 }
 
 // scaled box of a fixed nonant t (x = d xhat): [v - w, v + w] / d with w = fix_tol max(1, |v|) --

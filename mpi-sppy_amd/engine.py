@@ -281,6 +281,18 @@ class Engine:
         _lib.check(self.lib.phg_ph_step(self.h, float(convthresh), int(bool(first)), ptr(fused)))
         return bool(fused[0])
 
+    def set_fold(self, on):
+        """Folded PH update on / off (phg_set_fold); returns whether this batch's solves take it."""
+        out = np.zeros(1, np.int32)
+        _lib.check(self.lib.phg_set_fold(self.h, int(bool(on)), ptr(out)))
+        return bool(out[0])
+
+    def fold_partials(self):
+        """Reduce the per-scenario partials of a folded W update (the last solve's prologue) into the
+        exchange buffer's partials region (phg_fold_partials; no-op when none is pending) -- before
+        that region is all-reduced."""
+        _lib.check(self.lib.phg_fold_partials(self.h, self._cp_ptr()))
+
     def solve_undo(self):
         """Restore the solve state from before the last solve (phg_solve_undo)."""
         _lib.check(self.lib.phg_solve_undo(self.h))

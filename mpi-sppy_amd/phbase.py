@@ -334,6 +334,7 @@ class PHBase(SPBase):
         and, if PH had converged before the solve that followed it, undo that solve.  Returns
         (conv, undone)."""
         eng = self.engine
+        eng.fold_partials()        # a folded W update's partials (include/phg.h), before the SUM
         if eng.exchange is not None:
             self.mpicomm.allreduce_sum_(eng.convpart_view)
         conv = eng.conv_finish()

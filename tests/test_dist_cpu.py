@@ -53,6 +53,9 @@ class NumpyEngine:
     def convpart_view(self):
         return self.exchange[2 * self.N_tot:]
 
+    def fold_partials(self):
+        pass                       # the stand-in's updates are never folded
+
     def set(self, field, v):
         from mpisppy_amd import _lib
         if field == _lib.F_RHO:

@@ -347,14 +347,17 @@ def test_singleton_row_presolve_same_solutions():
 
 
 # ----------------------------------------------------------------------------- pipelined PH loop
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_pipelined_iteration_matches_sequential(fuse, monkeypatch):
+@pytest.mark.parametrize("fuse,fold", [("0", "1"), ("0", "0"), ("1", "0")])
+def test_pipelined_iteration_matches_sequential(fuse, fold, monkeypatch):
     """PHBase.update_and_solve (solve enqueued gated on the device conv, phg_conv_start/wait) runs
     the same PH as the sequential Compute_Xbar / Update_W / convergence_diff / solve_loop loop,
-    including the break before solve_loop at conv < convthresh (the gated solve is a no-op); with
+    including the break before solve_loop at conv < convthresh (the gated solve is a no-op).  With
     PHG_FUSE=1 the single-GPU step is the fused ph_step_kernel (node sums + W update in one launch),
-    bit-identical too."""
+    bit-identical too.  With the fold (default on this lane-local batch; phg_fold_partials) the W
+    update runs in the next solve's prologue: W, xbar, x bit-identical (the same FMA on the same
+    bits), the convergence metric summed in another order -- equal to 1e-14 relative."""
     monkeypatch.setenv("PHG_FUSE", fuse)
+    monkeypatch.setenv("PHG_FOLD", fold)
     out = []
     for pipe in (True, False):
         ph = _farmer_ph(4, cm=1, PHIterLimit=200, convthresh=1e-3, pdhg_pipeline=pipe)
@@ -363,8 +366,32 @@ def test_pipelined_iteration_matches_sequential(fuse, monkeypatch):
                     ph.nonants().copy(), ph.solve_count))
     (i1, c1, e1, h1, W1, x1, n1, k1), (i0, c0, e0, h0, W0, x0, n0, k0) = out
     assert i1 == i0 < 200 and c1 < 1e-3
-    assert h1 == h0 and c1 == c0 and e1 == e0 and k1 == k0
+    if fold == "1":
+        np.testing.assert_allclose(h1, h0, rtol=1e-14)
+        assert abs(c1 - c0) <= 1e-14 * abs(c0)
+    else:
+        assert h1 == h0 and c1 == c0
+    assert e1 == e0 and k1 == k0
     assert np.array_equal(W1, W0) and np.array_equal(x1, x0) and np.array_equal(n1, n0)
+
+
+def test_folded_update_at_full_size_matches_unfolded(monkeypatch):
+    """farmer cm=10 x 10 000 (the bench's batch): 30 pipelined PH iterations with the folded W update
+    (phg_fold_partials) and without -- W, xbar and x bit-identical after every run, conv history to
+    1e-13 relative; and the multi-GPU form of the fold (pdhg_exchange: the packed buffer all-reduced
+    by a 1-rank communicator, the partials reduced by phg_node_sums / phg_fold_partials) the same."""
+    res = []
+    for fold, exch in (("1", False), ("0", False), ("1", True)):
+        monkeypatch.setenv("PHG_FOLD", fold)
+        opts = dict(PHIterLimit=30, convthresh=1e-10)
+        if exch:
+            opts["pdhg_exchange"] = True
+        ph = _farmer_ph(10000, cm=10, **opts)
+        ph.ph_main(finalize=False)
+        res.append((ph.conv_history, ph.Ws().copy(), ph.xbars().copy(), ph.nonants().copy()))
+    for h, W, xb, x in res[1:]:
+        np.testing.assert_allclose(h, res[0][0], rtol=1e-13)
+        assert np.array_equal(W, res[0][1]) and np.array_equal(xb, res[0][2]) and np.array_equal(x, res[0][3])
 
 
 # ----------------------------------------------------------------------------- non-uniform trees (M3)

@@ -107,6 +107,52 @@ def run(S, N, reps=20):
             "check_ok": bool(ok), "err_xbar": err_xbar, "err_w": err_w, "setup_s": round(setup, 2)}
 
 
+def run_fold(S, N, reps=10):
+    """The folded PH iteration (include/phg.h phg_fold_partials): the W update moves into the next
+    solve's prologue.  Its cost there is measured as the difference of the same short solve (one
+    check trip, max_iter 2) with and without the fold, each preceded by its own update launches
+    (fold: node sums + xbar head; no fold: node sums + W update head).  Folded PH update time =
+    node sums + head + prologue difference; rate = the SURVEY 3-stream bytes over that time."""
+    import torch
+    eng = Engine(synthetic_batch(S, N), device=torch.cuda.current_device(), presolve=False)
+    eng.set(_lib.F_RHO, 1.0)
+    if eng.layout != "local":
+        eng.close()
+        return {"S": S, "N": N, "skipped": f"layout {eng.layout}: the fold is lane-local only"}
+    kw = dict(eps=1e-9, max_iter=2, check_every=2, warm_start=1, schedule=False)
+    eng.solve(0, 0, **kw)                       # a consistent x (scaled state and nonants)
+    out = {}
+    for tag, on in (("fold", True), ("nofold", False)):
+        active = eng.set_fold(on)
+        eng.ph_step(0.0, True)
+        eng.solve(1, 1, **kw)
+        eng.sync()
+        eng.timing_reset(solves=True, updates=True)
+        for _ in range(reps):
+            eng.ph_step(0.0, False)
+            eng.solve(1, 1, **kw)
+        sv_ms, n_sv, _ = eng.timing(0)
+        up_ms, n_up, _ = eng.timing(1)
+        ns_ms, n_ns, _ = eng.timing(2)
+        hd_ms, n_hd, _ = eng.timing(3)
+        eng.timing_reset(solves=False, updates=False)
+        out[tag] = {"active": active, "solve_us": sv_ms / n_sv * 1e3, "update_us": up_ms / n_up * 1e3,
+                    "node_sums_us": ns_ms / max(1, n_ns) * 1e3, "head_us": hd_ms / max(1, n_hd) * 1e3}
+    eng.set_fold(True)
+    eng.close()
+    d_solve = out["fold"]["solve_us"] - out["nofold"]["solve_us"]
+    t_fold = out["fold"]["update_us"] + d_solve
+    alg = 8 * S * N * 3 + 8 * S + 16 * N
+    r = {"S": S, "N": N, "SN": S * N, "bytes_per_update": alg,
+         "fold": {k: round(v, 2) if isinstance(v, float) else v for k, v in out["fold"].items()},
+         "nofold": {k: round(v, 2) if isinstance(v, float) else v for k, v in out["nofold"].items()},
+         "prologue_w_update_us": round(d_solve, 2), "folded_update_us": round(t_fold, 2),
+         "unfolded_update_us": round(out["nofold"]["update_us"], 2),
+         "folded_GBs": round(alg / (t_fold / 1e6) / 1e9, 1),
+         "folded_frac_hbm": round(alg / (t_fold / 1e6) / 1e9 / HBM_PEAK_GBS, 4)}
+    return r
+
+
 def main():
     import torch
     torch.cuda.set_device(0)
@@ -118,11 +164,22 @@ def main():
         r = run(S, N)
         print(json.dumps(r), flush=True)
         out.append(r)
+    fold_cases = ((10000, 100), (100000, 100), (1000000, 100))
+    if os.environ.get("SWEEP_FOLD_CASES"):
+        fold_cases = tuple(tuple(int(v) for v in c.split("x")) for c in os.environ["SWEEP_FOLD_CASES"].split(","))
+    fold = []
+    for S, N in fold_cases:
+        r = run_fold(S, N)
+        print(json.dumps(r), flush=True)
+        fold.append(r)
     if len(sys.argv) > 1:
         json.dump({"kernel": "node_sums_kernel + w_update_kernel (+ fused conv gate)",
                    "bytes_formula": "8*S*N*3 + 8*S + 16*N_tot (SURVEY 8(d)3, rho shared: no rho stream)",
                    "timing": "HIP events on the library stream around each update (phg_timing(1))",
-                   "results": out}, open(sys.argv[1], "w"), indent=1)
+                   "results": out,
+                   "folded": {"what": "W update in the next solve's prologue; its cost = the solve's time "
+                                      "with the fold minus without (one check trip, max_iter 2)",
+                              "results": fold}}, open(sys.argv[1], "w"), indent=1)
 
 
 if __name__ == "__main__":
