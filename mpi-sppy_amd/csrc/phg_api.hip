@@ -893,6 +893,9 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     a.xidx = h->xidx;
     if (dalloc(h, &h->conv_s, (size_t)S)) return -1;
     if (dalloc(h, &h->fold_st, (size_t)S)) return -1;
+    a.conv_s = h->conv_s;      // the folded update's per-scenario partials (fold_conv_kernel, node sums)
+    a.fold_st = h->fold_st;
+    a.fold_conv = 0;
     if (dalloc(h, &h->packed, 2 * (size_t)b->N_tot + 2 * (size_t)P + 3)) return -1;
     h->nodesum = h->packed;
     h->convpart = h->packed + 2 * (size_t)b->N_tot;
