@@ -250,8 +250,9 @@ int  phg_ph_update(phg_handle* h, double* host_conv);
  * solve k-1 (x_{k-2}, W_{k-1}, xbar_{k-1}).  After the last iteration, phg_conv_start on the
  * partials gives conv of the last update; if it is below thr, phg_solve_undo restores the state
  * before the last solve.                                                                         */
-/* Folded update (default for the lane-local layout without smoothing / variable probability;
- * PHG_FOLD=0 turns it off): phg_ph_head then only publishes conv_{k-1} and forms xbar_k; the next
+/* Folded update (lane-local layout without smoothing / variable probability; off by default --
+ * measured slower on farmer 10k, DESIGN.md -- on with phg_set_fold or PHG_FOLD=1): phg_ph_head
+ * then only publishes conv_{k-1} and forms xbar_k; the next
  * phg_solve applies W += rho (x - xbar) in its prologue -- it loads x (its warm start) and W (its
  * objective) anyway, so the update's second read of x and its own launch disappear -- and leaves
  * the per-scenario partials of update k on the device.  The next phg_node_sums reduces them into the

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void safe_bound_kernel(PdhgArgs a, SafeBoundAr
         cc = a.c[sn + j];
         qq = 0.0;
         const int kk = a.lay.col_nonant[j];
-        if (kk >= 0) ph_terms(a, sN + kk, cc, qq, pc);
+        if (kk >= 0) ph_terms(a, sN + kk, kk, cc, qq, pc);
         cc *= d;
         qq *= d * d;
     };

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(64) void pdhg_kernel(PdhgArgs a) {
             const int kk = L.col_nonant[j];
             if (kk >= 0) {
                 const long t = sN + kk;
-                ph_terms(a, t, cc, qq, prox_const);
+                ph_terms(a, t, kk, cc, qq, prox_const);
                 if (a.fix_nonants) fixed_box(a, t, d, lo_, hi_);
             }
             dcs[k] = d;

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             const int kk = a.lay.col_nonant[j];
             if (kk >= 0) {
                 const long tt = sN + kk;
-                ph_terms(a, tt, cc, qq, prox_const);
+                ph_terms(a, tt, kk, cc, qq, prox_const);
                 if (a.fix_nonants) fixed_box(a, tt, d, lo_, hi_);
             }
             c2 += cc * cc;

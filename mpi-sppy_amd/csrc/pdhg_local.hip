@@ -349,12 +349,12 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                     const long t = sN + kk;
                     double w = a.W[t];
                     if (a.fold_w) {   // Update_W (phbase.py:301-326) of the x this solve starts from
-                        const double dv = a.xs_in[b] * dd - a.xbar[a.xidx[t]];
-                        w = fma(a.rho[t], dv, w);
+                        const double dv = a.xs_in[b] * dd - a.xbar[xbar_slot(a, t, kk)];
+                        w = fma(rho_of(a, t, kk), dv, w);
                         a.W_rw[t] = w;
                         dsum += fabs(dv);
                     }
-                    ph_terms_w(a, t, w, cc, qq, prox_const);
+                    ph_terms_w(a, t, kk, w, cc, qq, prox_const);
                     if (a.fix_nonants) fixed_box(a, t, dd, lo_, hi_);
                 }
                 c2 += cc * cc;

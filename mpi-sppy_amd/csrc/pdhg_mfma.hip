@@ -96,7 +96,7 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
                 const int kk = col_nonant[j];
                 if (kk >= 0) {
                     const long t = sN + kk;
-                    ph_terms(a, t, cc, qq, prox_const);
+                    ph_terms(a, t, kk, cc, qq, prox_const);
                     if (a.fix_nonants) fixed_box(a, t, d, lo_, hi_);
                 }
                 c2 += cc * cc;

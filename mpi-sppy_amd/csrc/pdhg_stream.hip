@@ -133,7 +133,7 @@ __global__ __launch_bounds__(NT) void pdhg_stream_kernel(PdhgArgs a) {
         double lo_ = a.cl[b], hi_ = a.cu[b];
         const int kk = a.lay.col_nonant[j];
         if (kk >= 0) {
-            ph_terms(a, sN + kk, cc, qq, prox_const);
+            ph_terms(a, sN + kk, kk, cc, qq, prox_const);
             if (a.fix_nonants) fixed_box(a, sN + kk, d, lo_, hi_);
         }
         c2 += cc * cc;

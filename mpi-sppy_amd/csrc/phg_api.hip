@@ -196,9 +196,12 @@ struct phg_handle {
     // relative-gap test on the whole objective (PdhgArgs::gap_const); PHG_GAP_RAW=1 turns it off
     int gap_const = 1;
     int sum_stride = 1;        // PdhgArgs::sum_stride (PHG_SUM_STRIDE)
-    // folded PH update (phg_ph_head -> the next phg_solve's prologue does Update_W; PHG_FOLD=0 off):
-    // on for the lane-local layout without smoothing / variable probability
-    int fold = 1;
+    // folded PH update (phg_ph_head -> the next phg_solve's prologue does Update_W), lane-local
+    // layout without smoothing / variable probability.  OFF by default (PHG_FOLD=1 / phg_set_fold):
+    // measured on farmer 10k it slows the PDHG launch by ~9 us (the prologue's dependent W-update
+    // chain in every wave) for a ~2.5 us shorter update -- 0.3465 vs 0.340 ms per PH iteration; at
+    // S N = 1e8 (S = 1e6, N = 100) 797 vs 847 us per update (tools/ph_update_sweep.py)
+    int fold = 0;
     bool fold_w_pending = false;      // xbar of update k is in place, its W update not yet applied
     bool fold_conv_pending = false;   // the last solve did a folded update: its conv partials are
                                       // per scenario (conv_s / fold_st), not yet in any partials buffer
@@ -300,7 +303,7 @@ int phg_create(int device, phg_handle** out) {
     if (const char* ev = std::getenv("PHG_FUSE")) h->no_fuse = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_GAP_RAW")) h->gap_const = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_SUM_STRIDE")) h->sum_stride = std::atoi(ev) == 2 ? 2 : 1;
-    if (const char* ev = std::getenv("PHG_FOLD")) h->fold = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("PHG_FOLD")) h->fold = std::atoi(ev) != 0 ? 1 : 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return fail("phg_create: hipStreamCreate failed");
@@ -775,12 +778,17 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     // segments per level cap (PHG_NODESEG_MAX: tuning knob for tools/ph_update_sweep.py)
     int seg_max = 256;   // (512 -> 256 measured: S*N 1e6 / 1e7 / 1e8 33 -> 29, 73 -> 71, ~670 -> ~657 us)
     if (const char* ev = std::getenv("PHG_NODESEG_MAX")) seg_max = std::max(1, std::atoi(ev));
+    const bool seg_env = std::getenv("PHG_NODESEG_MAX") != nullptr;
     for (int lv = 0; lv < L; ++lv) {
         const int klen = b->level_len[lv];
+        // narrow levels get more segments: a node-sum workgroup covers 256 nonants of its segment
+        // (blockIdx.y), so with klen <= 256 the grid is the segment count alone -- 1024 of them keep
+        // ~4 workgroups per CU in flight (S N = 1e8 as 1e6 x 100: 256 segments ran at 2.3 TB/s)
+        const int seg_cap = seg_env ? seg_max : std::max(seg_max, 1024 / std::max(1, (klen + 255) / 256));
         // ~8 scenarios per thread of a 256-thread workgroup: enough workgroups to hide the load
         // latency at small S, whole-row coalesced streaming at large S
         // and at most ~256 segments per level, so the final per-node sums stay short at large S
-        const int chunk = std::max(klen >= 256 ? 8 : 8 * (256 / std::max(1, klen)), (S + seg_max - 1) / seg_max);
+        const int chunk = std::max(klen >= 256 ? 8 : 8 * (256 / std::max(1, klen)), (S + seg_cap - 1) / seg_cap);
         int s = 0;
         while (s < S) {
             const int g = b->scen_node[s * L + lv];
@@ -1981,6 +1989,8 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.vals = h->vals; a.c = h->c; a.cl = h->cl; a.cu = h->cu; a.rl = h->rl; a.ru = h->ru;
     a.dc = h->dc; a.dr = h->dr; a.eta = h->eta; a.obj_off = h->obj_off; a.bnorm = h->bnorm;
     a.W = h->W; a.rho = h->rho; a.xbar = h->xbar; a.xidx = h->xidx; a.fixed = h->fixed;
+    a.root_only = h->ph.root_only;
+    a.rho_k = h->ph.rho_k;
     a.Z = h->Z; a.Psm = h->Psm; a.smooth_on = h->smooth_on;
     // warm start from the front copy, results into the back copy (swapped after the launch);
     // unscaled x / y are not stored by the solve (materialize_outputs derives them on demand)

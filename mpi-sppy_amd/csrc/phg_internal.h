@@ -151,6 +151,7 @@ struct PdhgArgs {
                             // null -- the W update then reads N doubles instead of streaming S*N
     const double* xbar;     // [N_tot]
     const int*    xidx;     // [S*N]   xbar slot of (s,k)
+    int root_only;          // xidx[s*N + k] == k for every s (two-stage): xidx is not read
     const double* fixed;    // [S*N]
     const double* Z;        // [S*N]   smoothing centre z (smoothed PH, phbase.py:641-760)
     const double* Psm;      // [S*N]   smoothing weight p
@@ -306,11 +307,21 @@ struct PhArgs {
 // PH terms of nonant t = s*N + k in the min-form subproblem objective (phbase.py:670-760):
 //   c += w_on W;  prox_on: c -= rho xbar (+ p z), q = rho (+ p), const += rho/2 xbar^2 (+ p/2 z^2)
 // (ph_terms_w: with the value of W given -- the folded update's new W)
-__device__ __forceinline__ void ph_terms_w(const PdhgArgs& a, long t, double w, double& cc, double& qq, double& pc) {
+// kk = the nonant's index in its scenario (t = s N + kk): two-stage batches (root_only) read xbar[kk]
+// and, with rho the same in every scenario (rho_k), rho_k[kk] -- no dependent index load, no S*N
+// stream for rho
+__device__ __forceinline__ int xbar_slot(const PdhgArgs& a, long t, int kk) {
+    return a.root_only ? kk : a.xidx[t];
+}
+__device__ __forceinline__ double rho_of(const PdhgArgs& a, long t, int kk) {
+    return a.rho_k ? a.rho_k[kk] : a.rho[t];
+}
+__device__ __forceinline__ void ph_terms_w(const PdhgArgs& a, long t, int kk, double w, double& cc, double& qq,
+                                           double& pc) {
     if (a.w_on) cc += w;
     if (a.prox_on) {
-        const double r = a.rho[t];
-        const double xb = a.xbar[a.xidx[t]];
+        const double r = rho_of(a, t, kk);
+        const double xb = a.xbar[xbar_slot(a, t, kk)];
         cc -= r * xb;
         qq = r;
         pc += 0.5 * r * xb * xb;
@@ -322,8 +333,8 @@ __device__ __forceinline__ void ph_terms_w(const PdhgArgs& a, long t, double w, 
         }
     }
 }
-__device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, double& cc, double& qq, double& pc) {
-    ph_terms_w(a, t, a.w_on ? a.W[t] : 0.0, cc, qq, pc);
+__device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, int kk, double& cc, double& qq, double& pc) {
+    ph_terms_w(a, t, kk, a.w_on ? a.W[t] : 0.0, cc, qq, pc);
 }
 
 // scaled box of a fixed nonant t (x = d xhat): [v - w, v + w] / d with w = fix_tol max(1, |v|) --
