@@ -349,7 +349,8 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                     const long t = sN + kk;
                     double w = a.W[t];
                     if (a.fold_w) {   // Update_W (phbase.py:301-326) of the x this solve starts from
-                        const double dv = a.xs_in[b] * dd - a.xbar[xbar_slot(a, t, kk)];
+                        // the epilogue's xN = xs * dc, rounded as it was (no FMA contraction here)
+                        const double dv = __dsub_rn(__dmul_rn(a.xs_in[b], dd), a.xbar[xbar_slot(a, t, kk)]);
                         w = fma(rho_of(a, t, kk), dv, w);
                         a.W_rw[t] = w;
                         dsum += fabs(dv);

@@ -203,6 +203,7 @@ struct phg_handle {
     // S N = 1e8 (S = 1e6, N = 100) 797 vs 847 us per update (tools/ph_update_sweep.py)
     int fold = 0;
     bool fold_w_pending = false;      // xbar of update k is in place, its W update not yet applied
+    bool xn_external = false;         // PHG_F_XN was set by the caller: xN != xs dc until the next solve
     bool fold_conv_pending = false;   // the last solve did a folded update: its conv partials are
                                       // per scenario (conv_s / fold_st), not yet in any partials buffer
     double* conv_s = nullptr;
@@ -1932,6 +1933,7 @@ int phg_set(phg_handle* h, int32_t f, const double* in) {
         in = packed.data();
     }
     CK(hipMemcpyAsync(p, in, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    if (f == PHG_F_XN) h->xn_external = true;
     if (f == PHG_F_RHO) {   // rho the same in every scenario? then the W update reads its [N] copy
         bool shared = true;
         for (size_t e = (size_t)h->N; e < cnt && shared; ++e) shared = in[e] == in[e % (size_t)h->N];
@@ -2022,7 +2024,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.gap_const = h->gap_const;
     a.sum_stride = h->sum_stride;
     if (h->fold_w_pending) {
-        if (!fold_active(h)) {
+        if (!fold_active(h) || h->xn_external) {   // the prologue's x = xs dc would not be the caller's xN
             if (flush_fold(h)) return -1;
         } else {
             a.fold_w = 1;
@@ -2041,6 +2043,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
     if (timing_event(h, 0, 1)) return -1;
+    h->xn_external = false;
     if (o->safe_bound && !o->fix_nonants) {   // bound.hip: certificates whatever the statuses
         if (!h->sb.Y) {
             if (dalloc(h, &h->sb.Y, (size_t)h->S * h->m)) return -1;
