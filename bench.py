@@ -385,7 +385,9 @@ def main():
                    "parallelism": f"scenario shards over {world} GPU(s), one packed all-reduce per PH iteration"
                        + (" (libphg RCCL group)" if type(comm).__name__ == "PhgGroupComm" else ""),
                    "pdhg_layout": eng.layout, "lanes_per_scenario": eng.lanes_per_scenario,
-                   "presolve_rows_folded": eng.rows_folded},
+                   "presolve_rows_folded": eng.rows_folded,
+                   # value form the workgroup kernel streams (phg_values_info): per scenario vs one copy
+                   "values": eng.values_info() if eng.layout == "block" else None},
         # fp64 VALU-bound kernels (lane-local / gather): flops against the fp64 peak; the streaming
         # block kernel: algorithmic bytes against HBM
         "roofline": (mfma_rf if mfma_rf is not None else

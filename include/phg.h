@@ -72,7 +72,25 @@ typedef struct phg_batch {
      * prob_coeff in the node sums; W of a zero-probability nonant is kept at 0 (phbase.py:323-326).
      * NULL when unused.                                                                      */
     const double*  prob_coeff_var;
+    /* Value forms ("values: shared [nnz] or per-scenario [S*nnz] or a sparse delta
+     * list"; the reference's scenario_creator builds each scenario's model in full, so which
+     * coefficients vary is the instance's, e.g. netdes varies only the u_e of its vubs,
+     * examples/netdes/netdes.py:39-80):
+     *   PHG_VALS_PER_SCENARIO (0; callers that zero the struct): vals is [S*nnz];
+     *   PHG_VALS_SHARED       (1): vals is [nnz], one matrix for every scenario;
+     *   PHG_VALS_DELTA        (2): vals is [nnz], a shared base; the n_delta CSR positions
+     *                             delta_pos[] (strictly increasing) take per-scenario values
+     *                             delta_vals[S*n_delta] (scenario-major).
+     * Whatever the form, phg_load_batch finds the positions whose value differs between scenarios;
+     * when they are few (<= nnz/2) and the workgroup layout is chosen, all scenarios share one
+     * scaling and one copy of the constant entries, and the solver streams only the varying ones
+     * (PHG_DELTA=0 in the environment: per-scenario scaling and copies, for A/B runs).          */
+    int32_t vals_form;
+    int32_t n_delta;
+    const int32_t* delta_pos;
+    const double*  delta_vals;
 } phg_batch;
+enum { PHG_VALS_PER_SCENARIO = 0, PHG_VALS_SHARED = 1, PHG_VALS_DELTA = 2 };
 
 typedef struct phg_opts {
     double  eps_rel;       /* relative KKT tolerance (PDLP-style), e.g. 1e-9            */
@@ -198,6 +216,12 @@ int  phg_get_i32(phg_handle* h, int32_t field, int32_t* host_out);
 /* shared-matrix MFMA layout: out4 = {row tiles, column tiles, 16x4 fragments with a nonzero in
  * A x, in A^T y} (each is one v_mfma_f64_16x16x4_f64 per PDHG iteration per 16 scenarios)       */
 int  phg_mfma_info(phg_handle* h, int32_t* out4);
+/* value form of the loaded batch (phg_batch.vals_form): out4 = {CSR positions whose value differs
+ * between scenarios, 1 if all scenarios share one scaling and one copy of the constant entries (the
+ * delta form is in use), matrix values the PDHG kernel reads PER SCENARIO in one A x + A^T y,
+ * values it reads from the ONE shared copy in one A x + A^T y} (workgroup layout; the other layouts
+ * report {varying, 0, 0, 0})                                                                        */
+int  phg_values_info(phg_handle* h, int32_t* out4);
 int  phg_info(phg_handle* h, int32_t* out8);   /* S, n, m, nnz, N, N_tot, kernel variant
                                                   (>= 100: lane-local, >= 200: workgroup,
                                                   >= 300: shared-matrix MFMA, 400 + K:

@@ -27,7 +27,11 @@ class PhgBatch(C.Structure):
         ("node_off", i32p), ("N_tot", C.c_int32), ("prob", f64p), ("prob_coeff", f64p),
         ("scen_global0", C.c_int32), ("S_global", C.c_int32), ("virt_nproc", C.c_int32),
         ("prob_coeff_var", f64p),
+        ("vals_form", C.c_int32), ("n_delta", C.c_int32), ("delta_pos", i32p), ("delta_vals", f64p),
     ]
+
+
+VALS_PER_SCENARIO, VALS_SHARED, VALS_DELTA = 0, 1, 2
 
 
 class PhgOpts(C.Structure):
@@ -82,6 +86,7 @@ SIGNATURES = {
     "phg_set_fold": (C.c_int, [C.c_void_p, C.c_int32, i32p]),
     "phg_ph_step": (C.c_int, [C.c_void_p, C.c_double, C.c_int32, i32p]),
     "phg_mfma_info": (C.c_int, [C.c_void_p, i32p]),
+    "phg_values_info": (C.c_int, [C.c_void_p, i32p]),
     "phg_group_unique_id": (C.c_int, [C.c_void_p]),
     "phg_create_group": (C.c_int, [C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
     "phg_group_size": (C.c_int, [C.c_void_p, i32p]),

@@ -78,6 +78,18 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
     const double* rv = B.rvals + (long)s * B.vstride_r;
     const double* cv = B.cvals + (long)s * B.vstride_c;
+    // delta form (BlockLayout::rdrow): entry rows with a varying entry come from the scenario's blocks
+    const double* rvd = B.rvd ? B.rvd + (long)s * B.dstride_r : nullptr;
+    const double* cvd = B.cvd ? B.cvd + (long)s * B.dstride_c : nullptr;
+    // value of piece entry e (entry row R = e / NT, uniform over the workgroup)
+    auto rval = [&](int e, int R) {
+        const int d = B.rdrow[R];
+        return d >= 0 ? rvd[(long)d * NT + t] : rv[e];
+    };
+    auto cval = [&](int e, int R) {
+        const int d = B.cdrow[R];
+        return d >= 0 ? cvd[(long)d * NT + t] : cv[e];
+    };
 
     // ------------------------------------------------------------------ columns owned
     int cj[CPL], cf[CPL], cn[CPL];
@@ -146,7 +158,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll
             for (int k = 0; k < RE; ++k) {
                 const int e = off + k * NT + t;
-                rvr[ps][k] = k < kk ? rv[e] : 0.0;
+                rvr[ps][k] = k < kk ? rval(e, off / NT + k) : 0.0;
                 rir[ps][k] = k < kk ? B.ridx[e] : 0;
             }
             off += kk * NT;
@@ -160,7 +172,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll
             for (int k = 0; k < CE; ++k) {
                 const int e = off + k * NT + t;
-                cvr[ps][k] = k < kk ? cv[e] : 0.0;
+                cvr[ps][k] = k < kk ? cval(e, off / NT + k) : 0.0;
                 cir[ps][k] = k < kk ? B.cidx[e] : 0;
             }
             off += kk * NT;
@@ -182,7 +194,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
                     const int e = off + k * NT + t;
-                    acc = fma(rv[e], xl[B.ridx[e]], acc);
+                    acc = fma(rval(e, off / NT + k), xl[B.ridx[e]], acc);
                 }
                 off += kk * NT;
             }
@@ -206,7 +218,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
                     const int e = off + k * NT + t;
-                    acc = fma(cv[e], yl[B.cidx[e]], acc);
+                    acc = fma(cval(e, off / NT + k), yl[B.cidx[e]], acc);
                 }
                 off += kk * NT;
             }

@@ -114,6 +114,12 @@ struct phg_handle {
     int bshape[8] = {0};
     std::vector<int> block_rperm, block_cperm;   // piece layout -> CSR position (host copies)
     bool vals_shared = false;
+    // delta value form (phg_batch.vals_form): vary[p] = CSR position p differs between scenarios;
+    // delta_scale = one Ruiz scaling for every scenario (from the element-wise mean |a|), so the
+    // workgroup kernel streams per scenario only the piece-entry rows holding a varying entry
+    std::vector<char> vary;
+    int n_vary = 0;
+    bool delta_scale = false;
     int layout_policy = PHG_LAYOUT_AUTO;
     int vshape[6] = {0};
     int lshape[4] = {0};
@@ -1031,7 +1037,9 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
 static int build_block_values(phg_handle* h) {
     BlockLayout& L = h->blk;
     const int Er = (int)h->block_rperm.size(), Ec = (int)h->block_cperm.size();
-    const int Sv = h->vals_shared ? 1 : h->S;
+    const bool one = h->vals_shared || h->delta_scale;   // one copy of the (constant) entries
+    const int Sv = one ? 1 : h->S;
+    const int NT = h->bshape[0];
     int* rperm;
     int* cperm;
     double* rv;
@@ -1044,8 +1052,40 @@ static int build_block_values(phg_handle* h) {
     CK(piece_gather_launch(h->vals, h->nnz, cperm, Ec, Sv, cv, h->stream));
     L.rvals = rv;
     L.cvals = cv;
-    L.vstride_r = h->vals_shared ? 0 : Er;
-    L.vstride_c = h->vals_shared ? 0 : Ec;
+    L.vstride_r = one ? 0 : Er;
+    L.vstride_c = one ? 0 : Ec;
+    // delta form: per-scenario copies of the entry rows that hold a varying entry
+    auto deltas = [&](const std::vector<int>& perm, int E, int* drow, const double** dv, long* dstride) {
+        for (int R = 0; R < 32; ++R) drow[R] = -1;
+        *dv = nullptr;
+        *dstride = 0;
+        if (!h->delta_scale) return 0;
+        const int rows = E / NT;
+        if (rows > 32) return fail("phg_load_batch: piece layout has more than 32 entry rows");
+        std::vector<int> dperm;
+        int nd = 0;
+        for (int R = 0; R < rows; ++R) {
+            bool any = false;
+            for (int t = 0; t < NT; ++t) {
+                const int p = perm[(size_t)R * NT + t];
+                any |= p >= 0 && h->vary[p];
+            }
+            if (!any) continue;
+            drow[R] = nd++;
+            dperm.insert(dperm.end(), perm.begin() + (size_t)R * NT, perm.begin() + (size_t)(R + 1) * NT);
+        }
+        if (!nd) return 0;
+        int* dp;
+        double* out;
+        if (dput(h, &dp, dperm.data(), dperm.size())) return -1;
+        if (dalloc(h, &out, (size_t)h->S * dperm.size())) return -1;
+        CK(piece_gather_launch(h->vals, h->nnz, dp, (int)dperm.size(), h->S, out, h->stream));
+        *dv = out;
+        *dstride = (long)dperm.size();
+        return 0;
+    };
+    if (deltas(h->block_rperm, Er, L.rdrow, &L.rvd, &L.dstride_r)) return -1;
+    if (deltas(h->block_cperm, Ec, L.cdrow, &L.cvd, &L.dstride_c)) return -1;
     return 0;
 }
 
@@ -1437,6 +1477,38 @@ static int build_stream_values(phg_handle* h) {
     return 0;
 }
 
+// ----------------------------------------------------------------------------- value forms
+// phg_batch.vals_form: every entry point works on the per-scenario [S*nnz] form; the shared and delta
+// forms are expanded here (store holds the expansion, out points into it).  Returns 0 / -1.
+static int normalize_vals(const phg_batch* in, phg_batch& out, std::vector<double>& store, const char* who) {
+    out = *in;
+    if (in->vals_form == PHG_VALS_PER_SCENARIO || !in->vals) return 0;
+    if (in->vals_form != PHG_VALS_SHARED && in->vals_form != PHG_VALS_DELTA)
+        return fail(std::string(who) + ": unknown vals_form");
+    if (in->S <= 0 || in->nnz <= 0) return fail(std::string(who) + ": empty batch");
+    const size_t S = (size_t)in->S, nnz = (size_t)in->nnz;
+    store.resize(S * nnz);
+    for (size_t s = 0; s < S; ++s) std::memcpy(store.data() + s * nnz, in->vals, nnz * sizeof(double));
+    if (in->vals_form == PHG_VALS_DELTA) {
+        const int nd = in->n_delta;
+        if (nd < 0 || (nd > 0 && (!in->delta_pos || !in->delta_vals)))
+            return fail(std::string(who) + ": delta form needs n_delta >= 0, delta_pos and delta_vals");
+        for (int d = 0; d < nd; ++d) {
+            const int p = in->delta_pos[d];
+            if (p < 0 || p >= in->nnz || (d > 0 && p <= in->delta_pos[d - 1]))
+                return fail(std::string(who) + ": delta_pos must be strictly increasing CSR positions");
+        }
+        for (size_t s = 0; s < S; ++s)
+            for (int d = 0; d < nd; ++d) store[s * nnz + in->delta_pos[d]] = in->delta_vals[s * nd + d];
+    }
+    out.vals = store.data();
+    out.vals_form = PHG_VALS_PER_SCENARIO;
+    out.n_delta = 0;
+    out.delta_pos = nullptr;
+    out.delta_vals = nullptr;
+    return 0;
+}
+
 // ----------------------------------------------------------------------------- presolve
 // Singleton rows (PDLP-style presolve): a row  lo <= a x_j <= hi  with ONE nonzero, on a column
 // that is not a nonant, is the column bound  lo/a <= x_j <= hi/a  (swapped for a < 0).  The LP is
@@ -1620,8 +1692,12 @@ static void implied_bounds(const phg_batch* b, std::vector<double>& L, std::vect
         if (free_any[j]) free_cols.push_back(j);
 }
 
-int phg_implied_bounds(const phg_batch* b, double* lo, double* hi, int32_t* n_free) {
-    if (!b || !lo || !hi) return fail("phg_implied_bounds: null argument");
+int phg_implied_bounds(const phg_batch* b_in, double* lo, double* hi, int32_t* n_free) {
+    if (!b_in || !lo || !hi) return fail("phg_implied_bounds: null argument");
+    phg_batch bx;
+    std::vector<double> vstore;
+    if (normalize_vals(b_in, bx, vstore, "phg_implied_bounds")) return -1;
+    const phg_batch* b = &bx;
     if (b->S <= 0 || b->n <= 0 || b->m <= 0 || !b->rowptr || !b->colidx || !b->vals || !b->col_lo ||
         !b->col_hi || !b->row_lo || !b->row_hi)
         return fail("phg_implied_bounds: incomplete batch");
@@ -1651,8 +1727,11 @@ int phg_presolve_info(phg_handle* h, int32_t* out2) {
 int phg_plan(const phg_batch* b_in, int32_t* out8) {
     if (!b_in || !out8) return fail("phg_plan: null argument");
     if (b_in->n <= 0 || b_in->m <= 0 || !b_in->rowptr || !b_in->colidx) return fail("phg_plan: empty pattern");
+    phg_batch bx;
+    std::vector<double> vstore;
+    if (normalize_vals(b_in, bx, vstore, "phg_plan")) return -1;
     Presolved P;   // the plan of what phg_load_batch would run (default policy: presolve on)
-    presolve_singletons(b_in, P);
+    presolve_singletons(&bx, P);
     const phg_batch* b = &P.b;
     LocalPlan plan;
     int sh[4] = {0, 0, 0, 0};
@@ -1678,8 +1757,13 @@ int phg_plan(const phg_batch* b_in, int32_t* out8) {
     return 0;
 }
 
-int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
-    if (!h || !b_in) return fail("phg_load_batch: null argument");
+int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
+    if (!h || !b_arg) return fail("phg_load_batch: null argument");
+    if (!b_arg->vals) return fail("phg_load_batch: no values");
+    phg_batch bx;
+    std::vector<double> vstore;
+    if (normalize_vals(b_arg, bx, vstore, "phg_load_batch")) return -1;
+    const phg_batch* b_in = &bx;
     const phg_batch* b = b_in;
     if (h->loaded) return fail("phg_load_batch: handle already holds a batch");
     if (b->S <= 0 || b->n <= 0 || b->m <= 0 || b->nnz <= 0 || b->N <= 0 || b->L <= 0)
@@ -1730,12 +1814,16 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     }
     // one matrix for all scenarios? (then the block kernel streams a single copy, and the MFMA
     // layout applies)
-    {
-        bool same = true;
+    {   // ... and which positions vary (the delta form, whatever form the caller passed)
         const size_t nz = (size_t)b->nnz;
-        for (int s2 = 1; s2 < b->S && same; ++s2)
-            same = std::memcmp(b->vals, b->vals + s2 * nz, nz * sizeof(double)) == 0;
-        h->vals_shared = same;
+        h->vary.assign(nz, 0);
+        for (int s2 = 1; s2 < b->S; ++s2) {
+            const double* v = b->vals + s2 * nz;
+            for (size_t p = 0; p < nz; ++p) h->vary[p] |= (char)(v[p] != b->vals[p]);
+        }
+        h->n_vary = 0;
+        for (size_t p = 0; p < nz; ++p) h->n_vary += h->vary[p];
+        h->vals_shared = h->n_vary == 0;
     }
     // layout: shared-matrix MFMA > lane-local (block-structured patterns) > wave gather
     // (n, m <= 256) > workgroup block
@@ -1761,6 +1849,11 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
         br = build_block_layout(h, b, colptr, csc_row, csc_p);
         if (br < 0 || (br > 0 && pol == PHG_LAYOUT_BLOCK)) return -1;
         h->variant = -1;
+        // few varying entries: one scaling for all scenarios, so the constant entries have ONE
+        // scaled copy and only the varying ones stream per scenario (build_block_values)
+        const char* ed = std::getenv("PHG_DELTA");
+        const bool delta_off = ed && std::atoi(ed) == 0;
+        h->delta_scale = br == 0 && !delta_off && h->n_vary > 0 && 2L * h->n_vary <= (long)b->nnz;
     }
     if (h->mfma_variant < 0 && lr != 0 && gr != 0 && br != 0) {
         if (build_stream_layout(h, b, colptr, csc_row, csc_p, pol)) return -1;
@@ -1846,6 +1939,17 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     if (dalloc(h, &scratch, (size_t)S * (2 * n + 2 * m))) return -1;
     pa.vals = h->vals; pa.dc = h->dc; pa.dr = h->dr; pa.cl = h->cl; pa.cu = h->cu; pa.rl = h->rl;
     pa.ru = h->ru; pa.eta = h->eta; pa.bnorm = h->bnorm; pa.scratch = scratch;
+    pa.vmean = nullptr;
+    if (h->delta_scale) {   // Ruiz on the element-wise mean |a| over the scenarios (same dc, dr everywhere)
+        std::vector<double> vm((size_t)nnz, 0.0);
+        for (int s = 0; s < S; ++s)
+            for (int p = 0; p < nnz; ++p) vm[p] += std::fabs(b->vals[(size_t)s * nnz + p]);
+        for (int p = 0; p < nnz; ++p) vm[p] /= (double)S;
+        double* dp;
+        if (dput(h, &dp, vm.data(), vm.size())) return -1;
+        pa.vmean = dp;
+        if (dalloc(h, &pa.vm_scratch, (size_t)S * nnz)) return -1;
+    }
     CK(prep_launch(pa, h->stream));
     {   // safe bounds (bound.hip): pattern in CSR / CSC, implied column bounds, repair candidates
         std::vector<double> il, ih;
@@ -1865,6 +1969,20 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_in) {
     if (h->stream_layout && build_stream_values(h)) return -1;
     CK(hipStreamSynchronize(h->stream));
     h->loaded = true;
+    return 0;
+}
+
+int phg_values_info(phg_handle* h, int32_t* o) {
+    if (!h || !h->loaded || !o) return fail("phg_values_info: no batch loaded");
+    o[0] = h->n_vary;
+    o[1] = h->delta_scale ? 1 : 0;
+    o[2] = o[3] = 0;
+    if (h->block_variant >= 0) {
+        const long E = (long)h->block_rperm.size() + (long)h->block_cperm.size();
+        if (h->delta_scale) { o[2] = (int32_t)(h->blk.dstride_r + h->blk.dstride_c); o[3] = (int32_t)E; }
+        else if (h->vals_shared) o[3] = (int32_t)E;
+        else o[2] = (int32_t)E;
+    }
     return 0;
 }
 

@@ -57,6 +57,14 @@ struct BlockLayout {
     const double* rvals;    // [S or 1][sum rk NT] scaled values, row pieces (0 on padding)
     const double* cvals;    // [S or 1][sum ck NT] scaled values, column pieces
     long vstride_r, vstride_c;   // per-scenario strides (0: one matrix shared by all scenarios)
+    // delta form (phg_batch.vals_form; one scaling for all scenarios): entry row R (the NT entries
+    // e = R NT .. R NT + NT - 1 of the piece-major arrays) holding a varying entry reads its values
+    // from the scenario's block rdrow[R] of rvd ([S][nd_r NT]; the row's constant entries copied into
+    // it too), every other entry row from the shared rvals (vstride_r = 0); -1 = shared
+    int rdrow[32], cdrow[32];
+    const double* rvd;
+    const double* cvd;
+    long dstride_r, dstride_c;
 };
 
 // Shared-matrix MFMA layout (pdhg_mfma.hip): the A operands of v_mfma_f64_16x16x4_f64 for A x
@@ -245,6 +253,11 @@ struct PrepArgs {
     double* eta;            // [S]
     double* bnorm;          // [S]
     double* scratch;        // [S*(2n+2m)]
+    // non-null: the Ruiz / Pock-Chambolle scalings are those of this [nnz] matrix (the element-wise
+    // mean |a| over the scenarios), the same in every scenario, applied to each scenario's values;
+    // vm_scratch [S*nnz] holds each workgroup's running copy of it
+    const double* vmean;
+    double* vm_scratch;
 };
 
 struct NodeSeg {           // a contiguous scenario range inside one node (one level)

@@ -37,25 +37,36 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     double* pw = pv + n;       // [m]
     for (int j = tid; j < n; j += 256) dc[j] = 1.0;
     for (int i = tid; i < m; i += 256) dr[i] = 1.0;
+    // shared scaling (PrepArgs::vmean): the norms come from this workgroup's copy of the mean matrix,
+    // scaled alongside -- every workgroup computes the same dc, dr
+    double* vm = v;
+    if (a.vmean) {
+        vm = a.vm_scratch + (long)s * nnz;
+        for (int p = tid; p < nnz; p += 256) vm[p] = a.vmean[p];
+    }
     __syncthreads();
     for (int pass = 0; pass <= a.ruiz_iters; ++pass) {
         const bool pock = (pass == a.ruiz_iters);
         for (int i = tid; i < m; i += 256) {
             double acc = 0.0;
             for (int p = a.rowptr[i]; p < a.rowptr[i + 1]; ++p)
-                acc = pock ? acc + fabs(v[p]) : fmax(acc, fabs(v[p]));
+                acc = pock ? acc + fabs(vm[p]) : fmax(acc, fabs(vm[p]));
             rs[i] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
         }
         for (int j = tid; j < n; j += 256) {
             double acc = 0.0;
             for (int t = a.colptr[j]; t < a.colptr[j + 1]; ++t) {
-                const double av = fabs(v[a.csc_p[t]]);
+                const double av = fabs(vm[a.csc_p[t]]);
                 acc = pock ? acc + av : fmax(acc, av);
             }
             cs[j] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
         }
         __syncthreads();
-        for (int p = tid; p < nnz; p += 256) v[p] *= rs[a.row_of_p[p]] * cs[a.colidx[p]];
+        for (int p = tid; p < nnz; p += 256) {
+            const double f = rs[a.row_of_p[p]] * cs[a.colidx[p]];
+            v[p] *= f;
+            if (vm != v) vm[p] *= f;
+        }
         for (int j = tid; j < n; j += 256) dc[j] *= cs[j];
         for (int i = tid; i < m; i += 256) dr[i] *= rs[i];
         __syncthreads();

@@ -114,6 +114,17 @@ class BatchArrays:
         b.prob, b.prob_coeff = k(as_f64(self.prob)), k(as_f64(self.prob_coeff))
         b.scen_global0, b.S_global, b.virt_nproc = self.scen_global0, self.S_global, self.virt_nproc
         b.prob_coeff_var = k(as_f64(self.prob_coeff_var)) if self.prob_coeff_var is not None else None
+        form = getattr(self, "vals_form", _lib.VALS_PER_SCENARIO)
+        if form == _lib.VALS_SHARED:
+            if not (self.vals == self.vals[0]).all():
+                raise ValueError("vals_form SHARED: the scenarios' matrices differ")
+            b.vals, b.vals_form = k(as_f64(self.vals[0])), form
+        elif form == _lib.VALS_DELTA:
+            # the SURVEY 8(b) sparse delta list: the positions whose value differs from scenario 0's
+            pos = np.flatnonzero((self.vals != self.vals[0]).any(axis=0)).astype(np.int32)
+            b.vals, b.vals_form = k(as_f64(self.vals[0])), form
+            b.n_delta, b.delta_pos = len(pos), k(as_i32(pos))
+            b.delta_vals = k(as_f64(self.vals[:, pos]))
         return b, keep
 
 
@@ -187,6 +198,15 @@ class Engine:
         pi = np.zeros(2, np.int32)
         _lib.check(self.lib.phg_presolve_info(self.h, ptr(pi)))
         self.rows_folded, self.rows_kept = int(pi[0]), int(pi[1])
+
+    def values_info(self):
+        """Value form of the loaded batch (phg_values_info): positions varying between scenarios,
+        whether the shared-scaling delta form is in use, and the matrix values one A x + A^T y of
+        the workgroup kernel reads per scenario / from the one shared copy."""
+        out = np.zeros(4, np.int32)
+        _lib.check(self.lib.phg_values_info(self.h, ptr(out)))
+        return {"varying": int(out[0]), "delta": bool(out[1]), "per_scenario_vals": int(out[2]),
+                "shared_vals": int(out[3])}
 
     def mfma_fragments(self):
         """MFMA instructions per PDHG iteration per 16 scenarios (nonzero 16x4 fragments of A x and

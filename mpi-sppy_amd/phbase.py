@@ -103,6 +103,8 @@ class PHBase(SPBase):
         prob = [m._mpisppy_probability for m in models]
         batch = BatchArrays(models, self.all_nodenames, prob, self.scen_global0,
                             len(self.all_scenario_names), self._virt_nproc())
+        # how the values cross the C ABI (phg_batch.vals_form: 0 per scenario, 1 shared, 2 delta list)
+        batch.vals_form = int(self.options.get("pdhg_vals_form", _lib.VALS_PER_SCENARIO))
         device, stream, exchange = self._device_setup(batch)
         self.engine = Engine(batch, device=device, stream=stream, exchange=exchange,
                              layout=self.options.get("pdhg_layout", "auto"),

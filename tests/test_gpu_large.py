@@ -85,6 +85,54 @@ def test_prox_qp_block_kernel(case, S, layout):
         assert ph.engine.layout == layout and ph.engine.workgroups_per_scenario > 1
 
 
+def test_netdes_delta_values(monkeypatch):
+    """SURVEY 8(b) value forms on netdes (only the vubs' u_e vary, examples/netdes/netdes.py:39-80):
+    the per-scenario [S*nnz] form and the sparse delta list load the same device data (same bits),
+    with ONE scaling for all scenarios so the kernel streams per scenario only the piece-entry rows
+    holding a u_e; PHG_DELTA=0 (per-scenario scaling and copies) reaches the same prox-QP solutions
+    (1e-6) with a different preconditioner.  Both against the oracle's certified QPs (1e-5 / 1e-6)."""
+    S = 40
+    kw = {"num_scens": S}
+    o = oph.OraclePH(_opts(), om.netdes_names(S)[:4], om.netdes, kw)
+    o.Iter0()
+    o.Compute_Xbar()
+    o.Update_W()
+    res = {}
+    for tag, form, env in (("dense", 0, "1"), ("delta", 2, "1"), ("off", 0, "0")):
+        monkeypatch.setenv("PHG_DELTA", env)
+        ph = PH(_opts(pdhg_vals_form=form), netdes.scenario_names_creator(S), netdes.scenario_creator,
+                scenario_creator_kwargs=kw)
+        ph.PH_Prep()
+        assert ph.engine.layout == "block"
+        vi = ph.engine.values_info()
+        assert vi["varying"] == 1470, vi
+        if env == "1":
+            # two entry rows of 1024 per product: the x_e column pieces and the vub row pieces
+            assert vi["delta"] and 0 < vi["per_scenario_vals"] <= 4 * 1024 and vi["shared_vals"] > 0, vi
+        else:
+            assert not vi["delta"] and vi["per_scenario_vals"] >= 2 * 5880, vi
+        ph.Iter0()
+        ob0 = ph.engine.get(_lib.F_OBJ).copy()
+        W = np.zeros((S, ph.engine.N))
+        W[:4] = o.W
+        ph.engine.set(_lib.F_W, W.ravel())
+        ph.engine.set(_lib.F_XBAR, o.xbar[0])
+        ph.solve_loop()
+        assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+        res[tag] = (ob0, ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get_i32(_lib.I_ITERS).copy(), ph.nonants())
+    for a, b in zip(res["dense"], res["delta"]):
+        np.testing.assert_array_equal(a, b)
+    a, b = res["dense"], res["off"]
+    np.testing.assert_allclose(a[0], b[0], rtol=1e-6)
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-6)
+    np.testing.assert_allclose(a[3], b[3], atol=1e-5)
+    # the first 4 scenarios' prox-QPs against the oracle
+    o.solve_loop()
+    xo = np.array([o.nonants(k) for k in range(4)])
+    np.testing.assert_allclose(res["delta"][3][:4], xo, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(xo).max()))
+    np.testing.assert_allclose(res["delta"][1][:4], o.obj, rtol=1e-6)
+
+
 def test_border_matches_block_kernel():
     """The bordered block-diagonal kernel (pdhg_border.hip: 16 workgroups per scenario, one block
     per unit, the 24-nonzero demand / reserve rows as linking rows) runs the same arithmetic as the

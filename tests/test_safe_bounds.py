@@ -71,3 +71,32 @@ def test_farmer_free_columns_are_purchases():
     sold = [j for j, nm in enumerate(names) if nm.startswith("QuantitySuperQuotaSold")]
     assert np.isfinite(hi[:, sold]).all()
     assert (hi[:, sold] <= 30.0 * 500 * 10).all()   # yields < 30 t/acre, 5 000 acres
+
+
+@pytest.mark.parametrize("case", ["netdes", "sslp"])
+def test_value_forms_expand_identically(case):
+    """phg_batch.vals_form: the shared [nnz] form (sslp: only the right-hand sides
+    vary) and the sparse delta list (netdes: only the vubs' u_e vary) reach the host-side entry
+    points as the same per-scenario matrices -- phg_implied_bounds returns the same bits as for the
+    [S*nnz] form; a malformed delta list is rejected."""
+    from mpisppy_amd import _lib
+    b = CASES[case]()
+    ref = implied_bounds(b)
+    forms = [_lib.VALS_DELTA] + ([_lib.VALS_SHARED] if (b.vals == b.vals[0]).all() else [])
+    if case == "netdes":
+        assert 0 < int((b.vals != b.vals[0]).any(axis=0).sum()) <= 1470   # the vubs' u_e only
+    for form in forms:
+        b.vals_form = form
+        got = implied_bounds(b)
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]) and got[2] == ref[2]
+    b.vals_form = _lib.VALS_DELTA
+    cs, keep = b.c_struct()
+    if cs.n_delta >= 2:
+        pos = np.array([cs.delta_pos[1], cs.delta_pos[0]], np.int32)   # not increasing
+        keep.append(pos)
+        cs.n_delta, cs.delta_pos = 2, _lib.ptr(pos)
+        lo = np.empty(b.S * b.n)
+        hi = np.empty(b.S * b.n)
+        assert _lib.load().phg_implied_bounds(__import__("ctypes").byref(cs), _lib.ptr(lo), _lib.ptr(hi), None) != 0
+        assert b"strictly increasing" in _lib.load().phg_last_error()
+    b.vals_form = _lib.VALS_PER_SCENARIO
