@@ -1882,8 +1882,10 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
     if (dalloc(h, &h->Z, (size_t)S * N)) return -1;
     if (dalloc(h, &h->Psm, (size_t)S * N)) return -1;
     if (dalloc(h, &h->beta, (size_t)S * N)) return -1;
-    if (dalloc(h, &h->xbar, std::max(1, b->N_tot))) return -1;
-    if (dalloc(h, &h->xsqbar, std::max(1, b->N_tot))) return -1;
+    // xbar and xsqbar adjacent: [xbar | xsqbar] has the node-sum buffer's layout, so the W update of a
+    // pending folded update (flush_fold) reads them as its node sums
+    if (dalloc(h, &h->xbar, 2 * (size_t)std::max(1, b->N_tot))) return -1;
+    h->xsqbar = h->xbar + std::max(1, b->N_tot);
     if (dalloc(h, &h->xs, (size_t)S * n)) return -1;
     if (dalloc(h, &h->ys, (size_t)S * m)) return -1;
     if (dalloc(h, &h->omega, S)) return -1;

@@ -93,7 +93,7 @@ def test_netdes_delta_values(monkeypatch):
     (1e-6) with a different preconditioner.  Both against the oracle's certified QPs (1e-5 / 1e-6)."""
     S = 40
     kw = {"num_scens": S}
-    o = oph.OraclePH(_opts(), om.netdes_names(S)[:4], om.netdes, kw)
+    o = oph.OraclePH(_opts(), om.netdes_names(S)[:4], om.netdes, {"num_scens": 4})
     o.Iter0()
     o.Compute_Xbar()
     o.Update_W()
@@ -133,13 +133,16 @@ def test_netdes_delta_values(monkeypatch):
     np.testing.assert_allclose(res["delta"][1][:4], o.obj, rtol=1e-6)
 
 
-def test_border_matches_block_kernel():
+def test_border_matches_block_kernel(monkeypatch):
     """The bordered block-diagonal kernel (pdhg_border.hip: 16 workgroups per scenario, one block
     per unit, the 24-nonzero demand / reserve rows as linking rows) runs the same arithmetic as the
     workgroup-per-scenario block kernel in a different order: on a 24-unit x 12-period UC LP and
     one prox-QP at the oracle's W / x-bar, both reach the same iteration counts and objectives (to
     rounding), and the objectives match HiGHS at 1e-6.  (This LP is hard for PDHG: one scenario
-    stops at the 2e5-iteration cap with a 1e-9-level KKT error, in both kernels.)"""
+    stops at the 2e5-iteration cap with a 1e-9-level KKT error, in both kernels.)  Both with the
+    per-scenario scaling the bordered kernel uses (PHG_DELTA=0: the derates vary a few entries, which
+    would otherwise put the block kernel on the shared-scaling delta form)."""
+    monkeypatch.setenv("PHG_DELTA", "0")
     kw = {"num_gens": 24, "num_periods": 12, "num_scens": 3}
     o = oph.OraclePH(_opts(), om.uc_names(3), om.uc, kw)
     o.Iter0()
