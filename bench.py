@@ -56,7 +56,7 @@ def parse():
                          "case, i.e. farmer 10k = the BASELINE headline, sharded over the N GPUs: strong "
                          "scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0: skip)")
-    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local", "block", "mfma", "stream", "border"],
+    ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local", "block", "mfma", "stream", "border", "wave"],
                     help="PDHG data layout (include/phg.h: phg_set_layout)")
     ap.add_argument("--no-schedule", action="store_true", help="launch scenarios in index order")
     ap.add_argument("--check-every", type=int, default=32, help="PDHG restart/termination check interval")
@@ -341,7 +341,7 @@ def main():
     # the block kernel on a SHARED matrix (sslp) holds its pieces in registers and x / y in LDS: no
     # per-iteration HBM stream exists to price against the HBM roofline, so it is reported like the
     # register-resident kernels (fp64 flops against the fp64 peak), with the PMC-measured HBM rate beside
-    valu = eng.layout in ("local", "gather") or (eng.layout == "block" and nnz_distinct == 0)
+    valu = eng.layout in ("local", "gather", "wave") or (eng.layout == "block" and nnz_distinct == 0)
     # shared-matrix MFMA layout: SURVEY 8(d)2 F = 4 m n flops per scenario per PDHG iteration (A x and
     # A^T y as dense GEMM) and the flops the matrix cores actually execute (16 x 16 x 4 fragments:
     # 2048 flops per 16 scenarios each, the all-zero ones skipped)
@@ -408,6 +408,8 @@ def main():
                                           "x / y in LDS)" if nnz_distinct == 0 else
                                           "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)"),
                                 "mfma": "pdhg_mfma_kernel (shared matrix, v_mfma_f64_16x16x4_f64, 16 scenarios per wave)",
+                                "wave": "pdhg_wave_kernel (one wave per scenario, shared matrix once per workgroup in "
+                                        "LDS, no workgroup barrier in the iteration)",
                                 "stream": f"pdhg_stream_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
                                           "range split, iterates and values streamed)",
                                 "border": (f"pdhg_border_reg_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "

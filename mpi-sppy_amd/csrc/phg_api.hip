@@ -43,6 +43,10 @@ hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream);
 size_t pdhg_border_lds_bytes(const BorderLayout& B);
 int pdhg_border_max_per_thread();
 size_t pdhg_border_granule_words(const BorderLayout& B, const StreamLayout& L);
+int pdhg_wave_num_variants();
+void pdhg_wave_variant_shape(int v, int* out6);
+size_t pdhg_wave_lds_bytes(int v, int wave_doubles);
+hipError_t pdhg_wave_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_mfma_num_variants();
 void pdhg_mfma_variant_shape(int v, int* out2);
 hipError_t pdhg_mfma_launch(int v, const PdhgArgs& a, hipStream_t stream);
@@ -103,6 +107,10 @@ struct phg_handle {
     int variant = -1;          // gather kernel variant (pdhg.hip), or
     int local_variant = -1;    // lane-local kernel variant (pdhg_local.hip); preferred when >= 0
     int block_variant = -1;    // workgroup-per-scenario kernel variant (pdhg_block.hip)
+    int wave_variant = -1;     // one-wave-per-scenario shared-matrix kernel variant (pdhg_wave.hip)
+    int wshape[6] = {0};
+    WaveLayout wv{};
+    std::vector<int> wave_rperm, wave_cperm;   // piece / column-entry layout -> CSR position
     int mfma_variant = -1;     // shared-matrix MFMA kernel variant (pdhg_mfma.hip)
     bool stream_layout = false;   // multi-workgroup streaming kernel (pdhg_stream.hip)
     bool border_layout = false;   //   ... its bordered block-diagonal form (pdhg_border.hip)
@@ -1033,6 +1041,102 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     return 0;
 }
 
+// One-wave-per-scenario layout (pdhg_wave.hip) for a matrix shared by every scenario: column order =
+// the nonants first (their slots carry the prox diagonal), then the rest; every column's <= CE
+// entries; rows and 8-entry row pieces dealt over the lanes.  Returns 0 (built), 1 (does not fit:
+// the caller tries the workgroup layout), -1 (error).  PHG_WAVE=0: never (A/B runs).
+static int build_wave_layout(phg_handle* h, const phg_batch* b, const std::vector<int>& colptr,
+                             const std::vector<int>& csc_row, const std::vector<int>& csc_p) {
+    const char* ew = std::getenv("PHG_WAVE");
+    if ((ew && std::atoi(ew) == 0) || !h->vals_shared) return 1;
+    const int n = b->n, m = b->m, N = b->N;
+    int cmax = 0;
+    for (int j = 0; j < n; ++j) cmax = std::max(cmax, colptr[j + 1] - colptr[j]);
+    std::vector<int> rps, rpl, rpf(m), rpc(m);
+    for (int i = 0; i < m; ++i) {
+        rpf[i] = (int)rps.size();
+        for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; p += 8) {
+            rps.push_back(p);
+            rpl.push_back(std::min(8, b->rowptr[i + 1] - p));
+        }
+        rpc[i] = (int)rps.size() - rpf[i];
+    }
+    int sh[6], chosen = -1;
+    for (int v = 0; v < pdhg_wave_num_variants(); ++v) {
+        pdhg_wave_variant_shape(v, sh);
+        const int CPL = sh[0], RPL = sh[1], PPT = sh[2], CE = sh[3], NSL = sh[4];
+        if (n > CPL * 64 || m > RPL * 64 || (int)rps.size() > PPT * 64 || cmax > CE || N > NSL * 64) continue;
+        chosen = v;
+        break;
+    }
+    if (chosen < 0) return 1;
+    pdhg_wave_variant_shape(chosen, sh);
+    const int CPL = sh[0], RPL = sh[1], PPT = sh[2], CE = sh[3];
+    WaveLayout& L = h->wv;
+    L.n_pad = CPL * 64;       // x by column position (empty positions stay 0)
+    L.m_pad = (m + 1) & ~1;
+    L.wave_doubles = L.n_pad + L.m_pad + PPT * 64;
+    if (pdhg_wave_lds_bytes(chosen, L.wave_doubles) > 160 * 1024) return 1;
+    h->wave_variant = chosen;
+    std::memcpy(h->wshape, sh, sizeof sh);
+    // column order: nonants first
+    std::vector<int> order;
+    std::vector<char> isn(n, 0);
+    for (int k = 0; k < N; ++k) { order.push_back(b->nonant_col[k]); isn[b->nonant_col[k]] = 1; }
+    for (int j = 0; j < n; ++j) if (!isn[j]) order.push_back(j);
+    std::vector<int> col_of(CPL * 64, -1), cidx((size_t)CPL * 64 * CE, 0), pos(n, 0);
+    h->wave_cperm.assign((size_t)CPL * 64 * CE, -1);
+    for (int p = 0; p < n; ++p) {
+        const int j = order[p], slot = p / 64, ln = p % 64;
+        col_of[slot * 64 + ln] = j;
+        pos[j] = p;
+        for (int e = 0; e < colptr[j + 1] - colptr[j]; ++e) {
+            const size_t q = ((size_t)slot * 64 + ln) * CE + e;
+            cidx[q] = csc_row[colptr[j] + e];
+            h->wave_cperm[q] = csc_p[colptr[j] + e];
+        }
+    }
+    std::vector<int> row_of(RPL * 64, -1), rowf(RPL * 64, 0), rowc(RPL * 64, 0);
+    for (int i = 0; i < m; ++i) { row_of[i] = i; rowf[i] = rpf[i]; rowc[i] = rpc[i]; }
+    std::vector<int> ridx((size_t)PPT * 8 * 64, 0);
+    h->wave_rperm.assign((size_t)PPT * 8 * 64, -1);
+    for (size_t p = 0; p < rps.size(); ++p) {
+        const int slot = (int)p / 64, ln = (int)p % 64;
+        for (int e = 0; e < rpl[p]; ++e) {
+            const size_t q = ((size_t)slot * 8 + e) * 64 + ln;
+            ridx[q] = pos[b->colidx[rps[p] + e]];
+            h->wave_rperm[q] = rps[p] + e;
+        }
+    }
+    int* ip;
+    if (dput(h, &ip, col_of.data(), col_of.size())) return -1; L.col_of = ip;
+    if (dput(h, &ip, cidx.data(), cidx.size())) return -1; L.cidx = ip;
+    if (dput(h, &ip, row_of.data(), row_of.size())) return -1; L.row_of = ip;
+    if (dput(h, &ip, rowf.data(), rowf.size())) return -1; L.row_pfirst = ip;
+    if (dput(h, &ip, rowc.data(), rowc.size())) return -1; L.row_pcnt = ip;
+    if (dput(h, &ip, ridx.data(), ridx.size())) return -1; L.ridx = ip;
+    return 0;
+}
+
+// the wave layout's value copies (scenario 0's scaled matrix = every scenario's)
+static int build_wave_values(phg_handle* h) {
+    WaveLayout& L = h->wv;
+    int* rperm;
+    int* cperm;
+    double* rv;
+    double* cv;
+    const int Er = (int)h->wave_rperm.size(), Ec = (int)h->wave_cperm.size();
+    if (dput(h, &rperm, h->wave_rperm.data(), Er)) return -1;
+    if (dput(h, &cperm, h->wave_cperm.data(), Ec)) return -1;
+    if (dalloc(h, &rv, Er)) return -1;
+    if (dalloc(h, &cv, Ec)) return -1;
+    CK(piece_gather_launch(h->vals, h->nnz, rperm, Er, 1, rv, h->stream));
+    CK(piece_gather_launch(h->vals, h->nnz, cperm, Ec, 1, cv, h->stream));
+    L.rvals = rv;
+    L.cvals = cv;
+    return 0;
+}
+
 // piece-major copies of the (preconditioned) values; one copy when every scenario has the same A
 static int build_block_values(phg_handle* h) {
     BlockLayout& L = h->blk;
@@ -1845,7 +1949,16 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
         gr = build_layout(h, b, colptr, csc_row, csc_p);
         if (gr < 0 || (gr > 0 && pol == PHG_LAYOUT_GATHER)) return -1;
     }
-    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && pol != PHG_LAYOUT_STREAM && pol != PHG_LAYOUT_BORDER) {
+    int wr = 1;
+    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_WAVE)) {
+        wr = build_wave_layout(h, b, colptr, csc_row, csc_p);
+        if (wr < 0) return -1;
+        if (wr > 0 && pol == PHG_LAYOUT_WAVE)
+            return fail("phg_load_batch: the wave layout needs one matrix shared by all scenarios, <= 2 entries "
+                        "per column and n <= 1024, m <= 64");
+        if (wr == 0) h->variant = -1;
+    }
+    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && wr != 0 && pol != PHG_LAYOUT_STREAM && pol != PHG_LAYOUT_BORDER) {
         br = build_block_layout(h, b, colptr, csc_row, csc_p);
         if (br < 0 || (br > 0 && pol == PHG_LAYOUT_BLOCK)) return -1;
         h->variant = -1;
@@ -1855,7 +1968,7 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
         const bool delta_off = ed && std::atoi(ed) == 0;
         h->delta_scale = br == 0 && !delta_off && h->n_vary > 0 && 2L * h->n_vary <= (long)b->nnz;
     }
-    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && br != 0) {
+    if (h->mfma_variant < 0 && lr != 0 && gr != 0 && wr != 0 && br != 0) {
         if (build_stream_layout(h, b, colptr, csc_row, csc_p, pol)) return -1;
         h->variant = -1;
     }
@@ -1967,6 +2080,7 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
         if (dput(h, &ip, fc.data(), std::max<size_t>(1, fc.size()))) return -1; sb.free_col = ip;
     }
     if (h->block_variant >= 0 && build_block_values(h)) return -1;
+    if (h->wave_variant >= 0 && build_wave_values(h)) return -1;
     if (h->mfma_variant >= 0 && build_mfma_fragments(h, b)) return -1;
     if (h->stream_layout && build_stream_values(h)) return -1;
     CK(hipStreamSynchronize(h->stream));
@@ -2005,6 +2119,7 @@ int phg_info(phg_handle* h, int32_t* o) {
     else if (h->mfma_variant >= 0) { o[6] = 300 + h->mfma_variant; o[7] = 4; }
     else if (h->local_variant >= 0) { o[6] = 100 + h->local_variant; o[7] = h->lshape[0]; }
     else if (h->block_variant >= 0) { o[6] = 200 + h->block_variant; o[7] = h->bshape[0]; }
+    else if (h->wave_variant >= 0) { o[6] = 700 + h->wave_variant; o[7] = 64; }
     else { o[6] = h->variant; o[7] = 64; }
     return 0;
 }
@@ -2134,6 +2249,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     if (timing_event(h, 0, 0)) return -1;
     a.loc = h->loc;
     a.blk = h->blk;
+    a.wv = h->wv;
     a.mf = h->mf;
     a.st = h->st;
     a.gate = o->skip_if_conv_below > 0 ? h->gate : nullptr;
@@ -2161,6 +2277,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     else if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
     else if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
+    else if (h->wave_variant >= 0) CK(pdhg_wave_launch(h->wave_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
     if (timing_event(h, 0, 1)) return -1;
     h->xn_external = false;

@@ -67,6 +67,23 @@ struct BlockLayout {
     long dstride_r, dstride_c;
 };
 
+// One-wave-per-scenario shared-matrix layout (pdhg_wave.hip): column at position p of the column
+// order (nonants first) -> (slot p / 64, lane p % 64); its <= CE CSC entries; row i -> (slot i / 64,
+// lane i % 64); row pieces of <= 8 consecutive CSR entries, piece p -> (slot p / 64, lane p % 64).
+// The scaled values (the same in every scenario) are copied into each workgroup's LDS.
+struct WaveLayout {
+    int n_pad, m_pad;       // per-wave LDS: x [n_pad = CPL*64] by column position, y [m_pad]
+    int wave_doubles;       // n_pad + m_pad + PPT * 64
+    const int* col_of;      // [CPL*64]
+    const int* cidx;        // [CPL*64*CE] row of each column entry (0 on padding, value 0)
+    const int* row_of;      // [RPL*64]
+    const int* row_pfirst;  // [RPL*64]
+    const int* row_pcnt;    // [RPL*64]
+    const int* ridx;        // [PPT*8*64] column POSITION of each row-piece entry (0 on padding, value 0)
+    const double* rvals;    // [PPT][8][64] scaled values
+    const double* cvals;    // [CPL][64][CE]
+};
+
 // Shared-matrix MFMA layout (pdhg_mfma.hip): the A operands of v_mfma_f64_16x16x4_f64 for A x
 // (fragment (t, u, j): lane l holds A_hat[16 t + (l & 15)][16 u + 4 j + (l >> 4)]) and for A^T y
 // (fragment (u, t, j): lane l holds A_hat[16 t + 4 j + (l >> 4)][16 u + (l & 15)]), [fragment][64],
@@ -136,6 +153,7 @@ struct PdhgArgs {
     Layout lay;
     LocalLayout loc;
     BlockLayout blk;
+    WaveLayout wv;
     MfmaLayout mf;
     StreamLayout st;
     BorderLayout bd;

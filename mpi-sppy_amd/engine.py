@@ -159,7 +159,7 @@ def implied_bounds(batch):
 class Engine:
     """One libphg handle on one GPU (no CPU fallback: raises if the library or device is missing)."""
 
-    LAYOUTS = {"auto": 0, "gather": 1, "local": 2, "block": 3, "mfma": 4, "stream": 5, "border": 6}
+    LAYOUTS = {"auto": 0, "gather": 1, "local": 2, "block": 3, "mfma": 4, "stream": 5, "border": 6, "wave": 7}
 
     def __init__(self, batch, device=0, stream=None, exchange=None, layout="auto", presolve=True):
         self.lib = _lib.load()
@@ -188,13 +188,13 @@ class Engine:
         _lib.check(self.lib.phg_info(self.h, ptr(info)))
         self.variant = int(info[6])
         self.lanes_per_scenario = int(info[7])
-        self.layout = ("border" if self.variant >= 500 else "stream" if self.variant >= 400 else
+        self.layout = ("wave" if self.variant >= 700 else "border" if self.variant >= 500 else "stream" if self.variant >= 400 else
                        "mfma" if self.variant >= 300 else "block" if self.variant >= 200 else
                        "local" if self.variant >= 100 else "gather")
         # multi-workgroup layouts (range-split stream 400 + K, bordered 500 + K): workgroups per scenario
-        self.workgroups_per_scenario = self.variant % 100 if self.variant >= 400 else 1
+        self.workgroups_per_scenario = self.variant % 100 if 400 <= self.variant < 700 else 1
         # bordered layout: 600 + K the register-resident kernel, 500 + K the memory-resident one
-        self.border_reg = self.variant >= 600
+        self.border_reg = 600 <= self.variant < 700
         pi = np.zeros(2, np.int32)
         _lib.check(self.lib.phg_presolve_info(self.h, ptr(pi)))
         self.rows_folded, self.rows_kept = int(pi[0]), int(pi[1])

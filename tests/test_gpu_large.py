@@ -47,7 +47,7 @@ def test_iter0_lp_block_kernel(case, S):
     pn, pc, pkw, on, oc, okw = CASES[case]
     ph = PH(_opts(), pn(S), pc, scenario_creator_kwargs=pkw)
     ph.PH_Prep()
-    assert ph.engine.layout == "block"
+    assert ph.engine.layout == ("wave" if case == "sslp" else "block")   # sslp: one matrix for all scenarios
     tb = ph.Iter0()
     o = oph.OraclePH(_opts(), on(S), oc, okw)
     otb = o.Iter0()
@@ -57,8 +57,8 @@ def test_iter0_lp_block_kernel(case, S):
     assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
 
 
-@pytest.mark.parametrize("case,S,layout", [("sslp", 4, "auto"), ("netdes", 3, "auto"), ("sslp", 4, "stream"),
-                                           ("uc_small", 4, "stream")])
+@pytest.mark.parametrize("case,S,layout", [("sslp", 4, "auto"), ("sslp", 4, "block"), ("netdes", 3, "auto"),
+                                           ("sslp", 4, "stream"), ("uc_small", 4, "stream")])
 def test_prox_qp_block_kernel(case, S, layout):
     """layout "stream": the range-split multi-workgroup kernel (pdhg_stream.hip) with K > 1
     workgroups per scenario (few scenarios: K = 16), its cross-workgroup barriers and sums;
@@ -206,7 +206,8 @@ def test_uc_fullsize_stream_vs_oracle(S, layout):
 
 
 def test_block_register_pieces_same_bits(monkeypatch):
-    """sslp's pieces fit the registers (row pieces <= 8, columns in <= 2 rows), so AUTO runs the
+    """sslp's pieces fit the registers (row pieces <= 8, columns in <= 2 rows), so the block layout
+    (AUTO takes the wave layout for sslp: test_wave_kernel_matches_block_kernel) runs the
     block kernel with the matrix held in registers for the whole solve; PHG_BLOCK_STREAM=1 forces
     the form that re-reads values / indices every iteration.  Same products in the same order:
     Iter0 and one prox-QP solve give bit-identical objectives, iteration counts and nonants."""
@@ -218,7 +219,7 @@ def test_block_register_pieces_same_bits(monkeypatch):
     res = []
     for stream in ("0", "1"):
         monkeypatch.setenv("PHG_BLOCK_STREAM", stream)
-        ph = PH(_opts(), sslp.scenario_names_creator(S), sslp.scenario_creator)
+        ph = PH(_opts(pdhg_layout="block"), sslp.scenario_names_creator(S), sslp.scenario_creator)
         ph.PH_Prep()
         assert ph.engine.layout == "block"
         ph.Iter0()
@@ -229,3 +230,72 @@ def test_block_register_pieces_same_bits(monkeypatch):
         res.append((ob0, ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get_i32(_lib.I_ITERS).copy(), ph.nonants()))
     for a, b in zip(*res):
         np.testing.assert_array_equal(a, b)
+
+
+def test_uc_fullsize_lagrangian_lp_vs_oracle():
+    """The Lagrangian spoke's subproblem at full UC size (W on, prox off: lagrangian_bounder.py:21-44
+    with the W of the first PH update, phbase.py:301-326) through the bordered kernel, against HiGHS'
+    LP with the same W on two sampled scenarios: objectives at 1e-5 relative (pdhg_eps 1e-6, as the
+    UC runs), and each scenario's safe bound (phg_opts.safe_bound: a weak-duality certificate of the
+    dual iterate) at or below the LP optimum and within 1e-5 of it."""
+    S = 4
+    so = {"pdhg_eps": 1e-6}
+    ph = PH(_opts(iter0_solver_options=so, iterk_solver_options=so), uc.scenario_names_creator(S),
+            uc.scenario_creator, scenario_creator_kwargs={"num_scens": S})
+    ph.PH_Prep()
+    assert ph.engine.layout == "border" and ph.engine.workgroups_per_scenario > 1
+    ph.Iter0()
+    ph.Compute_Xbar()
+    ph.Update_W()
+    W = ph.engine.get(_lib.F_W).reshape(S, ph.engine.N)
+    assert np.abs(W).max() > 0
+    ph.engine.solve(1, 0, eps=1e-6, max_iter=200000, warm_start=3, safe_bound=True)
+    ph.engine.sync()
+    obj, bnd = ph.engine.get(_lib.F_OBJ), ph.engine.get(_lib.F_BOUND)
+    st = ph.engine.get_i32(_lib.I_STATUS)
+    pick = [0, S - 1]
+    o = oph.OraclePH(_opts(), [om.uc_names(S)[k] for k in pick], om.uc, {"num_scens": len(pick)})
+    o.W = W[pick].copy()
+    o.W_on, o.prox_on = 1, 0
+    o.solve_loop()
+    for i, k in enumerate(pick):
+        ref = o.obj[i]
+        assert st[k] == 0, (k, st[k])
+        assert abs(obj[k] - ref) <= 1e-5 * abs(ref), (k, obj[k], ref)
+        assert bnd[k] <= ref + 1e-9 * abs(ref) and ref - bnd[k] <= 1e-5 * abs(ref), (k, bnd[k], ref)
+
+
+def test_wave_kernel_matches_block_kernel():
+    """sslp (one matrix for every scenario, columns in <= 2 rows): AUTO runs pdhg_wave.hip -- one
+    wavefront per scenario, the matrix once per workgroup in LDS, no workgroup barrier in the loop --
+    which adds the same pieces in the same order as the workgroup kernel but reduces its KKT norms
+    over a wave instead of a workgroup.  Iter0 and two prox-QP solves at the oracle's W / x-bar, both
+    layouts: objectives and bounds agree to 1e-9 relative, nonants to 1e-7, every solve at status 0;
+    and the prox-QP nonants against the oracle at 1e-5 (test_prox_qp_block_kernel[sslp-4-auto])."""
+    S = 16
+    o = oph.OraclePH(_opts(), om.sslp_names(S), om.sslp, {})
+    o.Iter0()
+    o.Compute_Xbar()
+    o.Update_W()
+    res = {}
+    for layout in ("wave", "block"):
+        ph = PH(_opts(pdhg_layout=layout), sslp.scenario_names_creator(S), sslp.scenario_creator)
+        ph.PH_Prep()
+        assert ph.engine.layout == layout
+        ph.Iter0()
+        r = [ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get(_lib.F_BOUND).copy()]
+        assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+        for it in range(2):
+            ph.engine.set(_lib.F_W, o.W.ravel() * (it + 1))
+            ph.engine.set(_lib.F_XBAR, o.xbar[0])
+            ph.solve_loop()
+            assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+            r += [ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get(_lib.F_BOUND).copy(), ph.nonants().copy(),
+                  ph.engine.get_i32(_lib.I_ITERS).copy()]
+        res[layout] = r
+    a, b = res["wave"], res["block"]
+    for u in (0, 1, 2, 3, 6, 7):
+        np.testing.assert_allclose(a[u], b[u], rtol=1e-9, atol=1e-9)
+    for u in (4, 8):
+        np.testing.assert_allclose(a[u], b[u], atol=1e-7)
+    print("PDHG iterations wave / block:", a[5].sum() + a[9].sum(), b[5].sum() + b[9].sum())

@@ -18,3 +18,11 @@ timeout -k 10 400 python3 -u bench.py --traffic-json $O/netdes_traffic.json --co
 python3 -c "import json; d=json.load(open('$O/netdes.json')); r=d['roofline']; print('delta', d['value'], d['ms_per_step'], r['avg_launch_ms'], r['pdhg_iters_per_scen_per_step'], r.get('hbm_measured_GBs'), d['config']['values'], d.get('time_to_conv', {}).get('conv'), d.get('time_to_conv', {}).get('ph_iters'))"
 PHG_DELTA=0 timeout -k 10 400 python3 -u bench.py --conv-time 60 --cpu-seconds 0 --case netdes --scen 1024 > $O/netdes_off.json 2> $O/netdes_off.err || exit 1
 python3 -c "import json; d=json.load(open('$O/netdes_off.json')); r=d['roofline']; print('off', d['value'], d['ms_per_step'], r['avg_launch_ms'], r['pdhg_iters_per_scen_per_step'], d['config']['values'], d.get('time_to_conv', {}).get('conv'), d.get('time_to_conv', {}).get('ph_iters'))"
+# the one-wave-per-scenario shared-matrix kernel (sslp): parity tests, then sslp 4096 wave vs block
+timeout -k 10 600 python -u -m pytest tests/test_gpu_large.py tests/test_gpu_fullsize.py -k "sslp or wave" -v --timeout 300 --timeout-method thread -m gpu > $O/tests_wave.log 2>&1
+rc=$?; echo "pytest wave exit $rc"; grep -E "PASSED|FAILED|ERROR|passed|failed|wave / block" $O/tests_wave.log | tail -20
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+for L in wave block; do
+  timeout -k 10 300 python3 -u bench.py --conv-iters 0 --cpu-seconds 0 --case sslp --scen 4096 --layout $L > $O/sslp_$L.json 2> $O/sslp_$L.err || { tail -5 $O/sslp_$L.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/sslp_$L.json')); r=d['roofline']; print('$L', d['value'], d['ms_per_step'], r['avg_launch_ms'], r['pdhg_iters_per_scen_per_step'], r['frac'], d['config']['pdhg_layout'])"
+done
