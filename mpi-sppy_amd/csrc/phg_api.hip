@@ -443,7 +443,7 @@ int phg_set_smoothing(phg_handle* h, int32_t on) {
 int phg_set_layout(phg_handle* h, int32_t policy) {
     if (!h) return fail("null handle");
     if (h->loaded) return fail("phg_set_layout: must be called before phg_load_batch");
-    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_BORDER) return fail("phg_set_layout: bad policy");
+    if (policy < PHG_LAYOUT_AUTO || policy > PHG_LAYOUT_WAVE) return fail("phg_set_layout: bad policy");
     h->layout_policy = policy;
     return 0;
 }
@@ -2054,16 +2054,18 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
     if (dalloc(h, &scratch, (size_t)S * (2 * n + 2 * m))) return -1;
     pa.vals = h->vals; pa.dc = h->dc; pa.dr = h->dr; pa.cl = h->cl; pa.cu = h->cu; pa.rl = h->rl;
     pa.ru = h->ru; pa.eta = h->eta; pa.bnorm = h->bnorm; pa.scratch = scratch;
-    pa.vmean = nullptr;
-    if (h->delta_scale) {   // Ruiz on the element-wise mean |a| over the scenarios (same dc, dr everywhere)
-        std::vector<double> vm((size_t)nnz, 0.0);
-        for (int s = 0; s < S; ++s)
-            for (int p = 0; p < nnz; ++p) vm[p] += std::fabs(b->vals[(size_t)s * nnz + p]);
-        for (int p = 0; p < nnz; ++p) vm[p] /= (double)S;
-        double* dp;
-        if (dput(h, &dp, vm.data(), vm.size())) return -1;
-        pa.vmean = dp;
-        if (dalloc(h, &pa.vm_scratch, (size_t)S * nnz)) return -1;
+    pa.vary = nullptr; pa.row_allvar = nullptr; pa.col_allvar = nullptr;
+    if (h->delta_scale) {   // norms over the constant entries (PrepArgs::vary): one scaling of them everywhere
+        std::vector<unsigned char> vy(nnz), ra(m, 1), ca(n, 1);
+        for (int i = 0; i < m; ++i)
+            for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) {
+                vy[p] = h->vary[p] ? 1 : 0;
+                if (!h->vary[p]) { ra[i] = 0; ca[b->colidx[p]] = 0; }
+            }
+        unsigned char* u8;
+        if (dput(h, &u8, vy.data(), vy.size())) return -1; pa.vary = u8;
+        if (dput(h, &u8, ra.data(), ra.size())) return -1; pa.row_allvar = u8;
+        if (dput(h, &u8, ca.data(), ca.size())) return -1; pa.col_allvar = u8;
     }
     CK(prep_launch(pa, h->stream));
     {   // safe bounds (bound.hip): pattern in CSR / CSC, implied column bounds, repair candidates

@@ -271,11 +271,15 @@ struct PrepArgs {
     double* eta;            // [S]
     double* bnorm;          // [S]
     double* scratch;        // [S*(2n+2m)]
-    // non-null: the Ruiz / Pock-Chambolle scalings are those of this [nnz] matrix (the element-wise
-    // mean |a| over the scenarios), the same in every scenario, applied to each scenario's values;
-    // vm_scratch [S*nnz] holds each workgroup's running copy of it
-    const double* vmean;
-    double* vm_scratch;
+    // delta form (phg_batch.vals_form): vary [nnz] marks the entries that differ between scenarios.
+    // A row (column) with at least one constant entry takes its Ruiz / Pock-Chambolle norm over its
+    // constant entries only -- the same in every scenario, so the constant entries keep one scaled
+    // value everywhere (one shared copy in the solver); a row (column) of varying entries only
+    // (row_allvar / col_allvar: netdes' x_e columns, whose one entry is -u_e) is equilibrated per
+    // scenario.  Null: every norm over the scenario's own row / column.
+    const unsigned char* vary;
+    const unsigned char* row_allvar;   // [m]
+    const unsigned char* col_allvar;   // [n]
 };
 
 struct NodeSeg {           // a contiguous scenario range inside one node (one level)

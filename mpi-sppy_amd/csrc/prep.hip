@@ -37,36 +37,32 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     double* pw = pv + n;       // [m]
     for (int j = tid; j < n; j += 256) dc[j] = 1.0;
     for (int i = tid; i < m; i += 256) dr[i] = 1.0;
-    // shared scaling (PrepArgs::vmean): the norms come from this workgroup's copy of the mean matrix,
-    // scaled alongside -- every workgroup computes the same dc, dr
-    double* vm = v;
-    if (a.vmean) {
-        vm = a.vm_scratch + (long)s * nnz;
-        for (int p = tid; p < nnz; p += 256) vm[p] = a.vmean[p];
-    }
     __syncthreads();
+    // delta form (PrepArgs::vary): a norm over the constant entries of the row / column unless it has
+    // none -- every workgroup computes the same factors for those rows and columns
+    auto counts = [&](int p, bool allvar) { return !a.vary || !a.vary[p] || allvar; };
     for (int pass = 0; pass <= a.ruiz_iters; ++pass) {
         const bool pock = (pass == a.ruiz_iters);
         for (int i = tid; i < m; i += 256) {
+            const bool av_ = a.row_allvar && a.row_allvar[i];
             double acc = 0.0;
             for (int p = a.rowptr[i]; p < a.rowptr[i + 1]; ++p)
-                acc = pock ? acc + fabs(vm[p]) : fmax(acc, fabs(vm[p]));
+                if (counts(p, av_)) acc = pock ? acc + fabs(v[p]) : fmax(acc, fabs(v[p]));
             rs[i] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
         }
         for (int j = tid; j < n; j += 256) {
+            const bool av_ = a.col_allvar && a.col_allvar[j];
             double acc = 0.0;
             for (int t = a.colptr[j]; t < a.colptr[j + 1]; ++t) {
-                const double av = fabs(vm[a.csc_p[t]]);
+                const int p = a.csc_p[t];
+                if (!counts(p, av_)) continue;
+                const double av = fabs(v[p]);
                 acc = pock ? acc + av : fmax(acc, av);
             }
             cs[j] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
         }
         __syncthreads();
-        for (int p = tid; p < nnz; p += 256) {
-            const double f = rs[a.row_of_p[p]] * cs[a.colidx[p]];
-            v[p] *= f;
-            if (vm != v) vm[p] *= f;
-        }
+        for (int p = tid; p < nnz; p += 256) v[p] *= rs[a.row_of_p[p]] * cs[a.colidx[p]];
         for (int j = tid; j < n; j += 256) dc[j] *= cs[j];
         for (int i = tid; i < m; i += 256) dr[i] *= rs[i];
         __syncthreads();

@@ -32,6 +32,12 @@ def main():
         ph.PH_Prep()
         ph.Iter0()
         print("fold active" if ph.engine.set_fold(fold) else "fold off", flush=True)
+        # the folded update takes x = xs dc (the scaled state times the column scaling); the two-launch
+        # update takes the epilogue's xN -- are they the same bits?
+        xN = ph.engine.get(_lib.F_XN).reshape(S, ph.engine.N)
+        xu = ph.engine.get(_lib.F_X).reshape(S, -1)[:, ph.engine.batch.nonant_col]
+        print("  xN vs xs*dc after Iter0: max |diff|", float(np.abs(xN - xu).max()),
+              "differing", int((xN != xu).sum()), "of", xN.size, flush=True)
         phs.append(ph)
     for k in range(1, iters + 1):
         for ph in phs:
