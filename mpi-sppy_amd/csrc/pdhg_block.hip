@@ -62,7 +62,11 @@ __device__ __forceinline__ double piece_sum(const double* p, int cnt) {
 // CL: every column is ONE piece, held by the thread and slot that own the column (QPT == CPL;
 // checked on the host) -- so A^T y needs no partials in LDS and no workgroup barrier: three
 // barriers per PDHG iteration instead of four (sslp: every column has <= 2 entries; netdes <= 3).
-template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL>
+//
+// VS: the delta value form (BlockLayout::vscale) -- the pieces hold unscaled values and the scenario's
+// scaling is applied on the fly: x and y enter the LDS as dc x and dr y, A x leaves as dr (A (dc x)),
+// A^T y as dc (A^T (dr y)).
+template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL, bool VS>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     static_assert(!CL || QPT == CPL, "column-local A^T y needs one piece slot per column slot");
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
@@ -96,6 +100,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     // restart reference points live in the xs / ys state arrays (each thread reads back only the
     // elements it wrote), not in registers
     double x[CPL], aty[CPL], c[CPL], q[CPL], lo[CPL], hi[CPL], ip[CPL], xsum[CPL];
+    double dcs[VS ? CPL : 1], drs[VS ? RPL : 1];   // VS: the scenario's column / row scaling
     double prox_const = 0.0, c2 = 0.0;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
@@ -104,9 +109,11 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         cf[k] = B.col_pfirst[k * NT + t];
         cn[k] = B.col_pcnt[k * NT + t];
         x[k] = aty[k] = c[k] = q[k] = lo[k] = hi[k] = xsum[k] = 0.0;
+        if constexpr (VS) dcs[k] = 0.0;
         if (j >= 0) {
             const long b = sn + j;
             const double d = a.dc[b];
+            if constexpr (VS) dcs[k] = d;
             double cc = a.c[b], qq = 0.0;
             double lo_ = a.cl[b], hi_ = a.cu[b];
             const int kk = a.lay.col_nonant[j];
@@ -135,8 +142,10 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         rf[r] = B.row_pfirst[r * NT + t];
         rn[r] = B.row_pcnt[r * NT + t];
         y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
+        if constexpr (VS) drs[r] = 0.0;
         if (i >= 0) {
             const long b = sm + i;
+            if constexpr (VS) drs[r] = a.dr[b];
             row_bounds(a, i, b, rlo[r], rhi[r]);
             double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
             if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
@@ -202,7 +211,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < RPL; ++r) out[r] = piece_sum(rp + rf[r], rn[r]);
+        for (int r = 0; r < RPL; ++r) out[r] = VS ? piece_sum(rp + rf[r], rn[r]) * drs[r] : piece_sum(rp + rf[r], rn[r]);
     };
     // A^T y for the y currently in yl
     auto spmv_aty = [&](double (&out)[CPL]) {
@@ -222,24 +231,24 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
                 }
                 off += kk * NT;
             }
-            if constexpr (CL) out[ps] = 0.0 + acc;   // (the same bits as a one-piece piece_sum)
+            if constexpr (CL) out[ps] = VS ? acc * dcs[ps] : 0.0 + acc;   // (the same bits as a one-piece piece_sum)
             else cp[ps * NT + t] = acc;
         }
         if constexpr (!CL) {
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < CPL; ++k) out[k] = piece_sum(cp + cf[k], cn[k]);
+            for (int k = 0; k < CPL; ++k) out[k] = VS ? piece_sum(cp + cf[k], cn[k]) * dcs[k] : piece_sum(cp + cf[k], cn[k]);
         }
     };
     auto put_x = [&](const double (&v)[CPL]) {
 #pragma unroll
         for (int k = 0; k < CPL; ++k)
-            if (cj[k] >= 0) xl[cj[k]] = v[k];
+            if (cj[k] >= 0) xl[cj[k]] = VS ? v[k] * dcs[k] : v[k];
     };
     auto put_y = [&](const double (&v)[RPL]) {
 #pragma unroll
         for (int r = 0; r < RPL; ++r)
-            if (ri[r] >= 0) yl[ri[r]] = v[r];
+            if (ri[r] >= 0) yl[ri[r]] = VS ? v[r] * drs[r] : v[r];
     };
     // products at the current point (x, y): ends with every partial consumed
     auto products = [&]() {
@@ -493,13 +502,16 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 
 // ----------------------------------------------------------------------------- dispatch
 struct BlockVariant {
-    int NT, CPL, RPL, PPT, QPT, RE, CE, CL;
+    int NT, CPL, RPL, PPT, QPT, RE, CE, CL, VS;
     void (*fn)(PdhgArgs);
 };
 
-#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false>}
-#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true>}
-#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_>}
+#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, false>}
+#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, false>}
+#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false>}
+// the delta value form (unscaled shared pieces, scaling on the fly)
+#define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
+#define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
     PHG_BR(256, 3, 1, 2, 3, 8, 2, true),    // sslp-like: register-resident pieces, column-local A^T y
@@ -510,17 +522,27 @@ static const BlockVariant kBlockVariants[] = {
     PHG_BC(1024, 3, 2, 3, 3),    // netdes-like with column-local A^T y (streamed values)
     PHG_B(1024, 3, 2, 3, 3),     // netdes-like: n <= 3072, m <= 2048
     PHG_B(1024, 4, 4, 4, 4),     // <= 4096
+    // delta value form
+    PHG_BV(256, 3, 1, 2, 3),
+    PHG_BV(256, 4, 4, 4, 4),
+    PHG_BV(512, 4, 4, 4, 4),
+    PHG_BCV(1024, 3, 2, 3, 3),   // netdes (only the vubs' u_e vary)
+    PHG_BV(1024, 3, 2, 3, 3),
+    PHG_BV(1024, 4, 4, 4, 4),
 };
 #undef PHG_B
 #undef PHG_BR
 #undef PHG_BC
+#undef PHG_BV
+#undef PHG_BCV
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
 
-void pdhg_block_variant_shape(int v, int* out8) {
+void pdhg_block_variant_shape(int v, int* out9) {
     const BlockVariant& V = kBlockVariants[v];
-    out8[0] = V.NT; out8[1] = V.CPL; out8[2] = V.RPL; out8[3] = V.PPT; out8[4] = V.QPT; out8[5] = V.RE; out8[6] = V.CE;
-    out8[7] = V.CL;
+    out9[0] = V.NT; out9[1] = V.CPL; out9[2] = V.RPL; out9[3] = V.PPT; out9[4] = V.QPT; out9[5] = V.RE; out9[6] = V.CE;
+    out9[7] = V.CL;
+    out9[8] = V.VS;
 }
 
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad) {

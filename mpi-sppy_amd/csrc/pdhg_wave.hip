@@ -36,19 +36,24 @@ __device__ __forceinline__ void wsync() {
 }
 
 template <int CPL, int RPL, int PPT, int CE, int NSL, int WPG>
-__global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
+__global__ __launch_bounds__(64 * WPG, 8 / WPG) void pdhg_wave_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     constexpr int RE = 8;
+    constexpr int RMAX = 8;   // pieces per row (<= 64 entries; checked on the host)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const WaveLayout& V = a.wv;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double* rvs = smem;                          // [PPT][RE][64] row-piece values (shared)
     double* cvs = rvs + PPT * RE * 64;           // [CPL][64][CE] column values (shared)
-    double* xl = cvs + CPL * 64 * CE + (long)w * V.wave_doubles;   // [CPL*64] x by column position
+    int* xis = reinterpret_cast<int*>(cvs + CPL * 64 * CE);   // [PPT][RE][64] row-piece x positions (shared)
+    int* cis = xis + PPT * RE * 64;              // [CPL][64][CE] column entry rows (shared)
+    double* xl = reinterpret_cast<double*>(cis + CPL * 64 * CE) + (long)w * V.wave_doubles;   // [CPL*64] x by position
     double* yl = xl + V.n_pad;                   // [m_pad]
     double* rp = yl + V.m_pad;                   // [PPT*64] row-piece partials
     for (int e = threadIdx.x; e < PPT * RE * 64; e += 64 * WPG) rvs[e] = V.rvals[e];
     for (int e = threadIdx.x; e < CPL * 64 * CE; e += 64 * WPG) cvs[e] = V.cvals[e];
+    for (int e = threadIdx.x; e < PPT * RE * 64; e += 64 * WPG) xis[e] = V.ridx[e];
+    for (int e = threadIdx.x; e < CPL * 64 * CE; e += 64 * WPG) cis[e] = V.cidx[e];
     __syncthreads();   // the only workgroup barrier: the waves are independent from here on
     const int item = blockIdx.x * WPG + w;
     if (item >= a.S) return;
@@ -56,15 +61,12 @@ __global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
     const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
 
     // ------------------------------------------------------------------ columns owned
-    int cid[CPL][CE];            // rows of the column's entries (the column itself sits at xl[k*64 + lane])
     double x[CPL], c[CPL], lo[CPL], hi[CPL], xsum[CPL];
     double q[NSL > 0 ? NSL : 1], ip[NSL > 0 ? NSL : 1];
     double prox_const = 0.0, c2 = 0.0;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int j = V.col_of[k * 64 + lane];
-#pragma unroll
-        for (int e = 0; e < CE; ++e) cid[k][e] = V.cidx[(k * 64 + lane) * CE + e];
         x[k] = c[k] = lo[k] = hi[k] = xsum[k] = 0.0;
         if (k < NSL) q[k] = 0.0;
         if (j >= 0) {
@@ -108,18 +110,13 @@ __global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
             a.ys[b] = yy;
         }
     }
-    // row pieces: positions (k*64 + lane) of the columns they multiply (padding: position 0, value 0)
-    int xid[PPT][RE];
-#pragma unroll
-    for (int ps = 0; ps < PPT; ++ps)
-#pragma unroll
-        for (int e = 0; e < RE; ++e) xid[ps][e] = V.ridx[(ps * RE + e) * 64 + lane];
 
     // ------------------------------------------------------------------ products through LDS
-    auto put_x = [&](const double (&v)[CPL]) {
+    auto put_x = [&](auto f) {
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) xl[k * 64 + lane] = v[k];   // (empty positions hold 0)
+        for (int k = 0; k < CPL; ++k) xl[k * 64 + lane] = f(k);   // (empty positions hold 0)
     };
+    auto cur_x = [&](int k) { return x[k]; };
     auto put_y = [&](const double (&v)[RPL]) {
 #pragma unroll
         for (int r = 0; r < RPL; ++r)
@@ -130,7 +127,7 @@ __global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
     auto aty_col = [&](int k) {
         double acc = 0.0;
 #pragma unroll
-        for (int e = 0; e < CE; ++e) acc = fma(cvs[(k * 64 + lane) * CE + e], yl[cid[k][e]], acc);
+        for (int e = 0; e < CE; ++e) acc = fma(cvs[(k * 64 + lane) * CE + e], yl[cis[(k * 64 + lane) * CE + e]], acc);
         return acc;
     };
     // A x for the x in xl: pieces -> rp, then row owners add their pieces left to right
@@ -139,15 +136,18 @@ __global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
         for (int ps = 0; ps < PPT; ++ps) {
             double acc = 0.0;
 #pragma unroll
-            for (int e = 0; e < RE; ++e) acc = fma(rvs[(ps * RE + e) * 64 + lane], xl[xid[ps][e]], acc);
+            for (int e = 0; e < RE; ++e) acc = fma(rvs[(ps * RE + e) * 64 + lane], xl[xis[(ps * RE + e) * 64 + lane]], acc);
             rp[ps * 64 + lane] = acc;
         }
         wsync();
 #pragma unroll
         for (int r = 0; r < RPL; ++r) {
+            double pv[RMAX];
+#pragma unroll
+            for (int u = 0; u < RMAX; ++u) pv[u] = u < rn[r] ? rp[rf[r] + u] : 0.0;
             double t = 0.0;
-#pragma unroll 1
-            for (int u = 0; u < rn[r]; ++u) t += rp[rf[r] + u];
+#pragma unroll
+            for (int u = 0; u < RMAX; ++u) t += pv[u];   // (+0.0 past the row's pieces: the same sum)
             out[r] = t;
         }
         wsync();   // partials consumed before the next pieces overwrite them
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
     double tau = eta / omega, sig = eta * omega;
 #pragma unroll
     for (int k = 0; k < NSL; ++k) ip[k] = 1.0 / (1.0 + tau * q[k]);
-    put_x(x);
+    put_x(cur_x);
     put_y(y);
     wsync();
     spmv_ax(ax);
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
                 x[k] = xn;
                 xsum[k] += xn;
             }
-            put_x(x);
+            put_x(cur_x);
             wsync();
             double axn[RPL];
             spmv_ax(axn);
@@ -276,12 +276,10 @@ __global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
         double oc[6], oa[6];
         kkt([&](int k) { return x[k]; }, y, ax, oc);
         {   // the average iterate (every check, as the workgroup kernel): its products through LDS
-            double xa[CPL], ya[RPL], axa[RPL];
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) xa[k] = xsum[k] * inv;
+            double ya[RPL], axa[RPL];
 #pragma unroll
             for (int r = 0; r < RPL; ++r) ya[r] = ysum[r] * inv;
-            put_x(xa);
+            put_x([&](int k) { return xsum[k] * inv; });
             put_y(ya);
             wsync();
             spmv_ax(axa);
@@ -353,7 +351,7 @@ __global__ __launch_bounds__(64 * WPG) void pdhg_wave_kernel(PdhgArgs a) {
         }
         // x, y back into LDS (the average's products used it); A x of the point the iteration
         // continues from: recomputed after a restart to the average, else still in ax
-        put_x(x);
+        put_x(cur_x);
         put_y(y);
         wsync();
         if (restart && use_avg) spmv_ax(ax);
@@ -417,7 +415,8 @@ void pdhg_wave_variant_shape(int v, int* out6) {
 
 size_t pdhg_wave_lds_bytes(int v, int wave_doubles) {
     const WaveVariant& V = kWaveVariants[v];
-    return ((size_t)V.PPT * 8 * 64 + (size_t)V.CPL * 64 * V.CE + (size_t)V.WPG * wave_doubles) * sizeof(double);
+    const size_t ent = (size_t)V.PPT * 8 * 64 + (size_t)V.CPL * 64 * V.CE;   // values (double) + indices (int)
+    return ent * (sizeof(double) + sizeof(int)) + (size_t)V.WPG * wave_doubles * sizeof(double);
 }
 
 hipError_t pdhg_wave_launch(int v, const PdhgArgs& a, hipStream_t stream) {

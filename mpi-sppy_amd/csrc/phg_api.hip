@@ -33,7 +33,7 @@ int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long b
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_block_num_variants();
-void pdhg_block_variant_shape(int v, int* out8);
+void pdhg_block_variant_shape(int v, int* out9);
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad);
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream);
@@ -119,12 +119,12 @@ struct phg_handle {
     std::vector<int> stream_cperm;   // CSC entry -> CSR position (values gathered after prep)
     int mshape[2] = {0, 0};
     MfmaLayout mf{};
-    int bshape[8] = {0};
+    int bshape[9] = {0};
     std::vector<int> block_rperm, block_cperm;   // piece layout -> CSR position (host copies)
     bool vals_shared = false;
     // delta value form (phg_batch.vals_form): vary[p] = CSR position p differs between scenarios;
-    // delta_scale = one Ruiz scaling for every scenario (from the element-wise mean |a|), so the
-    // workgroup kernel streams per scenario only the piece-entry rows holding a varying entry
+    // delta_scale = the workgroup kernel holds the unscaled constant entries once and applies each
+    // scenario's scaling on the fly (BlockLayout::vscale), streaming only the entry rows that vary
     std::vector<char> vary;
     int n_vary = 0;
     bool delta_scale = false;
@@ -934,7 +934,7 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
 static constexpr int kPiece = 8;
 
 static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vector<int>& colptr,
-                              const std::vector<int>& csc_row, const std::vector<int>& csc_p) {
+                              const std::vector<int>& csc_row, const std::vector<int>& csc_p, bool want_delta) {
     const int n = b->n, m = b->m;
     // pieces in row (column) order
     std::vector<int> rpf(m), rpc(m), cpf(n), cpc(n);
@@ -967,10 +967,11 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     // PHG_BLOCK_CL=0: skip the column-local variants (A/B)
     const char* ec = std::getenv("PHG_BLOCK_CL");
     const bool cl_off = ec && std::atoi(ec) == 0;
-    int sh[8], chosen = -1;
+    int sh[9], chosen = -1;
     for (int v = 0; v < pdhg_block_num_variants(); ++v) {
         pdhg_block_variant_shape(v, sh);
         const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4], RE = sh[5], CE = sh[6], CL = sh[7];
+        if ((sh[8] != 0) != want_delta) continue;   // delta form: the on-the-fly scaling variants
         if (n > CPL * NT || m > RPL * NT || (int)rps.size() > PPT * NT || (int)cps.size() > QPT * NT) continue;
         if (RE > 0 && (stream_only || rlen > RE || clen > CE)) continue;   // pieces must fit the registers
         if (CL && (!col_one_piece || cl_off)) continue;
@@ -1138,8 +1139,10 @@ static int build_wave_values(phg_handle* h) {
 }
 
 // piece-major copies of the (preconditioned) values; one copy when every scenario has the same A
-static int build_block_values(phg_handle* h) {
+static int build_block_values(phg_handle* h, const double* raw) {
     BlockLayout& L = h->blk;
+    L.vscale = h->delta_scale ? 1 : 0;
+    const double* src = h->delta_scale ? raw : h->vals;   // unscaled values for the delta form
     const int Er = (int)h->block_rperm.size(), Ec = (int)h->block_cperm.size();
     const bool one = h->vals_shared || h->delta_scale;   // one copy of the (constant) entries
     const int Sv = one ? 1 : h->S;
@@ -1152,8 +1155,8 @@ static int build_block_values(phg_handle* h) {
     if (dput(h, &cperm, h->block_cperm.data(), Ec)) return -1;
     if (dalloc(h, &rv, (size_t)Sv * Er)) return -1;
     if (dalloc(h, &cv, (size_t)Sv * Ec)) return -1;
-    CK(piece_gather_launch(h->vals, h->nnz, rperm, Er, Sv, rv, h->stream));
-    CK(piece_gather_launch(h->vals, h->nnz, cperm, Ec, Sv, cv, h->stream));
+    CK(piece_gather_launch(src, h->nnz, rperm, Er, Sv, rv, h->stream));
+    CK(piece_gather_launch(src, h->nnz, cperm, Ec, Sv, cv, h->stream));
     L.rvals = rv;
     L.cvals = cv;
     L.vstride_r = one ? 0 : Er;
@@ -1183,7 +1186,7 @@ static int build_block_values(phg_handle* h) {
         double* out;
         if (dput(h, &dp, dperm.data(), dperm.size())) return -1;
         if (dalloc(h, &out, (size_t)h->S * dperm.size())) return -1;
-        CK(piece_gather_launch(h->vals, h->nnz, dp, (int)dperm.size(), h->S, out, h->stream));
+        CK(piece_gather_launch(src, h->nnz, dp, (int)dperm.size(), h->S, out, h->stream));
         *dv = out;
         *dstride = (long)dperm.size();
         return 0;
@@ -1959,14 +1962,16 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
         if (wr == 0) h->variant = -1;
     }
     if (h->mfma_variant < 0 && lr != 0 && gr != 0 && wr != 0 && pol != PHG_LAYOUT_STREAM && pol != PHG_LAYOUT_BORDER) {
-        br = build_block_layout(h, b, colptr, csc_row, csc_p);
-        if (br < 0 || (br > 0 && pol == PHG_LAYOUT_BLOCK)) return -1;
-        h->variant = -1;
-        // few varying entries: one scaling for all scenarios, so the constant entries have ONE
-        // scaled copy and only the varying ones stream per scenario (build_block_values)
+        // few varying entries: the constant ones as ONE unscaled copy, each scenario's scaling applied
+        // on the fly, only the varying ones streamed per scenario (build_block_values, BlockLayout::vscale)
         const char* ed = std::getenv("PHG_DELTA");
         const bool delta_off = ed && std::atoi(ed) == 0;
-        h->delta_scale = br == 0 && !delta_off && h->n_vary > 0 && 2L * h->n_vary <= (long)b->nnz;
+        const bool want_delta = !delta_off && h->n_vary > 0 && 2L * h->n_vary <= (long)b->nnz;
+        br = build_block_layout(h, b, colptr, csc_row, csc_p, want_delta);
+        if (br > 0 && want_delta) br = build_block_layout(h, b, colptr, csc_row, csc_p, false);
+        if (br < 0 || (br > 0 && pol == PHG_LAYOUT_BLOCK)) return -1;
+        h->variant = -1;
+        h->delta_scale = br == 0 && h->bshape[8] != 0;
     }
     if (h->mfma_variant < 0 && lr != 0 && gr != 0 && wr != 0 && br != 0) {
         if (build_stream_layout(h, b, colptr, csc_row, csc_p, pol)) return -1;
@@ -2052,21 +2057,14 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
     if (dput(h, &ip, row_of_p.data(), nnz)) return -1; pa.row_of_p = ip;
     double* scratch;
     if (dalloc(h, &scratch, (size_t)S * (2 * n + 2 * m))) return -1;
+    // delta form: the pieces take the caller's (unscaled) values; prep scales h->vals in place
+    double* raw = nullptr;
+    if (h->delta_scale) {
+        CK(hipMalloc((void**)&raw, (size_t)S * nnz * sizeof(double)));
+        CK(hipMemcpyAsync(raw, h->vals, (size_t)S * nnz * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    }
     pa.vals = h->vals; pa.dc = h->dc; pa.dr = h->dr; pa.cl = h->cl; pa.cu = h->cu; pa.rl = h->rl;
     pa.ru = h->ru; pa.eta = h->eta; pa.bnorm = h->bnorm; pa.scratch = scratch;
-    pa.vary = nullptr; pa.row_allvar = nullptr; pa.col_allvar = nullptr;
-    if (h->delta_scale) {   // norms over the constant entries (PrepArgs::vary): one scaling of them everywhere
-        std::vector<unsigned char> vy(nnz), ra(m, 1), ca(n, 1);
-        for (int i = 0; i < m; ++i)
-            for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p) {
-                vy[p] = h->vary[p] ? 1 : 0;
-                if (!h->vary[p]) { ra[i] = 0; ca[b->colidx[p]] = 0; }
-            }
-        unsigned char* u8;
-        if (dput(h, &u8, vy.data(), vy.size())) return -1; pa.vary = u8;
-        if (dput(h, &u8, ra.data(), ra.size())) return -1; pa.row_allvar = u8;
-        if (dput(h, &u8, ca.data(), ca.size())) return -1; pa.col_allvar = u8;
-    }
     CK(prep_launch(pa, h->stream));
     {   // safe bounds (bound.hip): pattern in CSR / CSC, implied column bounds, repair candidates
         std::vector<double> il, ih;
@@ -2081,7 +2079,11 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
         sb.nf = (int)fc.size();
         if (dput(h, &ip, fc.data(), std::max<size_t>(1, fc.size()))) return -1; sb.free_col = ip;
     }
-    if (h->block_variant >= 0 && build_block_values(h)) return -1;
+    if (h->block_variant >= 0 && build_block_values(h, raw)) return -1;
+    if (raw) {
+        CK(hipStreamSynchronize(h->stream));
+        CK(hipFree(raw));
+    }
     if (h->wave_variant >= 0 && build_wave_values(h)) return -1;
     if (h->mfma_variant >= 0 && build_mfma_fragments(h, b)) return -1;
     if (h->stream_layout && build_stream_values(h)) return -1;

@@ -57,10 +57,14 @@ struct BlockLayout {
     const double* rvals;    // [S or 1][sum rk NT] scaled values, row pieces (0 on padding)
     const double* cvals;    // [S or 1][sum ck NT] scaled values, column pieces
     long vstride_r, vstride_c;   // per-scenario strides (0: one matrix shared by all scenarios)
-    // delta form (phg_batch.vals_form; one scaling for all scenarios): entry row R (the NT entries
-    // e = R NT .. R NT + NT - 1 of the piece-major arrays) holding a varying entry reads its values
-    // from the scenario's block rdrow[R] of rvd ([S][nd_r NT]; the row's constant entries copied into
-    // it too), every other entry row from the shared rvals (vstride_r = 0); -1 = shared
+    // delta form (phg_batch.vals_form): the pieces hold the UNSCALED values -- the constant ones once
+    // for all scenarios -- and the kernel applies each scenario's own Ruiz / Pock-Chambolle scaling
+    // on the fly (A_hat x = Dr (A (Dc x)): x and y enter the LDS multiplied by dc / dr, the sums leave
+    // multiplied by dr / dc; vscale = 1).  Entry row R (the NT entries e = R NT .. R NT + NT - 1 of the
+    // piece-major arrays) holding a varying entry reads its values from the scenario's block rdrow[R]
+    // of rvd ([S][nd_r NT]; the row's constant entries copied into it too), every other entry row from
+    // the shared rvals (vstride_r = 0); -1 = shared
+    int vscale;
     int rdrow[32], cdrow[32];
     const double* rvd;
     const double* cvd;
@@ -271,15 +275,6 @@ struct PrepArgs {
     double* eta;            // [S]
     double* bnorm;          // [S]
     double* scratch;        // [S*(2n+2m)]
-    // delta form (phg_batch.vals_form): vary [nnz] marks the entries that differ between scenarios.
-    // A row (column) with at least one constant entry takes its Ruiz / Pock-Chambolle norm over its
-    // constant entries only -- the same in every scenario, so the constant entries keep one scaled
-    // value everywhere (one shared copy in the solver); a row (column) of varying entries only
-    // (row_allvar / col_allvar: netdes' x_e columns, whose one entry is -u_e) is equilibrated per
-    // scenario.  Null: every norm over the scenario's own row / column.
-    const unsigned char* vary;
-    const unsigned char* row_allvar;   // [m]
-    const unsigned char* col_allvar;   // [n]
 };
 
 struct NodeSeg {           // a contiguous scenario range inside one node (one level)

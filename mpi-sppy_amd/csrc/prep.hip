@@ -38,25 +38,18 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     for (int j = tid; j < n; j += 256) dc[j] = 1.0;
     for (int i = tid; i < m; i += 256) dr[i] = 1.0;
     __syncthreads();
-    // delta form (PrepArgs::vary): a norm over the constant entries of the row / column unless it has
-    // none -- every workgroup computes the same factors for those rows and columns
-    auto counts = [&](int p, bool allvar) { return !a.vary || !a.vary[p] || allvar; };
     for (int pass = 0; pass <= a.ruiz_iters; ++pass) {
         const bool pock = (pass == a.ruiz_iters);
         for (int i = tid; i < m; i += 256) {
-            const bool av_ = a.row_allvar && a.row_allvar[i];
             double acc = 0.0;
             for (int p = a.rowptr[i]; p < a.rowptr[i + 1]; ++p)
-                if (counts(p, av_)) acc = pock ? acc + fabs(v[p]) : fmax(acc, fabs(v[p]));
+                acc = pock ? acc + fabs(v[p]) : fmax(acc, fabs(v[p]));
             rs[i] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;
         }
         for (int j = tid; j < n; j += 256) {
-            const bool av_ = a.col_allvar && a.col_allvar[j];
             double acc = 0.0;
             for (int t = a.colptr[j]; t < a.colptr[j + 1]; ++t) {
-                const int p = a.csc_p[t];
-                if (!counts(p, av_)) continue;
-                const double av = fabs(v[p]);
+                const double av = fabs(v[a.csc_p[t]]);
                 acc = pock ? acc + av : fmax(acc, av);
             }
             cs[j] = acc > 0.0 ? 1.0 / sqrt(acc) : 1.0;

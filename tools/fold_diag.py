@@ -39,6 +39,7 @@ def main():
         print("  xN vs xs*dc after Iter0: max |diff|", float(np.abs(xN - xu).max()),
               "differing", int((xN != xu).sum()), "of", xN.size, flush=True)
         phs.append(ph)
+    xN0 = phs[1].engine.get(_lib.F_XN).copy()
     for k in range(1, iters + 1):
         for ph in phs:
             ph.engine.ph_step(0.0, k == 1)
@@ -51,6 +52,10 @@ def main():
         Wa, Wb = a.engine.get(_lib.F_W), b.engine.get(_lib.F_W)   # (fold: flushes nothing -- applied by the solve)
         dW, dx, dxb = np.abs(Wa - Wb), np.abs(xa - xb), np.abs(xba - xbb)
         line = f"it {k}: max|dW| {dW.max():.3e} max|dxN| {dx.max():.3e} max|dxbar| {dxb.max():.3e}"
+        if k == 1:   # W_1 = rho (x_0 - xbar_1) with rho = 1, W_0 = 0: exact on the host
+            Wh = xN0 - np.tile(xba, S)
+            line += (f"\n  host W_1: fold differs in {int((Wa != Wh).sum())}, two-launch in {int((Wb != Wh).sum())} of {Wh.size}"
+                     f"; xbar_1 fold == two-launch: {bool((xba == xbb).all())}")
         if dW.max() > 0:
             e = int(np.argmax(dW > 0))
             line += f"  first W diff at {e} (s {e // a.engine.N}, k {e % a.engine.N}): {Wa[e]!r} vs {Wb[e]!r}"
