@@ -183,13 +183,14 @@ int  phg_sync(phg_handle* h);
  *            shared-matrix fp64 MFMA layout (pdhg_mfma.hip, 16 scenarios per wave);
  *            else the lane-local register layout (pdhg_local.hip) when the pattern splits into
  *            blocks that fit a lane plus <= a few coupling rows, else the wave LDS-gather layout
- *            (pdhg.hip, n, m <= 256), else -- when every scenario has the same matrix, its columns
- *            have <= 2 entries and n <= 1024, m <= 64 -- one wavefront per scenario with the matrix
- *            once per workgroup in LDS (pdhg_wave.hip), else the workgroup-per-scenario streaming layout
+ *            (pdhg.hip, n, m <= 256), else the workgroup-per-scenario streaming layout
  *            (pdhg_block.hip, n, m up to 4096), else a multi-workgroup layout (K workgroups per
  *            scenario): the bordered block-diagonal one (pdhg_border.hip: column blocks coupled by
  *            <= 1024 linking rows, slices in LDS, one cross-workgroup exchange per iteration) when
  *            the pattern has that structure, else the range-split one (pdhg_stream.hip, any size)
+ *   WAVE   : (on request only) one wavefront per scenario, the matrix once per workgroup in LDS
+ *            (pdhg_wave.hip: every scenario the same matrix, columns with <= 2 entries, n <= 1024,
+ *            m <= 64; measured slower than BLOCK on sslp)
  *   GATHER / LOCAL / BLOCK / MFMA / STREAM / BORDER / WAVE : that layout or fail (MFMA, WAVE: shared matrix
  *            only; STREAM: the range-split kernel)                                             */
 enum { PHG_LAYOUT_AUTO = 0, PHG_LAYOUT_GATHER = 1, PHG_LAYOUT_LOCAL = 2, PHG_LAYOUT_BLOCK = 3,

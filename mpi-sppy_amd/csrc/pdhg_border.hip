@@ -1000,7 +1000,7 @@ hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream) {
     void* args[] = {&copy};
     const void* fn = a.bd.reg ? (const void*)pdhg_border_reg_kernel<kBorderRegNT, 2>
                               : (const void*)pdhg_border_kernel<kBorderNT>;
-    if (L.K == 1) return hipLaunchKernel(fn, grid, block, args, lds, stream);
+    if (L.K == 1 || !coop_launch_enabled()) return hipLaunchKernel(fn, grid, block, args, lds, stream);
     return hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)lds, stream);
 }
 

@@ -69,6 +69,14 @@ constexpr size_t local_lds_bytes() {
 template <int LPS, int CPL, int RPL, int D>
 constexpr int local_waves() { return 2; }
 
+// (xs dc) - xbar, each operation rounded on its own (the folded W update must see the bits of the
+// epilogue's xN = xs dc)
+__device__ __forceinline__ double x_minus_xbar(double xs, double dc, double xbar) {
+#pragma clang fp contract(off)
+    const double x = xs * dc;
+    return x - xbar;
+}
+
 template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC, unsigned long long BI>
 __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
@@ -349,8 +357,10 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                     const long t = sN + kk;
                     double w = a.W[t];
                     if (a.fold_w) {   // Update_W (phbase.py:301-326) of the x this solve starts from
-                        // the epilogue's xN = xs * dc, rounded as it was (no FMA contraction here)
-                        const double dv = __dsub_rn(__dmul_rn(a.xs_in[b], dd), a.xbar[xbar_slot(a, t, kk)]);
+                        // the epilogue's xN = xs * dc, rounded as it was: x - xbar without FMA
+                        // contraction (__dmul_rn / __dsub_rn alone are plain IR operations the
+                        // optimiser fused into fma(xs, dc, -xbar), 1 ulp off the two-launch update)
+                        const double dv = x_minus_xbar(a.xs_in[b], dd, a.xbar[xbar_slot(a, t, kk)]);
                         w = fma(rho_of(a, t, kk), dv, w);
                         a.W_rw[t] = w;
                         dsum += fabs(dv);

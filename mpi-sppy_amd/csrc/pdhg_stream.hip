@@ -413,7 +413,7 @@ hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream) {
     const void* fn = L.res ? (const void*)pdhg_stream_kernel<kStreamNT, true> : (const void*)pdhg_stream_kernel<kStreamNT, false>;
     PdhgArgs copy = a;
     void* args[] = {&copy};
-    if (L.K == 1) return hipLaunchKernel(fn, grid, block, args, lds, stream);
+    if (L.K == 1 || !coop_launch_enabled()) return hipLaunchKernel(fn, grid, block, args, lds, stream);
     return hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)lds, stream);
 }
 

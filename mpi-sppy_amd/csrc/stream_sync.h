@@ -7,9 +7,26 @@
 // every wave's vmcnt(0); the consumer polls with sc1 loads and its other waves load after a
 // workgroup barrier; one 1024-thread workgroup per CU (<= 128 VGPRs: the CU's 16 wave slots).
 #pragma once
+#include <cstdlib>
+
 #include "wave_ops.h"
 
 namespace phg {
+
+// K > 1 workgroups per scenario are launched cooperatively (hipLaunchCooperativeKernel: the
+// runtime guarantees co-residency or fails).  PHG_COOP=0: a plain launch of the same grid -- every
+// workgroup is resident anyway (one per CU, grid <= the CU count, nothing else on the device), and
+// the bounded waits of scen_barrier / the granule reads turn a missing co-resident into an error,
+// never a hang.  For rocprofv3: its kernel-trace teardown segfaults after any cooperative launch
+// (tools/repro/coop_exit.hip: a 64-thread cooperative kernel alone reproduces it, the plain launch
+// of the same kernel does not), so UC is profiled with PHG_COOP=0.
+inline bool coop_launch_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("PHG_COOP");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
 
 // write-through (sc1) store and L1-bypassing (sc1) load of the values other workgroups read
 __device__ __forceinline__ void put(double* p, double v) {

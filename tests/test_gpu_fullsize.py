@@ -1,5 +1,5 @@
 """Parity at the bench's full sizes (BASELINE.json configs): farmer cm=10 x 10 000 scenarios
-(local kernel), sslp_15_45_10 x 2 048 (one wave per scenario) and netdes x 1 024 (block kernel), hydro 3-stage tree x 20 000
+(local kernel), sslp_15_45_10 x 2 048 and netdes x 1 024 (block kernel), hydro 3-stage tree x 20 000
 (shared-matrix MFMA kernel).
 
 The whole batch is too large for the oracle, so the checks are
@@ -32,7 +32,7 @@ CASES = {
                lambda S: {"crops_multiplier": 10, "num_scens": S},
                lambda nm, S: om.farmer(nm, crops_multiplier=10, num_scens=S), 8, "local"),
     "sslp": (2048, lambda S: sslp.scenario_names_creator(S), sslp.scenario_creator, lambda S: {},
-             lambda nm, S: om.sslp(nm), 3, "wave"),
+             lambda nm, S: om.sslp(nm), 3, "block"),
     "netdes": (1024, lambda S: netdes.scenario_names_creator(S), netdes.scenario_creator,
                lambda S: {"num_scens": S}, lambda nm, S: om.netdes(nm, num_scens=S), 2, "block"),
 }

@@ -47,7 +47,7 @@ def test_iter0_lp_block_kernel(case, S):
     pn, pc, pkw, on, oc, okw = CASES[case]
     ph = PH(_opts(), pn(S), pc, scenario_creator_kwargs=pkw)
     ph.PH_Prep()
-    assert ph.engine.layout == ("wave" if case == "sslp" else "block")   # sslp: one matrix for all scenarios
+    assert ph.engine.layout == "block"
     tb = ph.Iter0()
     o = oph.OraclePH(_opts(), on(S), oc, okw)
     otb = o.Iter0()
@@ -57,7 +57,7 @@ def test_iter0_lp_block_kernel(case, S):
     assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
 
 
-@pytest.mark.parametrize("case,S,layout", [("sslp", 4, "auto"), ("sslp", 4, "block"), ("netdes", 3, "auto"),
+@pytest.mark.parametrize("case,S,layout", [("sslp", 4, "auto"), ("sslp", 4, "wave"), ("netdes", 3, "auto"),
                                            ("sslp", 4, "stream"), ("uc_small", 4, "stream")])
 def test_prox_qp_block_kernel(case, S, layout):
     """layout "stream": the range-split multi-workgroup kernel (pdhg_stream.hip) with K > 1
@@ -207,8 +207,7 @@ def test_uc_fullsize_stream_vs_oracle(S, layout):
 
 def test_block_register_pieces_same_bits(monkeypatch):
     """sslp's pieces fit the registers (row pieces <= 8, columns in <= 2 rows), so the block layout
-    (AUTO takes the wave layout for sslp: test_wave_kernel_matches_block_kernel) runs the
-    block kernel with the matrix held in registers for the whole solve; PHG_BLOCK_STREAM=1 forces
+    runs the block kernel with the matrix held in registers for the whole solve; PHG_BLOCK_STREAM=1 forces
     the form that re-reads values / indices every iteration.  Same products in the same order:
     Iter0 and one prox-QP solve give bit-identical objectives, iteration counts and nonants."""
     S = 8
@@ -266,8 +265,9 @@ def test_uc_fullsize_lagrangian_lp_vs_oracle():
 
 
 def test_wave_kernel_matches_block_kernel():
-    """sslp (one matrix for every scenario, columns in <= 2 rows): AUTO runs pdhg_wave.hip -- one
-    wavefront per scenario, the matrix once per workgroup in LDS, no workgroup barrier in the loop --
+    """sslp (one matrix for every scenario, columns in <= 2 rows) on the wave layout (pdhg_wave.hip, on
+    request only: slower than the block kernel on MI355X) -- one wavefront per scenario, the matrix
+    once per workgroup in LDS, no workgroup barrier in the loop --
     which adds the same pieces in the same order as the workgroup kernel but reduces its KKT norms
     over a wave instead of a workgroup.  Iter0 and two prox-QP solves at the oracle's W / x-bar, both
     layouts: objectives and bounds agree to 1e-9 relative, nonants to 1e-7, every solve at status 0;
