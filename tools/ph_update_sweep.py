@@ -160,7 +160,8 @@ def main():
     cases = ((10000, 100), (100000, 100), (100000, 1000))
     if os.environ.get("SWEEP_CASES"):   # e.g. "100000x1000,10000x100"
         cases = tuple(tuple(int(v) for v in c.split("x")) for c in os.environ["SWEEP_CASES"].split(","))
-    for S, N in cases:
+    only_fold = os.environ.get("SWEEP_ONLY_FOLD") == "1"
+    for S, N in (() if only_fold else cases):
         r = run(S, N)
         print(json.dumps(r), flush=True)
         out.append(r)
