@@ -584,6 +584,37 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         }
         return t < NL ? gget(g2 + (long)t * 2, ep) : 0.0;
     };
+    // the same exchange split around independent work (the PDHG iteration): ex_publish stores this
+    // workgroup's linking-row partials (hop 1 starts), ex_complete reads them back, publishes the row
+    // sums (hop 2 starts), runs mid() -- work that needs this call's workgroup barrier but not the
+    // linking rows' sums -- and returns the sum of row t.  The same arithmetic in the same order as
+    // exchange(): the same bits.
+    auto ex_publish = [&](double v) -> unsigned {
+        if (K == 1) return 0u;
+        const unsigned ep = ++ex_ep;
+        unsigned long long* g1 = G1 + ((long)slot * 2 + (ep & 1u)) * NL * K * 2;
+        if (t < NL) gput(g1 + ((long)t * K + kw) * 2, ep, v);
+        return ep;
+    };
+    auto ex_complete = [&](unsigned ep, double v, auto mid) {
+        if (K == 1) {
+            __syncthreads();
+            mid();
+            return v;
+        }
+        unsigned long long* g1 = G1 + ((long)slot * 2 + (ep & 1u)) * NL * K * 2;
+        unsigned long long* g2 = G2 + ((long)slot * 2 + (ep & 1u)) * NL * 2;
+        const int nown = (NL - kw + K - 1) / K;
+        for (int u = t; u < nown * K; u += NT) xtmp[u] = gget(g1 + ((long)(kw + K * (u / K)) * K + u % K) * 2, ep);
+        __syncthreads();
+        if (t < nown) {
+            double acc = xtmp[t * K];
+            for (int q = 1; q < K; ++q) acc += xtmp[t * K + q];
+            gput(g2 + (long)(kw + K * t) * 2, ep, acc);
+        }
+        mid();
+        return t < NL ? gget(g2 + (long)t * 2, ep) : 0.0;
+    };
     auto settle = [&]() {   // after an exchange: one workgroup barrier, then the give-up flag
         __syncthreads();
         if (s_dead) alive = false;
@@ -610,6 +641,15 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         return acc;
     };
     bool vals_loaded = false;
+    // owned columns with no linking-row entry (their A^T y needs only the local y)
+    __syncthreads();   // lcp / lri in LDS
+    bool loc_[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        loc_[e] = true;
+        if (cv_[e])
+            for (int p = lcp[t + e * NT]; p < lcp[t + e * NT + 1]; ++p) loc_[e] = loc_[e] && lri[p] >= 0;
+    }
 
     while (true) {
     if (kw == 0 && t == 0) {
@@ -790,6 +830,13 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
                     Xl[t + e * NT] = xn;
                 }
             __syncthreads();
+            // the iteration's one cross-workgroup step, overlapped: the linking-row partials go out
+            // first; the local rows' dual step runs during hop 1, the A^T y of the columns without a
+            // linking-row entry during hop 2 (it needs only the local y, visible after the exchange's
+            // barrier); the other columns' A^T y after the linking y.  Same operations as before,
+            // reordered: the same bits (test_border_matches_block_kernel)
+            const double axl = ax_link();
+            const unsigned ep = ex_publish(axl);
 #pragma unroll
             for (int e = 0; e < E; ++e)
                 if (rv_[e]) {
@@ -801,7 +848,11 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
                     ys[e] += yn;
                     Yl[t + e * NT] = yn;
                 }
-            const double axn_l = exchange(ax_link());   // the iteration's one cross-workgroup step
+            const double axn_l = ex_complete(ep, axl, [&]() {
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (cv_[e] && loc_[e]) aty[e] = aty_col(yl, t + e * NT);
+            });
             if (t < NL) {
                 const double g = l_y - sig * (2.0 * axn_l - l_ax);
                 l_y = fmax(fma(sig, l_lo, g), 0.0) + fmin(fma(sig, l_hi, g), 0.0);
@@ -812,7 +863,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             settle();
 #pragma unroll
             for (int e = 0; e < E; ++e)
-                if (cv_[e]) aty[e] = aty_col(yl, t + e * NT);
+                if (cv_[e] && !loc_[e]) aty[e] = aty_col(yl, t + e * NT);
         }
         if (!alive) break;
         it += chk;
