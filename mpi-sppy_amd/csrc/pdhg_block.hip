@@ -51,6 +51,18 @@ __device__ __forceinline__ double piece_sum(const double* p, int cnt) {
     for (int u = 0; u < cnt; ++u) acc += p[u];
     return acc;
 }
+// the same sum with the (<= 8) partials' loads issued together, added in the same order (PS
+// variants; + 0.0 past the row's pieces leaves the sum unchanged)
+__device__ __forceinline__ double piece_sum8(const double* p, int cnt) {
+    if (cnt > 8) return piece_sum(p, cnt);
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = u < cnt ? p[u] : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+    return acc;
+}
 
 // RE / CE > 0: every row (column) piece slot holds at most RE (CE) entries, and the thread's piece
 // values and LDS indices are loaded into registers once, in the prologue -- the matrix is constant
@@ -66,7 +78,7 @@ __device__ __forceinline__ double piece_sum(const double* p, int cnt) {
 // VS: the delta value form (BlockLayout::vscale) -- the pieces hold unscaled values and the scenario's
 // scaling is applied on the fly: x and y enter the LDS as dc x and dr y, A x leaves as dr (A (dc x)),
 // A^T y as dc (A^T (dr y)).
-template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL, bool VS>
+template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL, bool VS, bool PS = false>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     static_assert(!CL || QPT == CPL, "column-local A^T y needs one piece slot per column slot");
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
@@ -211,7 +223,10 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < RPL; ++r) out[r] = VS ? piece_sum(rp + rf[r], rn[r]) * drs[r] : piece_sum(rp + rf[r], rn[r]);
+        for (int r = 0; r < RPL; ++r) {
+            const double t_ = PS ? piece_sum8(rp + rf[r], rn[r]) : piece_sum(rp + rf[r], rn[r]);
+            out[r] = VS ? t_ * drs[r] : t_;
+        }
     };
     // A^T y for the y currently in yl
     auto spmv_aty = [&](double (&out)[CPL]) {
@@ -502,18 +517,21 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 
 // ----------------------------------------------------------------------------- dispatch
 struct BlockVariant {
-    int NT, CPL, RPL, PPT, QPT, RE, CE, CL, VS;
+    int NT, CPL, RPL, PPT, QPT, RE, CE, CL, VS, PS;
     void (*fn)(PdhgArgs);
 };
 
-#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, false>}
-#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, false>}
-#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false>}
+#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, false>}
+#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, false>}
+#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false>}
+// row piece sums with their loads issued together (on request: PHG_PSUM=1, A/B)
+#define PHG_BRP(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, true>}
 // the delta value form (unscaled shared pieces, scaling on the fly)
-#define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
-#define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
+#define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
+#define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
+    PHG_BRP(256, 3, 1, 2, 3, 8, 2, true),   // (PHG_PSUM=1 only)
     PHG_BR(256, 3, 1, 2, 3, 8, 2, true),    // sslp-like: register-resident pieces, column-local A^T y
     PHG_BR(256, 3, 1, 2, 3, 8, 2, false),   // the same with A^T y through LDS partials
     PHG_B(256, 3, 1, 2, 3),      // sslp-like: n <= 768, m <= 256
@@ -535,14 +553,17 @@ static const BlockVariant kBlockVariants[] = {
 #undef PHG_BC
 #undef PHG_BV
 #undef PHG_BCV
+#undef PHG_BRP
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
 
-void pdhg_block_variant_shape(int v, int* out9) {
+void pdhg_block_variant_shape(int v, int* out10) {
+    int* out9 = out10;
     const BlockVariant& V = kBlockVariants[v];
     out9[0] = V.NT; out9[1] = V.CPL; out9[2] = V.RPL; out9[3] = V.PPT; out9[4] = V.QPT; out9[5] = V.RE; out9[6] = V.CE;
     out9[7] = V.CL;
     out9[8] = V.VS;
+    out9[9] = V.PS;
 }
 
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad) {

@@ -33,7 +33,7 @@ int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long b
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_block_num_variants();
-void pdhg_block_variant_shape(int v, int* out9);
+void pdhg_block_variant_shape(int v, int* out10);
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad);
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream);
@@ -119,7 +119,7 @@ struct phg_handle {
     std::vector<int> stream_cperm;   // CSC entry -> CSR position (values gathered after prep)
     int mshape[2] = {0, 0};
     MfmaLayout mf{};
-    int bshape[9] = {0};
+    int bshape[10] = {0};
     std::vector<int> block_rperm, block_cperm;   // piece layout -> CSR position (host copies)
     bool vals_shared = false;
     // delta value form (phg_batch.vals_form): vary[p] = CSR position p differs between scenarios;
@@ -967,9 +967,13 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     // PHG_BLOCK_CL=0: skip the column-local variants (A/B)
     const char* ec = std::getenv("PHG_BLOCK_CL");
     const bool cl_off = ec && std::atoi(ec) == 0;
-    int sh[9], chosen = -1;
+    // PHG_PSUM=1: the variants whose row piece sums issue their loads together (A/B)
+    const char* eps_ = std::getenv("PHG_PSUM");
+    const bool psum = eps_ && std::atoi(eps_) != 0;
+    int sh[10], chosen = -1;
     for (int v = 0; v < pdhg_block_num_variants(); ++v) {
         pdhg_block_variant_shape(v, sh);
+        if ((sh[9] != 0) != psum && sh[9] != 0) continue;
         const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4], RE = sh[5], CE = sh[6], CL = sh[7];
         if ((sh[8] != 0) != want_delta) continue;   // delta form: the on-the-fly scaling variants
         if (n > CPL * NT || m > RPL * NT || (int)rps.size() > PPT * NT || (int)cps.size() > QPT * NT) continue;
