@@ -132,7 +132,10 @@ typedef struct phg_opts {
      * maximising) only when no finite certificate results.  For the bound consumers of spopt.py:
      * 225-230 (Iter0's trivial bound, spopt.py:377-422 Ebound; the Lagrangian spoke,
      * lagrangian_bounder.py:21-44) at scenarios that stopped at the iteration limit.  Not with
-     * fix_nonants.                                                                              */
+     * fix_nonants.  2: the certificate for EVERY scenario -- the dual objective of a converged solve
+     * is accurate to eps (1 + |p| + |d|) on either side of the optimum, as a CPU solver's bound is at
+     * its tolerances; at a loose eps (UC runs at 1e-6) that can sit above the optimum by ~1e-6
+     * relative, the certificate never does.                                                     */
     int32_t safe_bound;
 } phg_opts;
 

@@ -19,7 +19,7 @@
 // zero it, the scenario's bound is -inf: no finite certificate from this iterate.
 //
 // Applied to the scenarios that did NOT reach the KKT tolerance (status 1 / 2); the others keep the
-// PDHG epilogue's dual objective.  One 256-thread workgroup per scenario; duals and reduced costs in per-scenario scratch; the repair
+// PDHG epilogue's dual objective (safe_bound = 2: to every scenario).  One 256-thread workgroup per scenario; duals and reduced costs in per-scenario scratch; the repair
 // (a handful of columns on farmer: the Purchased columns, whose only row is the cattle-feed row) is
 // sequential in one thread; sums are fixed-order block reductions (deterministic).
 #include "phg_internal.h"
@@ -46,7 +46,8 @@ __global__ __launch_bounds__(256) void safe_bound_kernel(PdhgArgs a, SafeBoundAr
     // bound at optimality, as a CPU solver reports it at its tolerances; charging that iterate's
     // tolerance-level reduced costs against implied bounds would only loosen it (farmer: up to
     // 1.5e-6 relative, sold quantities capped at ~1e5)
-    if (a.status[s] == 0) return;
+    // (phg_opts.safe_bound = 2, SafeBoundArgs::all: every scenario -- a certificate at any eps)
+    if (a.status[s] == 0 && !b.all) return;
     const int n = a.n, m = a.m;
     const long sn = (long)s * n, sm = (long)s * m, snz = (long)s * a.nnz, sN = (long)s * a.N;
     double* Y = b.Y + sm;

@@ -2296,7 +2296,9 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             if (dalloc(h, &h->sb.Y, (size_t)h->S * h->m)) return -1;
             if (dalloc(h, &h->sb.R, (size_t)h->S * h->n)) return -1;
         }
-        CK(safe_bound_launch(a, h->sb, h->stream));
+        SafeBoundArgs sb = h->sb;
+        sb.all = o->safe_bound >= 2 ? 1 : 0;
+        CK(safe_bound_launch(a, sb, h->stream));
     }
     swap_state(h);
     ++h->swaps;

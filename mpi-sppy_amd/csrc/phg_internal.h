@@ -257,6 +257,7 @@ struct SafeBoundArgs {
     const double *ilo, *ihi;             // [S*n] unscaled
     const int* free_col;                 // [nf]
     int nf;
+    int all;                             // 1: every scenario (phg_opts.safe_bound = 2), else status != 0 only
     double *Y, *R;                       // [S*m], [S*n]
 };
 

@@ -25,6 +25,15 @@ from . import _lib
 from .engine import Engine
 
 
+
+def safe_bound_mode(eps):
+    """``phg_opts.safe_bound`` for an outer-bound solve at tolerance ``eps``: 1 (certificates for the
+    scenarios that stopped short; a converged scenario keeps its dual objective, accurate to ~eps on
+    either side of its optimum, as a CPU solver's bound at its tolerances) when eps is tight, 2 (a
+    weak-duality certificate for every scenario) when it is loose enough (> 1e-8) for that accuracy
+    to show -- UC's Lagrangian subproblems run at 1e-6."""
+    return 2 if eps > 1e-8 else 1
+
 class _BoundSpoke:
     converger_spoke_char = "?"
     bound_kind = None            # "outer" or "inner"
@@ -123,7 +132,7 @@ class LagrangianOuterBound(_BoundSpoke):
         o = self._solve_opts()
         self.engine.solve(1, 0, eps=o["pdhg_eps"], max_iter=o["pdhg_max_iter"],
                           check_every=o["pdhg_check_every"], warm_start=3,
-                          schedule=o["pdhg_schedule"], safe_bound=True)
+                          schedule=o["pdhg_schedule"], safe_bound=safe_bound_mode(o["pdhg_eps"]))
         return True
 
     def _collect(self):
@@ -308,7 +317,7 @@ def evaluate_lagrangian(opt, eps=None, max_iter=200000, warm=True):
             eng.copy_from(he, _lib.F_WARM)
         o = opt._solver_opts()
         eng.solve(1, 0, eps=eps or o["pdhg_eps"], max_iter=max_iter, check_every=o["pdhg_check_every"],
-                  warm_start=3 if warm else 0, schedule=False, safe_bound=True)
+                  warm_start=3 if warm else 0, schedule=False, safe_bound=safe_bound_mode(eps or o["pdhg_eps"]))
         eng.sync()
         st = eng.get_i32(_lib.I_STATUS)
         evaluate_lagrangian.last_status_counts = np.bincount(st, minlength=3).tolist()

@@ -255,10 +255,12 @@ class Engine:
               fix_nonants=False, schedule=True, beta=(0.0, 0.0, 0.0), theta=0.0, skip_below=0.0, fix_tol=0.0,
               safe_bound=False):
         """safe_bound: every scenario's F_BOUND is a valid outer bound whatever its status (bound.hip;
+        2: a weak-duality certificate also for the converged scenarios, whose own dual objective is
+        accurate to eps on either side;
         -inf / +inf only where the dual iterate yields no finite certificate)."""
         o = _lib.PhgOpts(float(eps), int(max_iter), int(check_every), int(warm_start),
                          int(bool(fix_nonants)), int(bool(schedule)), *[float(v) for v in beta],
-                         float(theta), float(skip_below), float(fix_tol), int(bool(safe_bound)))
+                         float(theta), float(skip_below), float(fix_tol), int(safe_bound))
         self.last_safe_bound = bool(safe_bound) and not fix_nonants
         import ctypes
         _lib.check(self.lib.phg_solve(self.h, int(w_on), int(prox_on), ctypes.byref(o)))

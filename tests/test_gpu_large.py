@@ -235,8 +235,11 @@ def test_uc_fullsize_lagrangian_lp_vs_oracle():
     """The Lagrangian spoke's subproblem at full UC size (W on, prox off: lagrangian_bounder.py:21-44
     with the W of the first PH update, phbase.py:301-326) through the bordered kernel, against HiGHS'
     LP with the same W on two sampled scenarios: objectives at 1e-5 relative (pdhg_eps 1e-6, as the
-    UC runs), and each scenario's safe bound (phg_opts.safe_bound: a weak-duality certificate of the
-    dual iterate) at or below the LP optimum and within 1e-5 of it."""
+    UC runs); each converged scenario's own dual objective within the solve's tolerance of the LP
+    optimum on either side (measured r03: 1.5e-6 ABOVE it on one scenario -- eps (1 + |p| + |d|) at
+    1e-6, as a CPU solver's bound at its tolerances); and with phg_opts.safe_bound = 2 (what the
+    Lagrangian spoke uses at this eps: cylinders.safe_bound_mode) a weak-duality certificate of the
+    dual iterate at or below the LP optimum and within 1e-5 of it."""
     S = 4
     so = {"pdhg_eps": 1e-6}
     ph = PH(_opts(iter0_solver_options=so, iterk_solver_options=so), uc.scenario_names_creator(S),
@@ -248,10 +251,14 @@ def test_uc_fullsize_lagrangian_lp_vs_oracle():
     ph.Update_W()
     W = ph.engine.get(_lib.F_W).reshape(S, ph.engine.N)
     assert np.abs(W).max() > 0
-    ph.engine.solve(1, 0, eps=1e-6, max_iter=200000, warm_start=3, safe_bound=True)
+    ph.engine.solve(1, 0, eps=1e-6, max_iter=200000, warm_start=3, safe_bound=2)
     ph.engine.sync()
     obj, bnd = ph.engine.get(_lib.F_OBJ), ph.engine.get(_lib.F_BOUND)
     st = ph.engine.get_i32(_lib.I_STATUS)
+    # the same solve's own dual objectives (status 0 keeps them with safe_bound = 1)
+    ph.engine.solve(1, 0, eps=1e-6, max_iter=200000, warm_start=3, safe_bound=1)
+    ph.engine.sync()
+    dob, st1 = ph.engine.get(_lib.F_BOUND), ph.engine.get_i32(_lib.I_STATUS)
     pick = [0, S - 1]
     o = oph.OraclePH(_opts(), [om.uc_names(S)[k] for k in pick], om.uc, {"num_scens": len(pick)})
     o.W = W[pick].copy()
@@ -262,6 +269,8 @@ def test_uc_fullsize_lagrangian_lp_vs_oracle():
         assert st[k] == 0, (k, st[k])
         assert abs(obj[k] - ref) <= 1e-5 * abs(ref), (k, obj[k], ref)
         assert bnd[k] <= ref + 1e-9 * abs(ref) and ref - bnd[k] <= 1e-5 * abs(ref), (k, bnd[k], ref)
+        if st1[k] == 0:
+            assert abs(dob[k] - ref) <= 4e-6 * abs(ref), (k, dob[k], ref)
 
 
 def test_wave_kernel_matches_block_kernel():
