@@ -280,8 +280,9 @@ int  phg_ph_update(phg_handle* h, double* host_conv);
  * solve k-1 (x_{k-2}, W_{k-1}, xbar_{k-1}).  After the last iteration, phg_conv_start on the
  * partials gives conv of the last update; if it is below thr, phg_solve_undo restores the state
  * before the last solve.                                                                         */
-/* Folded update (lane-local layout without smoothing / variable probability; off by default --
- * measured slower on farmer 10k, DESIGN.md -- on with phg_set_fold or PHG_FOLD=1): phg_ph_head
+/* Folded update (lane-local layout without smoothing / variable probability; by default on for
+ * batches with S*N >= 1e7 nonant values and off below -- measured slower on farmer 10k, faster at
+ * S*N = 1e8; phg_set_fold / PHG_FOLD override): phg_ph_head
  * then only publishes conv_{k-1} and forms xbar_k; the next
  * phg_solve applies W += rho (x - xbar) in its prologue -- it loads x (its warm start) and W (its
  * objective) anyway, so the update's second read of x and its own launch disappear -- and leaves

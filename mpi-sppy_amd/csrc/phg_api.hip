@@ -94,6 +94,9 @@ static int fail(const std::string& msg) {
             return fail(std::string(#call) + ": " + hipGetErrorString(e_));                   \
     } while (0)
 
+// batches from this many nonant values up take the folded PH update by default (phg_set_fold)
+static constexpr long kFoldMinSN = 10000000;
+
 struct phg_handle {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -215,7 +218,7 @@ struct phg_handle {
     // measured on farmer 10k it slows the PDHG launch by ~9 us (the prologue's dependent W-update
     // chain in every wave) for a ~2.5 us shorter update -- 0.3465 vs 0.340 ms per PH iteration; at
     // S N = 1e8 (S = 1e6, N = 100) 797 vs 847 us per update (tools/ph_update_sweep.py)
-    int fold = 0;
+    int fold = -1;             // -1: the size policy of phg_load_batch (on when S N >= kFoldMinSN)
     bool fold_w_pending = false;      // xbar of update k is in place, its W update not yet applied
     bool xn_external = false;         // PHG_F_XN was set by the caller: xN != xs dc until the next solve
     bool fold_conv_pending = false;   // the last solve did a folded update: its conv partials are
@@ -270,7 +273,7 @@ static int materialize_outputs(phg_handle* h) {
 // the folded update applies to this handle's solves (PdhgArgs::fold_w): lane-local layout, W kept
 // for every nonant (no variable-probability mask), no smoothing centre to update
 static bool fold_active(const phg_handle* h) {
-    return h->fold && h->local_variant >= 0 && !h->smooth_on && !h->ph.pcv;
+    return h->fold > 0 && h->local_variant >= 0 && !h->smooth_on && !h->ph.pcv;
 }
 
 // a folded W update whose solve has not run (xbar of update k in place, phg_ph_head done): apply it
@@ -1899,6 +1902,11 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
     CK(hipSetDevice(h->device));
     const int S = b->S, n = b->n, m = b->m, nnz = b->nnz, N = b->N;
     h->S = S; h->n = n; h->m = m; h->nnz = nnz; h->N = N; h->L = b->L; h->N_tot = b->N_tot;
+    // the folded PH update by batch size (no PHG_FOLD / phg_set_fold before the load): it pays where
+    // the update streams (S N = 1e8: 477 vs 650 us per update, 5.59 vs 5.76 ms per PH iteration with
+    // the solve) and costs where the PDHG launch is latency-bound (farmer 10k, S N = 3e5: 0.3465 vs
+    // 0.340 ms per PH iteration)
+    if (h->fold < 0) h->fold = (long)S * N >= kFoldMinSN ? 1 : 0;
     h->n_nodes = b->n_nodes; h->P = std::max(1, b->virt_nproc);
     h->n_pad = (n + 1) & ~1;
     h->sense = b->sense >= 0 ? 1.0 : -1.0;
