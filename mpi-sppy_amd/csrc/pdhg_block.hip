@@ -524,14 +524,14 @@ struct BlockVariant {
 #define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, false>}
 #define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, false>}
 #define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false>}
-// row piece sums with their loads issued together (on request: PHG_PSUM=1, A/B)
+// row piece sums with their loads issued together (default; PHG_PSUM=0 skips them, A/B)
 #define PHG_BRP(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, true>}
 // the delta value form (unscaled shared pieces, scaling on the fly)
 #define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
 #define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
-    PHG_BRP(256, 3, 1, 2, 3, 8, 2, true),   // (PHG_PSUM=1 only)
+    PHG_BRP(256, 3, 1, 2, 3, 8, 2, true),   // sslp: ... row piece sums' loads issued together (PHG_PSUM=0: not)
     PHG_BR(256, 3, 1, 2, 3, 8, 2, true),    // sslp-like: register-resident pieces, column-local A^T y
     PHG_BR(256, 3, 1, 2, 3, 8, 2, false),   // the same with A^T y through LDS partials
     PHG_B(256, 3, 1, 2, 3),      // sslp-like: n <= 768, m <= 256

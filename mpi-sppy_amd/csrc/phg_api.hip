@@ -970,9 +970,10 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     // PHG_BLOCK_CL=0: skip the column-local variants (A/B)
     const char* ec = std::getenv("PHG_BLOCK_CL");
     const bool cl_off = ec && std::atoi(ec) == 0;
-    // PHG_PSUM=1: the variants whose row piece sums issue their loads together (A/B)
+    // the variants whose row piece sums issue their loads together (sslp 4 096: 8.20 vs 8.86 ms per PH
+    // iteration, the same bits); PHG_PSUM=0 skips them (A/B)
     const char* eps_ = std::getenv("PHG_PSUM");
-    const bool psum = eps_ && std::atoi(eps_) != 0;
+    const bool psum = !(eps_ && std::atoi(eps_) == 0);
     int sh[10], chosen = -1;
     for (int v = 0; v < pdhg_block_num_variants(); ++v) {
         pdhg_block_variant_shape(v, sh);
