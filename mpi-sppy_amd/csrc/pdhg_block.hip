@@ -529,6 +529,7 @@ struct BlockVariant {
 // the delta value form (unscaled shared pieces, scaling on the fly)
 #define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
 #define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
+#define PHG_BCVP(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true, true>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
     PHG_BRP(256, 3, 1, 2, 3, 8, 2, true),   // sslp: ... row piece sums' loads issued together (PHG_PSUM=0: not)
@@ -544,7 +545,8 @@ static const BlockVariant kBlockVariants[] = {
     PHG_BV(256, 3, 1, 2, 3),
     PHG_BV(256, 4, 4, 4, 4),
     PHG_BV(512, 4, 4, 4, 4),
-    PHG_BCV(1024, 3, 2, 3, 3),   // netdes (only the vubs' u_e vary)
+    PHG_BCVP(1024, 3, 2, 3, 3),  // netdes (only the vubs' u_e vary), row piece sums' loads together
+    PHG_BCV(1024, 3, 2, 3, 3),   // the same with sequential piece sums (PHG_PSUM=0)
     PHG_BV(1024, 3, 2, 3, 3),
     PHG_BV(1024, 4, 4, 4, 4),
 };
@@ -554,6 +556,7 @@ static const BlockVariant kBlockVariants[] = {
 #undef PHG_BV
 #undef PHG_BCV
 #undef PHG_BRP
+#undef PHG_BCVP
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
 
