@@ -819,16 +819,21 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     bool use_avg_final = false;
     const int chk = a.check_every;
 
+    // primal step of owned column e (A^T y in aty)
+    auto primal = [&](int e) {
+        const double xn = clampd(fma(tau, aty[e] - cs[e], x[e]) * ip[e], lo[e], hi[e]);
+        x[e] = xn;
+        xs[e] += xn;
+        Xl[t + e * NT] = xn;
+    };
     while (alive) {
+        // pre: the columns without a linking entry took this iteration's primal step already, during
+        // the previous iteration's second hop (never across a check: their A^T y is final there)
+        bool pre = false;
         for (int kk = 0; kk < chk && alive; ++kk) {
 #pragma unroll
             for (int e = 0; e < E; ++e)
-                if (cv_[e]) {
-                    const double xn = clampd(fma(tau, aty[e] - cs[e], x[e]) * ip[e], lo[e], hi[e]);
-                    x[e] = xn;
-                    xs[e] += xn;
-                    Xl[t + e * NT] = xn;
-                }
+                if (cv_[e] && !(pre && loc_[e])) primal(e);
             __syncthreads();
             // the iteration's one cross-workgroup step, overlapped: the linking-row partials go out
             // first; the local rows' dual step runs during hop 1, the A^T y of the columns without a
@@ -848,10 +853,17 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
                     ys[e] += yn;
                     Yl[t + e * NT] = yn;
                 }
+            pre = kk + 1 < chk;
             const double axn_l = ex_complete(ep, axl, [&]() {
 #pragma unroll
                 for (int e = 0; e < E; ++e)
-                    if (cv_[e] && loc_[e]) aty[e] = aty_col(yl, t + e * NT);
+                    if (cv_[e] && loc_[e]) {
+                        aty[e] = aty_col(yl, t + e * NT);
+                        // the next iteration's primal step of this column: its A^T y is complete
+                        // (no linking row), and every read of Xl of this iteration has passed the
+                        // exchange's barrier
+                        if (pre) primal(e);
+                    }
             });
             if (t < NL) {
                 const double g = l_y - sig * (2.0 * axn_l - l_ax);
