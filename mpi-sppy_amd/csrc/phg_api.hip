@@ -320,7 +320,10 @@ int phg_create(int device, phg_handle** out) {
     if (const char* ev = std::getenv("PHG_AVG_EVERY")) h->avg_every = std::max(1, std::atoi(ev));
     if (const char* ev = std::getenv("PHG_FUSE")) h->no_fuse = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_GAP_RAW")) h->gap_const = std::atoi(ev) == 0;
-    if (const char* ev = std::getenv("PHG_SUM_STRIDE")) h->sum_stride = std::atoi(ev) == 2 ? 2 : 1;
+    if (const char* ev = std::getenv("PHG_SUM_STRIDE")) {
+        const int v = std::atoi(ev);
+        h->sum_stride = (v == 2 || v == 3) ? v : 1;   // 3: the windowed running sums (pdhg_local.hip)
+    }
     if (const char* ev = std::getenv("PHG_FOLD")) h->fold = std::atoi(ev) != 0 ? 1 : 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;

@@ -229,7 +229,8 @@ struct PdhgArgs {
     // constant-free form (PHG_GAP_RAW=1, A/B runs)
     int gap_const;
     // lane-local kernel: 1 = the average iterate's running sums take every PDHG iterate, 2 = every
-    // second one (PHG_SUM_STRIDE)
+    // second one, 3 = only the check_every iterates before each check that evaluates the average
+    // (PHG_SUM_STRIDE)
     int sum_stride;
     // folded PH update (phg_ph_head with the fold on, include/phg.h): the prologue first applies
     // Update_W of the x it warm-starts from -- W += rho (x - xbar), x = xs_in dc, the bits the last
