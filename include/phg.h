@@ -224,8 +224,9 @@ int  phg_get_i32(phg_handle* h, int32_t field, int32_t* host_out);
 int  phg_mfma_info(phg_handle* h, int32_t* out4);
 /* value form of the loaded batch (phg_batch.vals_form): out4 = {CSR positions whose value differs
  * between scenarios, 1 if all scenarios share one scaling and one copy of the constant entries (the
- * delta form is in use), matrix values the PDHG kernel reads PER SCENARIO in one A x + A^T y,
- * values it reads from the ONE shared copy in one A x + A^T y} (workgroup layout; the other layouts
+ * delta form is in use; 2: its unit form -- every constant entry is +-1 and the kernel holds the
+ * matrix in LDS as 16-bit entry codes), matrix values the PDHG kernel reads PER SCENARIO in one
+ * A x + A^T y, shared entries in one A x + A^T y} (workgroup layout; the other layouts
  * report {varying, 0, 0, 0})                                                                        */
 int  phg_values_info(phg_handle* h, int32_t* out4);
 int  phg_info(phg_handle* h, int32_t* out8);   /* S, n, m, nnz, N, N_tot, kernel variant

@@ -78,9 +78,15 @@ __device__ __forceinline__ double piece_sum8(const double* p, int cnt) {
 // VS: the delta value form (BlockLayout::vscale) -- the pieces hold unscaled values and the scenario's
 // scaling is applied on the fly: x and y enter the LDS as dc x and dr y, A x leaves as dr (A (dc x)),
 // A^T y as dc (A^T (dr y)).
-template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL, bool VS, bool PS = false>
+//
+// UN: the unit form (BlockLayout::rcode) -- VS with every constant entry +-1: the entry codes and the
+// scenario's varying entry rows sit in LDS, an entry adds or subtracts its x (y) or, on a varying
+// row, fma's its value; acc + v / acc - v are fma(+-1, v, acc) exactly, so the bits equal VS's.
+template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL, bool VS, bool PS = false,
+          bool UN = false>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     static_assert(!CL || QPT == CPL, "column-local A^T y needs one piece slot per column slot");
+    static_assert(!UN || (VS && RE == 0 && CE == 0), "the unit form is a streaming delta-form variant");
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const BlockLayout& B = a.blk;
@@ -105,6 +111,22 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     auto cval = [&](int e, int R) {
         const int d = B.cdrow[R];
         return d >= 0 ? cvd[(long)d * NT + t] : cv[e];
+    };
+    // UN: the scenario's varying entry rows [nd_r + nd_c][NT] and the codes [er + ec] in LDS.  Every
+    // thread reads back only its own entries (e % NT == t), so no barrier is needed before use.
+    double* dl = red + 16 * (NT / 64 + 1);
+    short* codes = reinterpret_cast<short*>(dl + (UN ? (B.nd_r + B.nd_c) * NT : 0));
+    if constexpr (UN) {
+        for (int i = t; i < B.nd_r * NT; i += NT) dl[i] = rvd[i];
+        for (int i = t; i < B.nd_c * NT; i += NT) dl[B.nd_r * NT + i] = cvd[i];
+        for (int i = t; i < B.er; i += NT) codes[i] = B.rcode[i];
+        for (int i = t; i < B.ec; i += NT) codes[B.er + i] = B.ccode[i];
+    }
+    // UN product of code cd (entry row with varying-row index d) with the LDS vector v
+    auto unit_fma = [&](int cd, int d, int drow0, const double* v, double acc) {
+        if (d >= 0) return fma(dl[(drow0 + d) * NT + t], v[cd - 1], acc);
+        const double u = v[(cd < 0 ? -cd : cd) - (cd != 0 ? 1 : 0)];
+        return cd > 0 ? acc + u : (cd < 0 ? acc - u : acc);
     };
 
     // ------------------------------------------------------------------ columns owned
@@ -215,7 +237,8 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
                     const int e = off + k * NT + t;
-                    acc = fma(rval(e, off / NT + k), xl[B.ridx[e]], acc);
+                    if constexpr (UN) acc = unit_fma(codes[e], B.rdrow[off / NT + k], 0, xl, acc);
+                    else acc = fma(rval(e, off / NT + k), xl[B.ridx[e]], acc);
                 }
                 off += kk * NT;
             }
@@ -242,7 +265,8 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
                     const int e = off + k * NT + t;
-                    acc = fma(cval(e, off / NT + k), yl[B.cidx[e]], acc);
+                    if constexpr (UN) acc = unit_fma(codes[B.er + e], B.cdrow[off / NT + k], B.nd_r, yl, acc);
+                    else acc = fma(cval(e, off / NT + k), yl[B.cidx[e]], acc);
                 }
                 off += kk * NT;
             }
@@ -517,19 +541,21 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 
 // ----------------------------------------------------------------------------- dispatch
 struct BlockVariant {
-    int NT, CPL, RPL, PPT, QPT, RE, CE, CL, VS, PS;
+    int NT, CPL, RPL, PPT, QPT, RE, CE, CL, VS, PS, UN;
     void (*fn)(PdhgArgs);
 };
 
-#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, false>}
-#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, false>}
-#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false>}
+#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, false>}
+#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, false>}
+#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false>}
 // row piece sums with their loads issued together (default; PHG_PSUM=0 skips them, A/B)
-#define PHG_BRP(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, true>}
+#define PHG_BRP(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, true>}
 // the delta value form (unscaled shared pieces, scaling on the fly)
-#define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
-#define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
-#define PHG_BCVP(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true, true>}
+#define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
+#define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
+// the unit form of the delta value form (BlockLayout::rcode): chosen at value time, not by the planner
+#define PHG_BCVU(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true, false, true>}
+#define PHG_BVU(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true, false, true>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
     PHG_BRP(256, 3, 1, 2, 3, 8, 2, true),   // sslp: ... row piece sums' loads issued together (PHG_PSUM=0: not)
@@ -550,6 +576,13 @@ static const BlockVariant kBlockVariants[] = {
                                  // at 1 024 -- 372 B/lane of spills at 128 VGPRs -- not kept)
     PHG_BV(1024, 3, 2, 3, 3),
     PHG_BV(1024, 4, 4, 4, 4),
+    // unit twins of the delta-form variants (same shapes; build_block_values switches to them)
+    PHG_BVU(256, 3, 1, 2, 3),
+    PHG_BVU(256, 4, 4, 4, 4),
+    PHG_BVU(512, 4, 4, 4, 4),
+    PHG_BCVU(1024, 3, 2, 3, 3),
+    PHG_BVU(1024, 3, 2, 3, 3),
+    PHG_BVU(1024, 4, 4, 4, 4),
 };
 #undef PHG_B
 #undef PHG_BR
@@ -557,27 +590,31 @@ static const BlockVariant kBlockVariants[] = {
 #undef PHG_BV
 #undef PHG_BCV
 #undef PHG_BRP
-#undef PHG_BCVP
+#undef PHG_BCVU
+#undef PHG_BVU
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
 
-void pdhg_block_variant_shape(int v, int* out10) {
-    int* out9 = out10;
+void pdhg_block_variant_shape(int v, int* out11) {
+    int* out9 = out11;
     const BlockVariant& V = kBlockVariants[v];
     out9[0] = V.NT; out9[1] = V.CPL; out9[2] = V.RPL; out9[3] = V.PPT; out9[4] = V.QPT; out9[5] = V.RE; out9[6] = V.CE;
     out9[7] = V.CL;
     out9[8] = V.VS;
     out9[9] = V.PS;
+    out9[10] = V.UN;
 }
 
-size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad) {
+// UN variants add the varying entry rows (nd doubles per thread) and the er + ec 16-bit codes
+size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad, int nd, int ecodes) {
     const BlockVariant& V = kBlockVariants[v];
-    return (size_t)(n_pad + m_pad + V.PPT * V.NT + V.QPT * V.NT + 16 * (V.NT / 64 + 1)) * sizeof(double);
+    const size_t base = (size_t)(n_pad + m_pad + V.PPT * V.NT + V.QPT * V.NT + 16 * (V.NT / 64 + 1)) * sizeof(double);
+    return V.UN ? base + (size_t)nd * V.NT * sizeof(double) + (size_t)ecodes * sizeof(short) : base;
 }
 
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream) {
     const BlockVariant& V = kBlockVariants[v];
-    const size_t lds = pdhg_block_lds_bytes(v, a.blk.n_pad, a.blk.m_pad);
+    const size_t lds = pdhg_block_lds_bytes(v, a.blk.n_pad, a.blk.m_pad, a.blk.nd_r + a.blk.nd_c, a.blk.er + a.blk.ec);
     hipLaunchKernelGGL(V.fn, dim3(a.S), dim3(V.NT), lds, stream, a);
     return hipGetLastError();
 }

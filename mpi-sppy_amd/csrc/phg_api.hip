@@ -33,8 +33,8 @@ int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long b
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_block_num_variants();
-void pdhg_block_variant_shape(int v, int* out10);
-size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad);
+void pdhg_block_variant_shape(int v, int* out11);
+size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad, int nd, int ecodes);
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream);
 hipError_t pdhg_stream_capacity(int* out);
@@ -122,7 +122,7 @@ struct phg_handle {
     std::vector<int> stream_cperm;   // CSC entry -> CSR position (values gathered after prep)
     int mshape[2] = {0, 0};
     MfmaLayout mf{};
-    int bshape[10] = {0};
+    int bshape[11] = {0};
     std::vector<int> block_rperm, block_cperm;   // piece layout -> CSR position (host copies)
     bool vals_shared = false;
     // delta value form (phg_batch.vals_form): vary[p] = CSR position p differs between scenarios;
@@ -977,16 +977,17 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     // iteration, the same bits); PHG_PSUM=0 skips them (A/B)
     const char* eps_ = std::getenv("PHG_PSUM");
     const bool psum = !(eps_ && std::atoi(eps_) == 0);
-    int sh[10], chosen = -1;
+    int sh[11], chosen = -1;
     for (int v = 0; v < pdhg_block_num_variants(); ++v) {
         pdhg_block_variant_shape(v, sh);
+        if (sh[10]) continue;   // unit twins: chosen by build_block_values
         if ((sh[9] != 0) != psum && sh[9] != 0) continue;
         const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4], RE = sh[5], CE = sh[6], CL = sh[7];
         if ((sh[8] != 0) != want_delta) continue;   // delta form: the on-the-fly scaling variants
         if (n > CPL * NT || m > RPL * NT || (int)rps.size() > PPT * NT || (int)cps.size() > QPT * NT) continue;
         if (RE > 0 && (stream_only || rlen > RE || clen > CE)) continue;   // pieces must fit the registers
         if (CL && (!col_one_piece || cl_off)) continue;
-        if (pdhg_block_lds_bytes(v, n_pad, m_pad) > 160 * 1024) continue;
+        if (pdhg_block_lds_bytes(v, n_pad, m_pad, 0, 0) > 160 * 1024) continue;
         chosen = v;
         break;
     }
@@ -1149,6 +1150,52 @@ static int build_wave_values(phg_handle* h) {
     return 0;
 }
 
+// Unit form (BlockLayout::rcode): when every constant entry of the delta form is -1, 0 or +1 (network
+// rows: netdes's flow balances and the y side of its capacity rows), the chosen variant's unit twin
+// keeps the whole matrix in LDS as 16-bit entry codes plus the scenario's varying entry rows.  Needs
+// the twin's LDS to fit and n, m < 32 767.  PHG_UNIT=0: never (A/B runs).
+static int build_unit_codes(phg_handle* h, const double* rv, const double* cv) {
+    BlockLayout& L = h->blk;
+    const char* eu = std::getenv("PHG_UNIT");
+    if ((eu && std::atoi(eu) == 0) || h->n >= 32767 || h->m >= 32767) return 0;
+    int twin = -1, sh[11];
+    for (int v = 0; v < pdhg_block_num_variants() && twin < 0; ++v) {
+        pdhg_block_variant_shape(v, sh);
+        if (sh[10] && std::equal(sh, sh + 10, h->bshape)) twin = v;
+    }
+    if (twin < 0 || pdhg_block_lds_bytes(twin, L.n_pad, L.m_pad, L.nd_r + L.nd_c, L.er + L.ec) > 160 * 1024) return 0;
+    const int NT = h->bshape[0];
+    auto codes = [&](const double* dv, const int* didx, int E, const int* drow, std::vector<short>& out) {
+        std::vector<double> val(E);
+        std::vector<int> idx(E);
+        if (hipMemcpy(val.data(), dv, (size_t)E * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(idx.data(), didx, (size_t)E * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+        out.assign(std::max(1, E), 0);
+        for (int e = 0; e < E; ++e) {
+            const int c = idx[e] + 1;
+            if (drow[e / NT] >= 0) { out[e] = (short)c; continue; }   // varying row: its value from rvd / cvd
+            if (val[e] == 1.0) out[e] = (short)c;
+            else if (val[e] == -1.0) out[e] = (short)-c;
+            else if (val[e] == 0.0 && !std::signbit(val[e])) out[e] = 0;
+            else return 1;   // a constant entry that is not a unit
+        }
+        return 0;
+    };
+    CK(hipStreamSynchronize(h->stream));   // the piece gathers wrote rv / cv
+    std::vector<short> rc, cc;
+    int r = codes(rv, L.ridx, L.er, L.rdrow, rc);
+    if (r == 0) r = codes(cv, L.cidx, L.ec, L.cdrow, cc);
+    if (r < 0) return fail("phg_load_batch: reading the piece values back failed");
+    if (r > 0) return 0;
+    short* p;
+    if (dput(h, &p, rc.data(), rc.size())) return -1; L.rcode = p;
+    if (dput(h, &p, cc.data(), cc.size())) return -1; L.ccode = p;
+    h->block_variant = twin;
+    pdhg_block_variant_shape(twin, h->bshape);
+    return 0;
+}
+
 // piece-major copies of the (preconditioned) values; one copy when every scenario has the same A
 static int build_block_values(phg_handle* h, const double* raw) {
     BlockLayout& L = h->blk;
@@ -1204,7 +1251,11 @@ static int build_block_values(phg_handle* h, const double* raw) {
     };
     if (deltas(h->block_rperm, Er, L.rdrow, &L.rvd, &L.dstride_r)) return -1;
     if (deltas(h->block_cperm, Ec, L.cdrow, &L.cvd, &L.dstride_c)) return -1;
-    return 0;
+    L.nd_r = (int)(L.dstride_r / NT);
+    L.nd_c = (int)(L.dstride_c / NT);
+    L.er = Er;
+    L.ec = Ec;
+    return h->delta_scale ? build_unit_codes(h, rv, cv) : 0;
 }
 
 // Shared-matrix MFMA layout (pdhg_mfma.hip).  Planner: the smallest tile grid (16 TM rows x 16 TN
@@ -2113,7 +2164,7 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
 int phg_values_info(phg_handle* h, int32_t* o) {
     if (!h || !h->loaded || !o) return fail("phg_values_info: no batch loaded");
     o[0] = h->n_vary;
-    o[1] = h->delta_scale ? 1 : 0;
+    o[1] = h->delta_scale ? (h->bshape[10] ? 2 : 1) : 0;
     o[2] = o[3] = 0;
     if (h->block_variant >= 0) {
         const long E = (long)h->block_rperm.size() + (long)h->block_cperm.size();

@@ -201,12 +201,13 @@ class Engine:
 
     def values_info(self):
         """Value form of the loaded batch (phg_values_info): positions varying between scenarios,
-        whether the shared-scaling delta form is in use, and the matrix values one A x + A^T y of
+        whether the shared-scaling delta form is in use (and its unit form: the matrix held in LDS as
+        +-1 entry codes), and the matrix values one A x + A^T y of
         the workgroup kernel reads per scenario / from the one shared copy."""
         out = np.zeros(4, np.int32)
         _lib.check(self.lib.phg_values_info(self.h, ptr(out)))
-        return {"varying": int(out[0]), "delta": bool(out[1]), "per_scenario_vals": int(out[2]),
-                "shared_vals": int(out[3])}
+        return {"varying": int(out[0]), "delta": bool(out[1]), "unit": int(out[1]) == 2,
+                "per_scenario_vals": int(out[2]), "shared_vals": int(out[3])}
 
     def mfma_fragments(self):
         """MFMA instructions per PDHG iteration per 16 scenarios (nonzero 16x4 fragments of A x and

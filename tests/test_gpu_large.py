@@ -90,7 +90,8 @@ def test_netdes_delta_values(monkeypatch):
     the per-scenario [S*nnz] form and the sparse delta list load the same device data (same bits),
     with ONE scaling for all scenarios so the kernel streams per scenario only the piece-entry rows
     holding a u_e; PHG_DELTA=0 (per-scenario scaling and copies) reaches the same prox-QP solutions
-    (1e-6) with a different preconditioner.  Both against the oracle's certified QPs (1e-5 / 1e-6)."""
+    (1e-6) with a different preconditioner; the unit form (constant entries +-1 held in LDS as entry
+    codes) returns the delta form's bits.  Both against the oracle's certified QPs (1e-5 / 1e-6)."""
     S = 40
     kw = {"num_scens": S}
     o = oph.OraclePH(_opts(), om.netdes_names(S)[:4], om.netdes, {"num_scens": 4})
@@ -98,8 +99,10 @@ def test_netdes_delta_values(monkeypatch):
     o.Compute_Xbar()
     o.Update_W()
     res = {}
-    for tag, form, env in (("dense", 0, "1"), ("delta", 2, "1"), ("off", 0, "0")):
+    for tag, form, env, unit in (("dense", 0, "1", "1"), ("delta", 2, "1", "1"), ("vs", 2, "1", "0"),
+                                 ("off", 0, "0", "1")):
         monkeypatch.setenv("PHG_DELTA", env)
+        monkeypatch.setenv("PHG_UNIT", unit)
         ph = PH(_opts(pdhg_vals_form=form), netdes.scenario_names_creator(S), netdes.scenario_creator,
                 scenario_creator_kwargs=kw)
         ph.PH_Prep()
@@ -109,6 +112,8 @@ def test_netdes_delta_values(monkeypatch):
         if env == "1":
             # two entry rows of 1024 per product: the x_e column pieces and the vub row pieces
             assert vi["delta"] and 0 < vi["per_scenario_vals"] <= 4 * 1024 and vi["shared_vals"] > 0, vi
+            # netdes's constant entries are all +-1: the unit form (matrix in LDS) unless PHG_UNIT=0
+            assert vi["unit"] == (unit == "1"), vi
         else:
             assert not vi["delta"] and vi["per_scenario_vals"] >= 2 * 5880, vi
         ph.Iter0()
@@ -121,6 +126,9 @@ def test_netdes_delta_values(monkeypatch):
         assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
         res[tag] = (ob0, ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get_i32(_lib.I_ITERS).copy(), ph.nonants())
     for a, b in zip(res["dense"], res["delta"]):
+        np.testing.assert_array_equal(a, b)
+    # the unit form adds / subtracts where the delta form fma's +-1: the same bits
+    for a, b in zip(res["delta"], res["vs"]):
         np.testing.assert_array_equal(a, b)
     a, b = res["dense"], res["off"]
     np.testing.assert_allclose(a[0], b[0], rtol=1e-6)
