@@ -108,8 +108,9 @@ typedef struct phg_opts {
     double  beta_necessary;    /* default 0.8  */
     double  beta_artificial;   /* default 0.25 (tuned on PH prox-QPs; PDLP uses 0.36) */
     /* primal weight smoothing at restarts, omega <- (dy/dx)^theta omega^(1-theta);
-     * (0, 1], <= 0 selects the default 0.8 (PDLP uses 0.5; 0.8 measured on MI355X: farmer
-     * 10k +10 %, sslp 2048 +16 %, netdes 1024 -1 % solves/s)                                 */
+     * (0, 1], <= 0 selects the default by subproblem size n (after presolve): 0.8 for
+     * n < 2 000, 0.5 for n < 10 000, 0.05 above (PDLP uses 0.5; measured on MI355X, round 3:
+     * farmer 0.8 best, netdes 0.5 +8-11 % over 0.8, UC 0.05 7.8x fewer ms per PH iteration)   */
     double  primal_weight_theta;
     /* > 0: the solve is a device-side no-op when the convergence metric of the handle's last
      * phg_conv_start is below this value (PH's "conv < convthresh: stop before solve_loop",

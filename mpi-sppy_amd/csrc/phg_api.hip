@@ -1196,6 +1196,22 @@ static int build_unit_codes(phg_handle* h, const double* rv, const double* cv) {
     return 0;
 }
 
+// Default primal-weight smoothing theta (omega <- r^theta omega^(1 - theta) at a restart, r the
+// restart's ||dy|| / ||dx||) by subproblem size, measured per PH iteration on MI355X (DESIGN.md,
+// round 3): farmer (n 120) 0.8 best (0.5: -2 %, 0.3: -12 %); sslp (705) 0.6-0.8; hydro 0.6 by 4 %;
+// netdes (2 940) 0.5 by 8-11 %; UC (20 400) 0.05: 83 vs 641 ms per PH iteration (PH iterations
+// 1-8 at 64 scenarios; mean PDHG iterations per solve 930 vs 13 609, the slowest 12 892 vs 58 968).
+// PHG_THETA overrides it (A/B runs).
+static double theta_default(int n) {
+    static const double env = [] {
+        const char* e = std::getenv("PHG_THETA");
+        const double v = e ? std::atof(e) : 0.0;
+        return v > 0.0 && v <= 1.0 ? v : 0.0;
+    }();
+    if (env > 0.0) return env;
+    return n >= 10000 ? 0.05 : (n >= 2000 ? 0.5 : 0.8);
+}
+
 // piece-major copies of the (preconditioned) values; one copy when every scenario has the same A
 static int build_block_values(phg_handle* h, const double* raw) {
     BlockLayout& L = h->blk;
@@ -2317,7 +2333,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.beta_suf = o->beta_sufficient > 0 ? o->beta_sufficient : 0.2;
     a.beta_nec = o->beta_necessary > 0 ? o->beta_necessary : 0.8;
     a.beta_art = o->beta_artificial > 0 ? o->beta_artificial : 0.25;
-    a.theta = o->primal_weight_theta > 0 && o->primal_weight_theta <= 1 ? o->primal_weight_theta : 0.8;
+    a.theta = o->primal_weight_theta > 0 && o->primal_weight_theta <= 1 ? o->primal_weight_theta : theta_default(h->n);
     if (h->local_variant >= 0 || h->mfma_variant >= 0) a.check_every = (a.check_every + 1) & ~1;   // 2 iterations per trip
     if (timing_event(h, 0, 0)) return -1;
     a.loc = h->loc;
