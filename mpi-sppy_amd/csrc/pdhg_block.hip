@@ -82,10 +82,18 @@ __device__ __forceinline__ double piece_sum8(const double* p, int cnt) {
 // UN: the unit form (BlockLayout::rcode) -- VS with every constant entry +-1: the entry codes and the
 // scenario's varying entry rows sit in LDS, an entry adds or subtracts its x (y) or, on a varying
 // row, fma's its value; acc + v / acc - v are fma(+-1, v, acc) exactly, so the bits equal VS's.
+//
+// SEG: the row-segment form (BlockLayout built by build_block_layout's segment planner) -- every row's
+// pieces sit in an aligned segment of 1, 2, 4 or 8 consecutive lanes of one wave (row_pcnt = the
+// segment length, the row owned by the segment's first lane), so a row sum is a DPP butterfly over
+// its segment inside the wave: no partials in LDS and no workgroup barrier between the pieces and
+// the row owners -- two barriers per PDHG iteration instead of three.  The segment sums add the
+// pieces pairwise ((p0 + p1) + (p2 + p3)) + ..., a different order from the sequential piece_sum.
 template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL, bool VS, bool PS = false,
-          bool UN = false>
+          bool UN = false, bool SEG = false>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     static_assert(!CL || QPT == CPL, "column-local A^T y needs one piece slot per column slot");
+    static_assert(!SEG || (PPT == 1 && RPL == 1 && RE > 0 && !VS), "row segments: one register piece, one row per lane");
     static_assert(!UN || (VS && RE == 0 && CE == 0), "the unit form is a streaming delta-form variant");
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -242,13 +250,24 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
                 }
                 off += kk * NT;
             }
-            rp[ps * NT + t] = acc;
+            if constexpr (SEG) {
+                // the segment's sum in its first lane: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror
+                const double v1 = acc + dpp_d<0xB1>(acc);
+                const double v2 = v1 + dpp_d<0x4E>(v1);
+                const double v3 = v2 + dpp_d<0x141>(v2);
+                const int L = rn[0];
+                out[0] = L >= 8 ? v3 : (L >= 4 ? v2 : (L >= 2 ? v1 : acc));
+            } else {
+                rp[ps * NT + t] = acc;
+            }
         }
-        __syncthreads();
+        if constexpr (!SEG) {
+            __syncthreads();
 #pragma unroll
-        for (int r = 0; r < RPL; ++r) {
-            const double t_ = PS ? piece_sum8(rp + rf[r], rn[r]) : piece_sum(rp + rf[r], rn[r]);
-            out[r] = VS ? t_ * drs[r] : t_;
+            for (int r = 0; r < RPL; ++r) {
+                const double t_ = PS ? piece_sum8(rp + rf[r], rn[r]) : piece_sum(rp + rf[r], rn[r]);
+                out[r] = VS ? t_ * drs[r] : t_;
+            }
         }
     };
     // A^T y for the y currently in yl
@@ -541,23 +560,26 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 
 // ----------------------------------------------------------------------------- dispatch
 struct BlockVariant {
-    int NT, CPL, RPL, PPT, QPT, RE, CE, CL, VS, PS, UN;
+    int NT, CPL, RPL, PPT, QPT, RE, CE, CL, VS, PS, UN, SEG;
     void (*fn)(PdhgArgs);
 };
 
-#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, false>}
-#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, false>}
-#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false>}
+#define PHG_B(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, false>}
+#define PHG_BC(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, false>}
+#define PHG_BR(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false>}
 // row piece sums with their loads issued together (default; PHG_PSUM=0 skips them, A/B)
-#define PHG_BRP(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, true>}
+#define PHG_BRP(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 1, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, true>}
 // the delta value form (unscaled shared pieces, scaling on the fly)
-#define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
-#define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
+#define PHG_BV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true>}
+#define PHG_BCV(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 0, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true>}
 // the unit form of the delta value form (BlockLayout::rcode): chosen at value time, not by the planner
-#define PHG_BCVU(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true, false, true>}
-#define PHG_BVU(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true, false, true>}
+#define PHG_BCVU(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true, false, true>}
+#define PHG_BVU(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true, false, true>}
+// row segments (sslp-like: rows of <= 8 pieces, one piece per thread; PHG_BLOCK_SEG=0 skips them)
+#define PHG_BRS(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, false, false, true>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
+    PHG_BRS(256, 3, 1, 1, 3, 8, 2, true),   // sslp: 180 row pieces in 15 8-lane + 45 2-lane segments
     PHG_BRP(256, 3, 1, 2, 3, 8, 2, true),   // sslp: ... row piece sums' loads issued together (PHG_PSUM=0: not)
     PHG_BR(256, 3, 1, 2, 3, 8, 2, true),    // sslp-like: register-resident pieces, column-local A^T y
     PHG_BR(256, 3, 1, 2, 3, 8, 2, false),   // the same with A^T y through LDS partials
@@ -591,18 +613,20 @@ static const BlockVariant kBlockVariants[] = {
 #undef PHG_BCV
 #undef PHG_BRP
 #undef PHG_BCVU
+#undef PHG_BRS
 #undef PHG_BVU
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }
 
-void pdhg_block_variant_shape(int v, int* out11) {
-    int* out9 = out11;
+void pdhg_block_variant_shape(int v, int* out12) {
+    int* out9 = out12;
     const BlockVariant& V = kBlockVariants[v];
     out9[0] = V.NT; out9[1] = V.CPL; out9[2] = V.RPL; out9[3] = V.PPT; out9[4] = V.QPT; out9[5] = V.RE; out9[6] = V.CE;
     out9[7] = V.CL;
     out9[8] = V.VS;
     out9[9] = V.PS;
     out9[10] = V.UN;
+    out9[11] = V.SEG;
 }
 
 // UN variants add the varying entry rows (nd doubles per thread) and the er + ec 16-bit codes

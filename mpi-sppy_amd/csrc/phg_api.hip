@@ -33,7 +33,7 @@ int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long b
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_block_num_variants();
-void pdhg_block_variant_shape(int v, int* out11);
+void pdhg_block_variant_shape(int v, int* out12);
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad, int nd, int ecodes);
 hipError_t pdhg_block_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream);
@@ -122,7 +122,7 @@ struct phg_handle {
     std::vector<int> stream_cperm;   // CSC entry -> CSR position (values gathered after prep)
     int mshape[2] = {0, 0};
     MfmaLayout mf{};
-    int bshape[11] = {0};
+    int bshape[12] = {0};
     std::vector<int> block_rperm, block_cperm;   // piece layout -> CSR position (host copies)
     bool vals_shared = false;
     // delta value form (phg_batch.vals_form): vary[p] = CSR position p differs between scenarios;
@@ -977,10 +977,29 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     // iteration, the same bits); PHG_PSUM=0 skips them (A/B)
     const char* eps_ = std::getenv("PHG_PSUM");
     const bool psum = !(eps_ && std::atoi(eps_) == 0);
-    int sh[11], chosen = -1;
+    // row segments (SEG variants): every row's pieces in an aligned 1 / 2 / 4 / 8-lane segment, rows
+    // placed longest segment first (which keeps every segment aligned); seg_len[i], seg_lane[i]
+    const char* esg = std::getenv("PHG_BLOCK_SEG");
+    const bool seg_off = esg && std::atoi(esg) == 0;
+    std::vector<int> seg_len(m), seg_lane(m);
+    int seg_lanes = 0;
+    bool seg_ok = m > 0;
+    for (int i = 0; i < m && seg_ok; ++i) {
+        const int c = rpc[i];
+        if (c > 8) seg_ok = false;
+        seg_len[i] = c <= 1 ? 1 : (c <= 2 ? 2 : (c <= 4 ? 4 : 8));
+    }
+    if (seg_ok) {
+        std::vector<int> ord(m);
+        for (int i = 0; i < m; ++i) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](int u, int v) { return seg_len[u] > seg_len[v]; });
+        for (int i : ord) { seg_lane[i] = seg_lanes; seg_lanes += seg_len[i]; }
+    }
+    int sh[12], chosen = -1;
     for (int v = 0; v < pdhg_block_num_variants(); ++v) {
         pdhg_block_variant_shape(v, sh);
         if (sh[10]) continue;   // unit twins: chosen by build_block_values
+        if (sh[11] && (seg_off || !seg_ok || seg_lanes > sh[0] || m > sh[0])) continue;
         if ((sh[9] != 0) != psum && sh[9] != 0) continue;
         const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4], RE = sh[5], CE = sh[6], CL = sh[7];
         if ((sh[8] != 0) != want_delta) continue;   // delta form: the on-the-fly scaling variants
@@ -1011,9 +1030,22 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
         col_of[idx] = j; colf[idx] = cpf[j]; colc[idx] = cpc[j];
     }
     std::vector<int> row_of(RPL * NT, -1), rowf(RPL * NT, 0), rowc(RPL * NT, 0);
-    for (int i = 0; i < m; ++i) {
-        const int idx = (i / NT) * NT + i % NT;
-        row_of[idx] = i; rowf[idx] = rpf[i]; rowc[idx] = rpc[i];
+    if (sh[11]) {
+        // row segments: the row's owner is its segment's first lane (row_pcnt = segment length), its
+        // pieces the segment's lanes; the piece list in lane order, empty pieces on the padding lanes
+        std::vector<int> lps(NT, 0), lpl(NT, 0);
+        for (int i = 0; i < m; ++i) {
+            const int l0 = seg_lane[i];
+            row_of[l0] = i; rowf[l0] = l0; rowc[l0] = seg_len[i];
+            for (int q = 0; q < rpc[i]; ++q) { lps[l0 + q] = rps[rpf[i] + q]; lpl[l0 + q] = rpl[rpf[i] + q]; }
+        }
+        rps.swap(lps);
+        rpl.swap(lpl);
+    } else {
+        for (int i = 0; i < m; ++i) {
+            const int idx = (i / NT) * NT + i % NT;
+            row_of[idx] = i; rowf[idx] = rpf[i]; rowc[idx] = rpc[i];
+        }
     }
     // piece-major entry layout
     auto lay = [&](const std::vector<int>& ps, const std::vector<int>& pl, int SLOTS, int* kk,
@@ -1158,10 +1190,10 @@ static int build_unit_codes(phg_handle* h, const double* rv, const double* cv) {
     BlockLayout& L = h->blk;
     const char* eu = std::getenv("PHG_UNIT");
     if ((eu && std::atoi(eu) == 0) || h->n >= 32767 || h->m >= 32767) return 0;
-    int twin = -1, sh[11];
+    int twin = -1, sh[12];
     for (int v = 0; v < pdhg_block_num_variants() && twin < 0; ++v) {
         pdhg_block_variant_shape(v, sh);
-        if (sh[10] && std::equal(sh, sh + 10, h->bshape)) twin = v;
+        if (sh[10] && std::equal(sh, sh + 10, h->bshape) && sh[11] == h->bshape[11]) twin = v;
     }
     if (twin < 0 || pdhg_block_lds_bytes(twin, L.n_pad, L.m_pad, L.nd_r + L.nd_c, L.er + L.ec) > 160 * 1024) return 0;
     const int NT = h->bshape[0];
