@@ -83,17 +83,18 @@ __device__ __forceinline__ double piece_sum8(const double* p, int cnt) {
 // scenario's varying entry rows sit in LDS, an entry adds or subtracts its x (y) or, on a varying
 // row, fma's its value; acc + v / acc - v are fma(+-1, v, acc) exactly, so the bits equal VS's.
 //
-// SEG: the row-segment form (BlockLayout built by build_block_layout's segment planner) -- every row's
-// pieces sit in an aligned segment of 1, 2, 4 or 8 consecutive lanes of one wave (row_pcnt = the
-// segment length, the row owned by the segment's first lane), so a row sum is a DPP butterfly over
-// its segment inside the wave: no partials in LDS and no workgroup barrier between the pieces and
-// the row owners -- two barriers per PDHG iteration instead of three.  The segment sums add the
-// pieces pairwise ((p0 + p1) + (p2 + p3)) + ..., a different order from the sequential piece_sum.
+// SEG = 8 / 16: the row-segment form (BlockLayout built by build_block_layout's segment planner) --
+// every row's pieces sit in an aligned segment of 1, 2, 4, 8 (or 16) consecutive lanes of one wave,
+// in the piece slot of the row's own slot (PPT == RPL; row_pcnt = the segment length, the row owned
+// by the segment's first lane), so a row sum is a DPP butterfly over its segment inside the wave: no
+// partials in LDS and no workgroup barrier between the pieces and the row owners -- two barriers per
+// PDHG iteration instead of three.  The segment sums add the pieces pairwise ((p0 + p1) + (p2 +
+// p3)) + ..., a different order from the sequential piece_sum.
 template <int NT, int CPL, int RPL, int PPT, int QPT, int RE, int CE, bool CL, bool VS, bool PS = false,
-          bool UN = false, bool SEG = false>
+          bool UN = false, int SEG = 0>
 __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     static_assert(!CL || QPT == CPL, "column-local A^T y needs one piece slot per column slot");
-    static_assert(!SEG || (PPT == 1 && RPL == 1 && RE > 0 && !VS), "row segments: one register piece, one row per lane");
+    static_assert(SEG == 0 || ((SEG == 8 || SEG == 16) && PPT == RPL), "row segments: piece slot r holds row slot r's rows");
     static_assert(!UN || (VS && RE == 0 && CE == 0), "the unit form is a streaming delta-form variant");
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -250,18 +251,24 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
                 }
                 off += kk * NT;
             }
-            if constexpr (SEG) {
-                // the segment's sum in its first lane: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror
+            if constexpr (SEG > 0) {
+                // the segment's sum in its first lane: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+                // row_mirror (every lane of an aligned group ends with the same bits: a + b = b + a)
                 const double v1 = acc + dpp_d<0xB1>(acc);
                 const double v2 = v1 + dpp_d<0x4E>(v1);
                 const double v3 = v2 + dpp_d<0x141>(v2);
-                const int L = rn[0];
-                out[0] = L >= 8 ? v3 : (L >= 4 ? v2 : (L >= 2 ? v1 : acc));
+                const int L = rn[ps];
+                double t_ = L >= 8 ? v3 : (L >= 4 ? v2 : (L >= 2 ? v1 : acc));
+                if constexpr (SEG == 16) {
+                    const double v4 = v3 + dpp_d<0x140>(v3);
+                    t_ = L >= 16 ? v4 : t_;
+                }
+                out[ps] = VS ? t_ * drs[ps] : t_;
             } else {
                 rp[ps * NT + t] = acc;
             }
         }
-        if constexpr (!SEG) {
+        if constexpr (SEG == 0) {
             __syncthreads();
 #pragma unroll
             for (int r = 0; r < RPL; ++r) {
@@ -575,8 +582,10 @@ struct BlockVariant {
 // the unit form of the delta value form (BlockLayout::rcode): chosen at value time, not by the planner
 #define PHG_BCVU(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true, false, true>}
 #define PHG_BVU(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 0, 1, 0, 1, 0, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, false, true, false, true>}
-// row segments (sslp-like: rows of <= 8 pieces, one piece per thread; PHG_BLOCK_SEG=0 skips them)
-#define PHG_BRS(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, 0, 1, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, false, false, true>}
+// row segments of <= SEG lanes (rows of <= 8 / 16 pieces; PHG_BLOCK_SEG=0 skips them)
+#define PHG_BRS(a_, b_, c_, d_, e_, f_, g_, h_) {a_, b_, c_, d_, e_, f_, g_, h_, 0, 0, 0, 8, pdhg_block_kernel<a_, b_, c_, d_, e_, f_, g_, h_, false, false, false, 8>}
+#define PHG_BCVS(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 0, 16, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true, false, false, 16>}
+#define PHG_BCVUS(a_, b_, c_, d_, e_) {a_, b_, c_, d_, e_, 0, 0, 1, 1, 0, 1, 16, pdhg_block_kernel<a_, b_, c_, d_, e_, 0, 0, true, true, false, true, 16>}
 // preference order: smallest workgroup that holds the problem
 static const BlockVariant kBlockVariants[] = {
     PHG_BRS(256, 3, 1, 1, 3, 8, 2, true),   // sslp: 180 row pieces in 15 8-lane + 45 2-lane segments
@@ -593,6 +602,7 @@ static const BlockVariant kBlockVariants[] = {
     PHG_BV(256, 3, 1, 2, 3),
     PHG_BV(256, 4, 4, 4, 4),
     PHG_BV(512, 4, 4, 4, 4),
+    PHG_BCVS(1024, 3, 2, 2, 3),  // netdes: rows in lane segments (<= 16 lanes; 1 910 of 2 048)
     PHG_BCV(1024, 3, 2, 3, 3),   // netdes (only the vubs' u_e vary).  (Its row piece sums with the
                                  // loads issued together, PHG_BCVP: 58.0 vs 42.0 ms per PH iteration
                                  // at 1 024 -- 372 B/lane of spills at 128 VGPRs -- not kept)
@@ -603,6 +613,7 @@ static const BlockVariant kBlockVariants[] = {
     PHG_BVU(256, 4, 4, 4, 4),
     PHG_BVU(512, 4, 4, 4, 4),
     PHG_BCVU(1024, 3, 2, 3, 3),
+    PHG_BCVUS(1024, 3, 2, 2, 3),
     PHG_BVU(1024, 3, 2, 3, 3),
     PHG_BVU(1024, 4, 4, 4, 4),
 };
@@ -614,6 +625,8 @@ static const BlockVariant kBlockVariants[] = {
 #undef PHG_BRP
 #undef PHG_BCVU
 #undef PHG_BRS
+#undef PHG_BCVS
+#undef PHG_BCVUS
 #undef PHG_BVU
 
 int pdhg_block_num_variants() { return (int)(sizeof(kBlockVariants) / sizeof(kBlockVariants[0])); }

@@ -977,33 +977,39 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     // iteration, the same bits); PHG_PSUM=0 skips them (A/B)
     const char* eps_ = std::getenv("PHG_PSUM");
     const bool psum = !(eps_ && std::atoi(eps_) == 0);
-    // row segments (SEG variants): every row's pieces in an aligned 1 / 2 / 4 / 8-lane segment, rows
-    // placed longest segment first (which keeps every segment aligned); seg_len[i], seg_lane[i]
+    // row segments (SEG variants): every row's pieces in an aligned 1 / 2 / 4 / 8 / 16-lane segment of
+    // one row slot, rows placed longest segment first, a slot filled before the next (which keeps
+    // every segment aligned); seg_len[i], seg_pos[i] = slot * NT + lane.  Returns the slots used
+    // (NT lanes each), or a large number when a row does not fit.
     const char* esg = std::getenv("PHG_BLOCK_SEG");
     const bool seg_off = esg && std::atoi(esg) == 0;
-    std::vector<int> seg_len(m), seg_lane(m);
-    int seg_lanes = 0;
-    bool seg_ok = m > 0;
-    for (int i = 0; i < m && seg_ok; ++i) {
-        const int c = rpc[i];
-        if (c > 8) seg_ok = false;
-        seg_len[i] = c <= 1 ? 1 : (c <= 2 ? 2 : (c <= 4 ? 4 : 8));
-    }
-    if (seg_ok) {
+    std::vector<int> seg_len(m), seg_pos(m);
+    auto seg_plan = [&](int NT_, int maxlen) {
+        for (int i = 0; i < m; ++i) {
+            const int c = rpc[i];
+            if (c > maxlen) return 1 << 20;
+            seg_len[i] = c <= 1 ? 1 : (c <= 2 ? 2 : (c <= 4 ? 4 : (c <= 8 ? 8 : 16)));
+        }
         std::vector<int> ord(m);
         for (int i = 0; i < m; ++i) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](int u, int v) { return seg_len[u] > seg_len[v]; });
-        for (int i : ord) { seg_lane[i] = seg_lanes; seg_lanes += seg_len[i]; }
-    }
+        int slot = 0, lane = 0;
+        for (int i : ord) {
+            if (lane + seg_len[i] > NT_) { ++slot; lane = 0; }
+            seg_pos[i] = slot * NT_ + lane;
+            lane += seg_len[i];
+        }
+        return m > 0 ? slot + 1 : 1 << 20;
+    };
     int sh[12], chosen = -1;
     for (int v = 0; v < pdhg_block_num_variants(); ++v) {
         pdhg_block_variant_shape(v, sh);
         if (sh[10]) continue;   // unit twins: chosen by build_block_values
-        if (sh[11] && (seg_off || !seg_ok || seg_lanes > sh[0] || m > sh[0])) continue;
+        if (sh[11] && (seg_off || seg_plan(sh[0], sh[11] / 1) > sh[2])) continue;
         if ((sh[9] != 0) != psum && sh[9] != 0) continue;
         const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4], RE = sh[5], CE = sh[6], CL = sh[7];
         if ((sh[8] != 0) != want_delta) continue;   // delta form: the on-the-fly scaling variants
-        if (n > CPL * NT || m > RPL * NT || (int)rps.size() > PPT * NT || (int)cps.size() > QPT * NT) continue;
+        if (n > CPL * NT || m > RPL * NT || (!sh[11] && (int)rps.size() > PPT * NT) || (int)cps.size() > QPT * NT) continue;
         if (RE > 0 && (stream_only || rlen > RE || clen > CE)) continue;   // pieces must fit the registers
         if (CL && (!col_one_piece || cl_off)) continue;
         if (pdhg_block_lds_bytes(v, n_pad, m_pad, 0, 0) > 160 * 1024) continue;
@@ -1032,10 +1038,12 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
     std::vector<int> row_of(RPL * NT, -1), rowf(RPL * NT, 0), rowc(RPL * NT, 0);
     if (sh[11]) {
         // row segments: the row's owner is its segment's first lane (row_pcnt = segment length), its
-        // pieces the segment's lanes; the piece list in lane order, empty pieces on the padding lanes
-        std::vector<int> lps(NT, 0), lpl(NT, 0);
+        // pieces the segment's lanes of the same slot; the piece list in slot-lane order, empty
+        // pieces on the padding lanes
+        seg_plan(NT, sh[11]);
+        std::vector<int> lps((size_t)RPL * NT, 0), lpl((size_t)RPL * NT, 0);
         for (int i = 0; i < m; ++i) {
-            const int l0 = seg_lane[i];
+            const int l0 = seg_pos[i];
             row_of[l0] = i; rowf[l0] = l0; rowc[l0] = seg_len[i];
             for (int q = 0; q < rpc[i]; ++q) { lps[l0 + q] = rps[rpf[i] + q]; lpl[l0 + q] = rpl[rpf[i] + q]; }
         }

@@ -151,6 +151,7 @@ def test_border_matches_block_kernel(monkeypatch):
     per-scenario scaling the bordered kernel uses (PHG_DELTA=0: the derates vary a few entries, which
     would otherwise put the block kernel on the shared-scaling delta form)."""
     monkeypatch.setenv("PHG_DELTA", "0")
+    monkeypatch.setenv("PHG_BLOCK_SEG", "0")   # (row segments sum the pieces in another order)
     kw = {"num_gens": 24, "num_periods": 12, "num_scens": 3}
     o = oph.OraclePH(_opts(), om.uc_names(3), om.uc, kw)
     o.Iter0()
