@@ -550,7 +550,14 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
 
     bool valid = true, live = false;   // valid: the group may still receive work
     const int chk = a.check_every;
+    // PdhgArgs::prof: cycles in the PDHG iterations, in the checks, in loads (uniform per wave)
+    unsigned long long pf_it = 0, pf_chk = 0, pf_load = 0, pf_n = 0, pf_t1 = 0, pf_kkt = 0;
     for (;;) {
+        unsigned long long pf_t0 = 0;
+        if (a.prof) {
+            pf_t0 = clock64();
+            if (pf_t1) pf_chk += pf_t0 - pf_t1;
+        }
         const bool need = valid && !live;
         if (wave_any(need)) {
             if (need) {
@@ -562,6 +569,11 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                     valid = false;
                 }
             }
+        }
+        if (a.prof) {
+            const unsigned long long now = clock64();
+            pf_load += now - pf_t0;
+            pf_t0 = now;
         }
         if (!wave_any(live)) break;
         // two PDHG iterations per trip (check_every is even): the A x / A x+ hand-over is a
@@ -659,6 +671,11 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         it += chk;
         since += chk;
         cnt += a.sum_stride == 2 ? chk / 2 : (win && !win_block ? 0 : chk);
+        if (a.prof) {
+            pf_t1 = clock64();
+            pf_it += pf_t1 - pf_t0;
+            ++pf_n;
+        }
 
         // ---------------------------------------------------------- restart / termination check
         const double inv = 1.0 / (double)cnt;
@@ -669,6 +686,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         const bool avg = wave_any(live && (a.avg_every <= 1 || ((it / chk) % a.avg_every) == 0));
         if constexpr (FOLDT) mv_aty(y, yd, aty);   // not formed in the iterations
         kkt_both(avg, inv, oc, oa);
+        if (a.prof) pf_kkt += clock64() - pf_t1;
         if (!avg)
 #pragma unroll
             for (int u = 0; u < 6; ++u) oa[u] = u == 4 ? INFINITY : (u == 5 ? -INFINITY : INFINITY);
@@ -737,6 +755,10 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                 since = 0;
             }
         }
+    }
+    if (a.prof && lane < 4) {   // (lane-indexed: a vector store)
+        const unsigned long long v = lane == 0 ? pf_it : (lane == 1 ? pf_chk : (lane == 2 ? pf_load : pf_kkt));
+        a.prof[(size_t)blockIdx.x * 4 + lane] = v;
     }
     if constexpr (PERSIST) {
         // the last wave out re-arms the queue for the next (stream-ordered) launch: every wave

@@ -2404,7 +2404,31 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     if (h->border_layout) CK(pdhg_border_launch(a, h->stream));
     else if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));
     else if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
-    else if (h->local_variant >= 0) CK(pdhg_local_launch(h->local_variant, a, h->stream));
+    else if (h->local_variant >= 0) {
+        // PHG_LOCAL_PROF=1 (diagnostic): per-wave cycle split of the lane-local kernel, summed over
+        // the waves and printed to stderr after every launch (synchronises the stream)
+        static const bool lprof = [] { const char* e = std::getenv("PHG_LOCAL_PROF"); return e && std::atoi(e); }();
+        static unsigned long long* pbuf = nullptr;
+        static size_t pcap = 0;
+        const size_t waves = (size_t)a.S;   // >= the grid (G scenarios per wave)
+        if (lprof && pcap < waves * 4) {
+            if (pbuf) CK(hipFree(pbuf));
+            CK(hipMalloc((void**)&pbuf, waves * 4 * sizeof(unsigned long long)));
+            pcap = waves * 4;
+        }
+        if (lprof) CK(hipMemsetAsync(pbuf, 0, pcap * sizeof(unsigned long long), h->stream));
+        a.prof = lprof ? pbuf : nullptr;
+        CK(pdhg_local_launch(h->local_variant, a, h->stream));
+        if (lprof) {
+            std::vector<unsigned long long> hb(pcap);
+            CK(hipMemcpyAsync(hb.data(), pbuf, pcap * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+            CK(hipStreamSynchronize(h->stream));
+            double t[4] = {0, 0, 0, 0};
+            for (size_t i = 0; i < pcap; ++i) t[i % 4] += (double)hb[i];
+            fprintf(stderr, "PHG_LOCAL_PROF iter_cycles %.6e check_cycles %.6e load_cycles %.6e kkt_cycles %.6e\n", t[0], t[1],
+                    t[2], t[3]);
+        }
+    }
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
     else if (h->wave_variant >= 0) CK(pdhg_wave_launch(h->wave_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
