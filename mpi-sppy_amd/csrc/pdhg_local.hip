@@ -550,8 +550,9 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
 
     bool valid = true, live = false;   // valid: the group may still receive work
     const int chk = a.check_every;
-    // PdhgArgs::prof: cycles in the PDHG iterations, in the checks, in loads (uniform per wave)
-    unsigned long long pf_it = 0, pf_chk = 0, pf_load = 0, pf_n = 0, pf_t1 = 0, pf_kkt = 0;
+    // PdhgArgs::prof: cycles in the PDHG iterations, in the checks (of which the KKT part and the
+    // restart block), in loads; checks (uniform per wave)
+    unsigned long long pf_it = 0, pf_chk = 0, pf_load = 0, pf_n = 0, pf_t1 = 0, pf_kkt = 0, pf_rst = 0;
     for (;;) {
         unsigned long long pf_t0 = 0;
         if (a.prof) {
@@ -711,6 +712,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                                       (cand <= a.beta_nec * a.beta_nec * krst && cand > GS(CI::SC + CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
         if (live) GS(CI::SC + CI::KPREV) = cand;
+        const unsigned long long pf_r0 = a.prof ? clock64() : 0ull;
         if (wave_any(restart)) {
             const bool ra = restart && use_avg;
             if (wave_any(ra)) {
@@ -755,10 +757,12 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                 since = 0;
             }
         }
+        if (a.prof) pf_rst += clock64() - pf_r0;
     }
-    if (a.prof && lane < 4) {   // (lane-indexed: a vector store)
-        const unsigned long long v = lane == 0 ? pf_it : (lane == 1 ? pf_chk : (lane == 2 ? pf_load : pf_kkt));
-        a.prof[(size_t)blockIdx.x * 4 + lane] = v;
+    if (a.prof && lane < 6) {   // (lane-indexed: a vector store)
+        const unsigned long long v = lane == 0 ? pf_it : lane == 1 ? pf_chk : lane == 2 ? pf_load : lane == 3 ? pf_kkt
+                                   : lane == 4 ? pf_rst : pf_n;
+        a.prof[(size_t)blockIdx.x * 8 + lane] = v;
     }
     if constexpr (PERSIST) {
         // the last wave out re-arms the queue for the next (stream-ordered) launch: every wave

@@ -2411,10 +2411,10 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         static unsigned long long* pbuf = nullptr;
         static size_t pcap = 0;
         const size_t waves = (size_t)a.S;   // >= the grid (G scenarios per wave)
-        if (lprof && pcap < waves * 4) {
+        if (lprof && pcap < waves * 8) {
             if (pbuf) CK(hipFree(pbuf));
-            CK(hipMalloc((void**)&pbuf, waves * 4 * sizeof(unsigned long long)));
-            pcap = waves * 4;
+            CK(hipMalloc((void**)&pbuf, waves * 8 * sizeof(unsigned long long)));
+            pcap = waves * 8;
         }
         if (lprof) CK(hipMemsetAsync(pbuf, 0, pcap * sizeof(unsigned long long), h->stream));
         a.prof = lprof ? pbuf : nullptr;
@@ -2423,10 +2423,11 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             std::vector<unsigned long long> hb(pcap);
             CK(hipMemcpyAsync(hb.data(), pbuf, pcap * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
             CK(hipStreamSynchronize(h->stream));
-            double t[4] = {0, 0, 0, 0};
-            for (size_t i = 0; i < pcap; ++i) t[i % 4] += (double)hb[i];
-            fprintf(stderr, "PHG_LOCAL_PROF iter_cycles %.6e check_cycles %.6e load_cycles %.6e kkt_cycles %.6e\n", t[0], t[1],
-                    t[2], t[3]);
+            double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (size_t i = 0; i < pcap; ++i) t[i % 8] += (double)hb[i];
+            fprintf(stderr,
+                    "PHG_LOCAL_PROF iter_cycles %.6e check_cycles %.6e load_cycles %.6e kkt_cycles %.6e restart_cycles %.6e "
+                    "checks %.0f\n", t[0], t[1], t[2], t[3], t[4], t[5]);
         }
     }
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));

@@ -202,8 +202,8 @@ struct PdhgArgs {
     double* xs;             // [S*n]
     double* ys;             // [S*m]
     double* omega;          // [S]
-    // diagnostic (PHG_LOCAL_PROF, lane-local kernel only): per wave {iteration cycles, check
-    // cycles, load cycles, checks}; null = off
+    // diagnostic (PHG_LOCAL_PROF, lane-local kernel only): per wave [8] {iteration cycles, check
+    // cycles, load cycles, KKT cycles, restart-block cycles, checks}; null = off
     unsigned long long* prof;
     // outputs
     double* x_out;          // [S*n] unscaled, or null: left to phg_get / eval (xs * dc, see unscale_launch)
