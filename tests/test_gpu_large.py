@@ -218,7 +218,9 @@ def test_block_register_pieces_same_bits(monkeypatch):
     """sslp's pieces fit the registers (row pieces <= 8, columns in <= 2 rows), so the block layout
     runs the block kernel with the matrix held in registers for the whole solve; PHG_BLOCK_STREAM=1 forces
     the form that re-reads values / indices every iteration.  Same products in the same order:
-    Iter0 and one prox-QP solve give bit-identical objectives, iteration counts and nonants."""
+    Iter0 and one prox-QP solve give bit-identical objectives, iteration counts and nonants.  (Row
+    segments off: the segment form sums a row's pieces pairwise, the streaming variants in order.)"""
+    monkeypatch.setenv("PHG_BLOCK_SEG", "0")
     S = 8
     o = oph.OraclePH(_opts(), om.sslp_names(S), om.sslp, {})
     o.Iter0()
