@@ -80,8 +80,8 @@ __device__ __forceinline__ double piece_sum8(const double* p, int cnt) {
 // A^T y as dc (A^T (dr y)).
 //
 // UN: the unit form (BlockLayout::rcode) -- VS with every constant entry +-1: the entry codes and the
-// scenario's varying entry rows sit in LDS, an entry adds or subtracts its x (y) or, on a varying
-// row, fma's its value; acc + v / acc - v are fma(+-1, v, acc) exactly, so the bits equal VS's.
+// scenario's varying entry rows sit in LDS; an entry fma's its x (y) with +-1 built from the code's
+// sign bit or, on a varying row, with its value -- the delta form's products, bit for bit.
 //
 // SEG = 8 / 16: the row-segment form (BlockLayout built by build_block_layout's segment planner) --
 // every row's pieces sit in an aligned segment of 1, 2, 4, 8 (or 16) consecutive lanes of one wave,
@@ -103,7 +103,8 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     const int s = a.order ? a.order[blockIdx.x] : blockIdx.x;
     double* xl = smem;                   // [n_pad]
     double* yl = xl + B.n_pad;           // [m_pad]
-    double* rp = yl + B.m_pad;           // [PPT*NT] row-piece partials
+    double* zl = yl + B.m_pad;           // [2] zl[0] = 0.0: the unit form's padding entries read it
+    double* rp = zl + 2;                 // [PPT*NT] row-piece partials
     double* cp = rp + PPT * NT;          // [QPT*NT] column-piece partials
     double* red = cp + QPT * NT;         // [16 * (NT/64 + 1)] reduction scratch
     const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
@@ -132,10 +133,16 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
         for (int i = t; i < B.ec; i += NT) codes[B.er + i] = B.ccode[i];
     }
     // UN product of code cd (entry row with varying-row index d) with the LDS vector v
-    auto unit_fma = [&](int cd, int d, int drow0, const double* v, double acc) {
-        if (d >= 0) return fma(dl[(drow0 + d) * NT + t], v[cd - 1], acc);
-        const double u = v[(cd < 0 ? -cd : cd) - (cd != 0 ? 1 : 0)];
-        return cd > 0 ? acc + u : (cd < 0 ? acc - u : acc);
+    // (code = LDS byte address of the x / y element, bit 0 the value's sign; padding: zl)
+    if constexpr (UN) {
+        if (t == 0) zl[0] = 0.0;   // read after the first products() barrier
+    }
+    auto unit_fma = [&](int cd, int d, int drow0, double acc) {
+        const unsigned cu = (unsigned)(unsigned short)cd;
+        const double v = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(smem) + (cu & 0xFFF8u));
+        if (d >= 0) return fma(dl[(drow0 + d) * NT + t], v, acc);
+        // +-1.0 built from the sign bit: fma(+-1, v, acc), the delta form's bits
+        return fma(__hiloint2double((int)(0x3FF00000u | (cu << 31)), 0), v, acc);
     };
 
     // ------------------------------------------------------------------ columns owned
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
                     const int e = off + k * NT + t;
-                    if constexpr (UN) acc = unit_fma(codes[e], B.rdrow[off / NT + k], 0, xl, acc);
+                    if constexpr (UN) acc = unit_fma(codes[e], B.rdrow[off / NT + k], 0, acc);
                     else acc = fma(rval(e, off / NT + k), xl[B.ridx[e]], acc);
                 }
                 off += kk * NT;
@@ -291,7 +298,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
                     const int e = off + k * NT + t;
-                    if constexpr (UN) acc = unit_fma(codes[B.er + e], B.cdrow[off / NT + k], B.nd_r, yl, acc);
+                    if constexpr (UN) acc = unit_fma(codes[B.er + e], B.cdrow[off / NT + k], B.nd_r, acc);
                     else acc = fma(cval(e, off / NT + k), yl[B.cidx[e]], acc);
                 }
                 off += kk * NT;
@@ -645,7 +652,7 @@ void pdhg_block_variant_shape(int v, int* out12) {
 // UN variants add the varying entry rows (nd doubles per thread) and the er + ec 16-bit codes
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad, int nd, int ecodes) {
     const BlockVariant& V = kBlockVariants[v];
-    const size_t base = (size_t)(n_pad + m_pad + V.PPT * V.NT + V.QPT * V.NT + 16 * (V.NT / 64 + 1)) * sizeof(double);
+    const size_t base = (size_t)(n_pad + m_pad + 2 + V.PPT * V.NT + V.QPT * V.NT + 16 * (V.NT / 64 + 1)) * sizeof(double);
     return V.UN ? base + (size_t)nd * V.NT * sizeof(double) + (size_t)ecodes * sizeof(short) : base;
 }
 

@@ -1197,7 +1197,8 @@ static int build_wave_values(phg_handle* h) {
 static int build_unit_codes(phg_handle* h, const double* rv, const double* cv) {
     BlockLayout& L = h->blk;
     const char* eu = std::getenv("PHG_UNIT");
-    if ((eu && std::atoi(eu) == 0) || h->n >= 32767 || h->m >= 32767) return 0;
+    // codes are 16-bit LDS byte addresses: x, y and the zero slot after them must sit below 64 KiB
+    if ((eu && std::atoi(eu) == 0) || (long)(L.n_pad + L.m_pad + 1) * 8 > 0xFFF8) return 0;
     int twin = -1, sh[12];
     for (int v = 0; v < pdhg_block_num_variants() && twin < 0; ++v) {
         pdhg_block_variant_shape(v, sh);
@@ -1205,7 +1206,10 @@ static int build_unit_codes(phg_handle* h, const double* rv, const double* cv) {
     }
     if (twin < 0 || pdhg_block_lds_bytes(twin, L.n_pad, L.m_pad, L.nd_r + L.nd_c, L.er + L.ec) > 160 * 1024) return 0;
     const int NT = h->bshape[0];
-    auto codes = [&](const double* dv, const int* didx, int E, const int* drow, std::vector<short>& out) {
+    // entry code: the LDS byte address of the entry's x (row pieces: xl at 0) or y (column pieces: yl
+    // at n_pad doubles) with the value's sign in bit 0; padding -> the zero slot after yl
+    const unsigned zero_addr = (unsigned)(L.n_pad + L.m_pad) * 8u;
+    auto codes = [&](const double* dv, const int* didx, int E, const int* drow, int base, std::vector<short>& out) {
         std::vector<double> val(E);
         std::vector<int> idx(E);
         if (hipMemcpy(val.data(), dv, (size_t)E * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
@@ -1213,19 +1217,19 @@ static int build_unit_codes(phg_handle* h, const double* rv, const double* cv) {
             return -1;
         out.assign(std::max(1, E), 0);
         for (int e = 0; e < E; ++e) {
-            const int c = idx[e] + 1;
+            const unsigned c = (unsigned)(base + idx[e]) * 8u;
             if (drow[e / NT] >= 0) { out[e] = (short)c; continue; }   // varying row: its value from rvd / cvd
             if (val[e] == 1.0) out[e] = (short)c;
-            else if (val[e] == -1.0) out[e] = (short)-c;
-            else if (val[e] == 0.0 && !std::signbit(val[e])) out[e] = 0;
+            else if (val[e] == -1.0) out[e] = (short)(c | 1u);
+            else if (val[e] == 0.0 && !std::signbit(val[e])) out[e] = (short)zero_addr;
             else return 1;   // a constant entry that is not a unit
         }
         return 0;
     };
     CK(hipStreamSynchronize(h->stream));   // the piece gathers wrote rv / cv
     std::vector<short> rc, cc;
-    int r = codes(rv, L.ridx, L.er, L.rdrow, rc);
-    if (r == 0) r = codes(cv, L.cidx, L.ec, L.cdrow, cc);
+    int r = codes(rv, L.ridx, L.er, L.rdrow, 0, rc);
+    if (r == 0) r = codes(cv, L.cidx, L.ec, L.cdrow, L.n_pad, cc);
     if (r < 0) return fail("phg_load_batch: reading the piece values back failed");
     if (r > 0) return 0;
     short* p;

@@ -70,9 +70,9 @@ struct BlockLayout {
     const double* cvd;
     long dstride_r, dstride_c;
     // unit form (UN variants, delta form only): every constant entry is -1, 0 or +1, so the pieces
-    // need no shared values at all -- entry e is the 16-bit code rcode[e] / ccode[e] = +-(index + 1)
-    // (the sign is the value's; 0 = padding; index + 1 on the varying entry rows, whose values come
-    // from rvd / cvd).  The codes and the scenario's nd_r + nd_c varying entry rows are copied into
+    // need no shared values at all -- entry e is the 16-bit code rcode[e] / ccode[e] = the LDS byte
+    // address of its x (y) element with the value's sign in bit 0 (padding: the zero slot after y;
+    // on the varying entry rows the sign bit is 0 and the values come from rvd / cvd).  The codes and the scenario's nd_r + nd_c varying entry rows are copied into
     // the workgroup's LDS once, so the PDHG iterations read no matrix data from memory.
     int nd_r, nd_c, er, ec;   // varying entry rows; code counts (sum rk NT, sum ck NT)
     const short* rcode;
