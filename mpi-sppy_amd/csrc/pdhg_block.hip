@@ -137,6 +137,19 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     if constexpr (UN) {
         if (t == 0) zl[0] = 0.0;   // read after the first products() barrier
     }
+    // the varying entry rows as bit masks (their block index = the set bits below them, as
+    // build_block_values numbers them): uniform scalar arithmetic instead of a kernarg load per entry row
+    unsigned rdm = 0, cdm = 0;
+    if constexpr (UN) {
+#pragma unroll
+        for (int R = 0; R < 32; ++R) {
+            rdm |= B.rdrow[R] >= 0 ? 1u << R : 0u;
+            cdm |= B.cdrow[R] >= 0 ? 1u << R : 0u;
+        }
+    }
+    auto drow_of = [](unsigned msk, int R) {
+        return (msk >> R) & 1u ? __builtin_popcount(msk & ((1u << R) - 1u)) : -1;
+    };
     auto unit_fma = [&](int cd, int d, int drow0, double acc) {
         const unsigned cu = (unsigned)(unsigned short)cd;
         const double v = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(smem) + (cu & 0xFFF8u));
@@ -253,7 +266,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
                     const int e = off + k * NT + t;
-                    if constexpr (UN) acc = unit_fma(codes[e], B.rdrow[off / NT + k], 0, acc);
+                    if constexpr (UN) acc = unit_fma(codes[e], drow_of(rdm, off / NT + k), 0, acc);
                     else acc = fma(rval(e, off / NT + k), xl[B.ridx[e]], acc);
                 }
                 off += kk * NT;
@@ -298,7 +311,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
                     const int e = off + k * NT + t;
-                    if constexpr (UN) acc = unit_fma(codes[B.er + e], B.cdrow[off / NT + k], B.nd_r, acc);
+                    if constexpr (UN) acc = unit_fma(codes[B.er + e], drow_of(cdm, off / NT + k), B.nd_r, acc);
                     else acc = fma(cval(e, off / NT + k), yl[B.cidx[e]], acc);
                 }
                 off += kk * NT;
