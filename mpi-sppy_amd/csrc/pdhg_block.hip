@@ -277,8 +277,8 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
                 const double v1 = acc + dpp_d<0xB1>(acc);
                 const double v2 = v1 + dpp_d<0x4E>(v1);
                 const double v3 = v2 + dpp_d<0x141>(v2);
-                const int L = rn[ps];
-                double t_ = L >= 8 ? v3 : (L >= 4 ? v2 : (L >= 2 ? v1 : acc));
+                const int L = rn[ps];   // 0 on lanes that own no row: their sum is 0 (their y stays 0)
+                double t_ = L >= 8 ? v3 : (L >= 4 ? v2 : (L >= 2 ? v1 : (L == 1 ? acc : 0.0)));
                 if constexpr (SEG == 16) {
                     const double v4 = v3 + dpp_d<0x140>(v3);
                     t_ = L >= 16 ? v4 : t_;
