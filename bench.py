@@ -27,7 +27,7 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 dense peak: the VALU rate (v_fma_f64, 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak
 
 
-DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_r02.json")
+DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_r03.json")
 
 
 def parse():
@@ -316,10 +316,10 @@ def main():
     achieved_gbs = bytes_it * pdhg_iters / args.steps / avg_launch_s / 1e9
     traffic = None
     # PMC bytes per launch (tools/traffic_from_pmc.py): only for the case and kernel (layout) they
-    # were measured on; farmer: profiles/traffic_r02.json, other cases profiles/cases_r02/<case>_traffic.json
-    tpath = args.traffic_json if args.case == "farmer" or args.traffic_json != DEFAULT_TRAFFIC else \
-        os.path.join(ROOT, "profiles", "cases_r02", f"{args.case}_traffic.json")
-    if os.path.exists(tpath):
+    # were measured on -- the default file is the headline's (farmer); another case's PMC bytes only
+    # when passed explicitly (--traffic-json), since its kernels changed after the round-2 files
+    tpath = args.traffic_json if args.case == "farmer" or args.traffic_json != DEFAULT_TRAFFIC else None
+    if tpath and os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             if tj.get("layout") == eng.layout and tj.get("case", "farmer") == args.case:
@@ -341,7 +341,11 @@ def main():
     # the block kernel on a SHARED matrix (sslp) holds its pieces in registers and x / y in LDS: no
     # per-iteration HBM stream exists to price against the HBM roofline, so it is reported like the
     # register-resident kernels (fp64 flops against the fp64 peak), with the PMC-measured HBM rate beside
-    valu = eng.layout in ("local", "gather", "wave") or (eng.layout == "block" and nnz_distinct == 0)
+    # ... and so is the delta form's unit variant (netdes: the whole matrix in LDS as entry codes plus
+    # the scenario's varying entry rows, copied once per solve): no matrix bytes in the iteration
+    vinfo = eng.values_info() if eng.layout == "block" else None
+    unit = bool(vinfo and vinfo.get("unit"))
+    valu = eng.layout in ("local", "gather", "wave") or (eng.layout == "block" and (nnz_distinct == 0 or unit))
     # shared-matrix MFMA layout: SURVEY 8(d)2 F = 4 m n flops per scenario per PDHG iteration (A x and
     # A^T y as dense GEMM) and the flops the matrix cores actually execute (16 x 16 x 4 fragments:
     # 2048 flops per 16 scenarios each, the all-zero ones skipped)
@@ -387,7 +391,7 @@ def main():
                    "pdhg_layout": eng.layout, "lanes_per_scenario": eng.lanes_per_scenario,
                    "presolve_rows_folded": eng.rows_folded,
                    # value form the workgroup kernel streams (phg_values_info): per scenario vs one copy
-                   "values": eng.values_info() if eng.layout == "block" else None},
+                   "values": vinfo},
         # fp64 VALU-bound kernels (lane-local / gather): flops against the fp64 peak; the streaming
         # block kernel: algorithmic bytes against HBM
         "roofline": (mfma_rf if mfma_rf is not None else
@@ -406,6 +410,8 @@ def main():
                                 "gather": "pdhg_kernel (wave LDS-gather, fp64 VALU)",
                                 "block": ("pdhg_block_kernel (workgroup per scenario, shared matrix: pieces in registers, "
                                           "x / y in LDS)" if nnz_distinct == 0 else
+                                          "pdhg_block_kernel (workgroup per scenario, delta value form: the +-1 entries as "
+                                          "LDS address codes and the scenario's varying entry rows in LDS)" if unit else
                                           "pdhg_block_kernel (workgroup per scenario, streamed CSR/CSC pieces)"),
                                 "mfma": "pdhg_mfma_kernel (shared matrix, v_mfma_f64_16x16x4_f64, 16 scenarios per wave)",
                                 "wave": "pdhg_wave_kernel (one wave per scenario, shared matrix once per workgroup in "
