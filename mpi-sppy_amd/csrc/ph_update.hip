@@ -545,6 +545,7 @@ __global__ __launch_bounds__(256) void w_update_kernel(PhArgs a, const double* n
                                                        double head_thr, int first) {
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
+    if (!HEAD && a.skip_gate && a.skip_gate[0] < a.skip_below) return;   // grid-uniform (flush_fold)
     if constexpr (HEAD) {
         __shared__ double red256[256];
         // first PH iteration: no update precedes it, whatever the buffer holds

@@ -223,6 +223,10 @@ struct phg_handle {
     bool xn_external = false;         // PHG_F_XN was set by the caller: xN != xs dc until the next solve
     bool fold_conv_pending = false;   // the last solve did a folded update: its conv partials are
                                       // per scenario (conv_s / fold_st), not yet in any partials buffer
+    double fold_thr = 0.0;            // convthresh of the head that left fold_w_pending (flush_fold's gate)
+    bool flushed_partials = false;    // flush_fold wrote its conv partials into the handle's own buffer;
+                                      // the next phg_node_sums / phg_fold_partials into a caller's
+                                      // exchange buffer copies them there
     double* conv_s = nullptr;
     int* fold_st = nullptr;
 };
@@ -279,12 +283,29 @@ static bool fold_active(const phg_handle* h) {
 // a folded W update whose solve has not run (xbar of update k in place, phg_ph_head done): apply it
 // now with the standalone kernel (W, and its conv partials into the handle's own buffer) -- for
 // anything that reads or rewrites W, or a second head before a solve
+// (gated like the head that left it pending -- nothing moves when that head found conv
+// below its convthresh -- and its partials, written to the handle's own buffer, are carried into the
+// caller's exchange buffer by the next phg_node_sums / phg_fold_partials instead of being lost, which
+// would leave that buffer's already all-reduced partials to be summed a second time)
 static int flush_fold(phg_handle* h) {
     if (!h->fold_w_pending) return 0;
     PhArgs a = h->ph;
+    a.skip_gate = h->gate;
+    a.skip_below = h->fold_thr;
     CK(w_update_launch(a, h->xbar, h->convpart, h->stream));
     h->fold_w_pending = false;
     h->fold_conv_pending = false;
+    h->flushed_partials = true;
+    return 0;
+}
+
+// flushed partials into a caller's partials region (dst: the exchange buffer's, or null = the handle's
+// own, where they already are)
+static int carry_flushed_partials(phg_handle* h, double* dst) {
+    if (!h->flushed_partials) return 0;
+    h->flushed_partials = false;
+    if (!dst || dst == h->convpart) return 0;
+    CK(hipMemcpyAsync(dst, h->convpart, (2 * (size_t)h->P + 2) * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     return 0;
 }
 
@@ -2397,6 +2418,13 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             if (flush_fold(h)) return -1;
         } else {
             a.fold_w = 1;
+            // the head's gate holds for the prologue's W update too: a solve the caller did not gate
+            // is skipped when that head found conv below its convthresh (nothing moves: the
+            // reference breaks before Update_W and solve_loop, phbase.py:1008-1010)
+            if (!a.gate && h->fold_thr > -INFINITY) {
+                a.gate = h->gate;
+                a.gate_below = h->fold_thr;
+            }
             a.W_rw = h->W;
             a.conv_s = h->conv_s;
             a.fold_st = h->fold_st;
@@ -2472,6 +2500,7 @@ int phg_node_sums(phg_handle* h, double* dev_nodesum) {
     a.fold_st = h->fold_st;
     CK(node_sums_launch(a, dev_nodesum ? dev_nodesum : h->nodesum, h->stream));
     h->fold_conv_pending = false;
+    if (carry_flushed_partials(h, dev_nodesum ? dev_nodesum + 2 * (size_t)h->N_tot : nullptr)) return -1;
     if (timing_event(h, 2, 1)) return -1;
     return 0;
 }
@@ -2511,6 +2540,7 @@ int phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t fi
         if (flush_fold(h)) return -1;
         CK(xbar_head_launch(a, dev_packed ? dev_packed : h->packed, convthresh, first, h->stream));
         h->fold_w_pending = true;
+        h->fold_thr = first ? -INFINITY : convthresh;
     } else {
         CK(ph_head_launch(a, dev_packed ? dev_packed : h->packed, convthresh, first, h->stream));
     }
@@ -2615,6 +2645,7 @@ int phg_set_fold(phg_handle* h, int32_t on, int32_t* active) {
 int phg_fold_partials(phg_handle* h, double* dev_convpart) {
     if (!h || !h->loaded) return fail("phg_fold_partials: no batch loaded");
     CK(hipSetDevice(h->device));
+    if (carry_flushed_partials(h, dev_convpart)) return -1;
     if (!h->fold_conv_pending) return 0;
     CK(fold_conv_launch(h->ph, dev_convpart ? dev_convpart : h->convpart, h->stream));
     h->fold_conv_pending = false;

@@ -344,6 +344,11 @@ struct PhArgs {
     const double* conv_s;
     const int* fold_st;
     int fold_conv;
+    // a folded update applied on its own (flush_fold): the head's published conv (gate[0]) and its
+    // convthresh -- below it the head left xbar unchanged and W must not move either (the
+    // reference's break before Update_W, phbase.py:1008-1010); null: no gate
+    const double* skip_gate;
+    double skip_below;
 };
 
 

@@ -86,9 +86,7 @@ def _from_linear_model(m):
     return sf
 
 
-def _from_duck(model):
-    variables = list(model.variables())
-    col = {id(v): j for j, v in enumerate(variables)}
+def _duck_bounds(variables):
     n = len(variables)
     lo = np.empty(n)
     hi = np.empty(n)
@@ -97,6 +95,22 @@ def _from_duck(model):
             lo[j] = hi[j] = float(v.value)
         else:
             lo[j], hi[j] = _bound(v.lb, -INF), _bound(v.ub, INF)
+    return lo, hi
+
+
+def _duck_objective(ob, col, n, name):
+    c = np.zeros(n)
+    for v, a in ob.terms:
+        c[col[id(v)]] += float(a)
+    q = _qdiag(((col[id(v1)], col[id(v2)], a) for v1, v2, a in (getattr(ob, "quadratic", None) or [])), n, name)
+    return c, q, float(getattr(ob, "constant", 0.0) or 0.0), int(getattr(ob, "sense", 1))
+
+
+def _from_duck(model):
+    variables = list(model.variables())
+    col = {id(v): j for j, v in enumerate(variables)}
+    n = len(variables)
+    lo, hi = _duck_bounds(variables)
     rows, rlo, rhi, rnames = [], [], [], []
     for r in model.constraints():
         d = {}
@@ -108,16 +122,10 @@ def _from_duck(model):
         rlo.append(_bound(r.lower, -INF) - k)
         rhi.append(_bound(r.upper, INF) - k)
         rnames.append(getattr(r, "name", f"r{len(rows) - 1}"))
-    ob = model.objective()
-    c = np.zeros(n)
-    for v, a in ob.terms:
-        c[col[id(v)]] += float(a)
-    q = _qdiag(((col[id(v1)], col[id(v2)], a) for v1, v2, a in (getattr(ob, "quadratic", None) or [])), n,
-               getattr(model, "name", ""))
+    c, q, c0, sense = _duck_objective(model.objective(), col, n, getattr(model, "name", ""))
     rp, ci, vals = _csr(rows, n)
     return StandardForm(getattr(model, "name", ""), variables, [getattr(v, "name", f"x{j}") for j, v in enumerate(variables)],
-                        c, float(getattr(ob, "constant", 0.0) or 0.0), int(getattr(ob, "sense", 1)), rp, ci, vals,
-                        np.array(rlo), np.array(rhi), rnames, lo, hi, qdiag=q)
+                        c, c0, sense, rp, ci, vals, np.array(rlo), np.array(rhi), rnames, lo, hi, qdiag=q)
 
 
 def _qdiag(terms, n, name):
@@ -131,11 +139,8 @@ def _qdiag(terms, n, name):
     return q
 
 
-def _from_pyomo(model):   # parity unpinned: Pyomo is not importable here (module docstring)
+def _pyomo_bounds(variables):   # parity unpinned (module docstring)
     import pyomo.environ as pyo
-    from pyomo.repn import generate_standard_repn
-    variables = list(model.component_data_objects(pyo.Var, active=True, descend_into=True))
-    col = {id(v): j for j, v in enumerate(variables)}
     n = len(variables)
     lo, hi = np.empty(n), np.empty(n)
     for j, v in enumerate(variables):
@@ -143,6 +148,37 @@ def _from_pyomo(model):   # parity unpinned: Pyomo is not importable here (modul
             lo[j] = hi[j] = float(pyo.value(v))
         else:
             lo[j], hi[j] = _bound(v.lb, -INF), _bound(v.ub, INF)
+    return lo, hi
+
+
+def _pyomo_objective(model, col, n, obj=None):   # parity unpinned (module docstring)
+    import pyomo.environ as pyo
+    from pyomo.repn import generate_standard_repn
+    if obj is None:
+        objs = list(model.component_data_objects(pyo.Objective, active=True, descend_into=True))
+        if len(objs) != 1:
+            raise ValueError(f"expected one active objective, found {len(objs)}")
+        obj = objs[0]
+    # linear, or quadratic with diagonal terms only: PH's W and prox terms (phbase.py:724-750); the
+    # mutable Params (W, xbars, rho, W_on, prox_on) enter with their CURRENT values
+    repn = generate_standard_repn(obj.expr, compute_values=True, quadratic=True)
+    if repn.nonlinear_expr is not None:
+        raise ValueError("the objective has a nonlinear part; only linear + diagonal quadratic is supported")
+    c = np.zeros(n)
+    for v, a in zip(repn.linear_vars, repn.linear_coefs):
+        c[col[id(v)]] += float(a)
+    q = _qdiag(((col[id(v1)], col[id(v2)], a) for (v1, v2), a in
+                zip(repn.quadratic_vars or [], repn.quadratic_coefs or [])), n, model.name)
+    return c, q, float(repn.constant), 1 if obj.sense == pyo.minimize else -1
+
+
+def _from_pyomo(model):   # parity unpinned: Pyomo is not importable here (module docstring)
+    import pyomo.environ as pyo
+    from pyomo.repn import generate_standard_repn
+    variables = list(model.component_data_objects(pyo.Var, active=True, descend_into=True))
+    col = {id(v): j for j, v in enumerate(variables)}
+    n = len(variables)
+    lo, hi = _pyomo_bounds(variables)
     rows, rlo, rhi, rnames = [], [], [], []
     for con in model.component_data_objects(pyo.Constraint, active=True, descend_into=True):
         repn = generate_standard_repn(con.body, compute_values=True)
@@ -156,21 +192,9 @@ def _from_pyomo(model):   # parity unpinned: Pyomo is not importable here (modul
         rlo.append(-INF if con.lower is None else float(pyo.value(con.lower)) - k)
         rhi.append(INF if con.upper is None else float(pyo.value(con.upper)) - k)
         rnames.append(con.name)
-    objs = list(model.component_data_objects(pyo.Objective, active=True, descend_into=True))
-    if len(objs) != 1:
-        raise ValueError(f"expected one active objective, found {len(objs)}")
-    # linear, or quadratic with diagonal terms only: PH's W and prox terms (phbase.py:724-750)
-    repn = generate_standard_repn(objs[0].expr, compute_values=True, quadratic=True)
-    if repn.nonlinear_expr is not None:
-        raise ValueError("the objective has a nonlinear part; only linear + diagonal quadratic is supported")
-    c = np.zeros(n)
-    for v, a in zip(repn.linear_vars, repn.linear_coefs):
-        c[col[id(v)]] += float(a)
-    q = _qdiag(((col[id(v1)], col[id(v2)], a) for (v1, v2), a in
-                zip(repn.quadratic_vars or [], repn.quadratic_coefs or [])), n, model.name)
+    c, q, c0, sense = _pyomo_objective(model, col, n)
     rp, ci, vals = _csr(rows, n)
-    sense = 1 if objs[0].sense == pyo.minimize else -1
-    return StandardForm(model.name, variables, [v.name for v in variables], c, float(repn.constant), sense, rp, ci,
+    return StandardForm(model.name, variables, [v.name for v in variables], c, c0, sense, rp, ci,
                         vals, np.array(rlo), np.array(rhi), rnames, lo, hi, qdiag=q)
 
 
@@ -183,6 +207,38 @@ def extract(model):
     if hasattr(model, "component_data_objects"):
         return _from_pyomo(model)
     raise TypeError(f"cannot extract a standard form from {type(model).__name__}")
+
+
+def objective_of(model, sf, obj=None):
+    """The objective of ``model`` as it stands NOW, over ``sf``'s columns: (c, qdiag, c0, sense).
+
+    What a solver plugin must re-read before every solve of a model the caller mutates in place:
+    the reference's PH keeps ONE model per scenario and changes the mutable Params W, xbars, rho,
+    W_on, prox_on between solves (``phbase.py:621-638, 716-760``), so the objective's linear part,
+    diagonal and constant change while the constraint matrix does not.  ``obj`` (Pyomo only) is the
+    objective ``set_objective`` was handed (``spopt.py:147-160``)."""
+    if isinstance(model, LinearModel):
+        q = getattr(model, "_qdiag", None)
+        return (np.array(model._cost, np.float64), np.zeros(model.n) if q is None else np.asarray(q, np.float64).copy(),
+                float(model.obj_offset), int(model.sense))
+    if hasattr(model, "variables") and hasattr(model, "constraints"):
+        return _duck_objective(model.objective(), sf.col_of, sf.n, getattr(model, "name", ""))
+    if hasattr(model, "component_data_objects"):
+        return _pyomo_objective(model, sf.col_of, sf.n, obj)
+    raise TypeError(f"cannot read an objective from {type(model).__name__}")
+
+
+def column_bounds_of(model, sf):
+    """The column bounds of ``model`` as they stand NOW (a fixed variable: lo = hi = its value), over
+    ``sf``'s columns -- ``_fix_nonants`` / ``_restore_nonants`` fix and free variables in place
+    (``spopt.py:590-640``)."""
+    if isinstance(model, LinearModel):
+        return np.array(model._lo, np.float64), np.array(model._hi, np.float64)
+    if hasattr(model, "variables") and hasattr(model, "constraints"):
+        return _duck_bounds(sf.variables)
+    if hasattr(model, "component_data_objects"):
+        return _pyomo_bounds(sf.variables)
+    raise TypeError(f"cannot read column bounds from {type(model).__name__}")
 
 
 def to_linear_model(sf, name=None):
@@ -219,16 +275,21 @@ def as_scenario_model(model):
         lm._mpisppy_probability = model._mpisppy_probability
     lm._source = model
     lm._source_vars = sf.variables
+    lm._source_sf = sf        # column map for re-reading the objective / bounds (objective_of)
     return lm
 
 
-def load_values(lm, x):
-    """Write column values ``x`` back into the model's variables (``load_vars``)."""
+def load_values(lm, x, vars_to_load=None):
+    """Write column values ``x`` back into the model's variables (``load_vars``; ``vars_to_load``: only
+    those source variables)."""
     lm._solution = np.asarray(x, np.float64).copy()
     src = getattr(lm, "_source_vars", None)
     if src is None:
         return
+    only = None if vars_to_load is None else {id(v) for v in vars_to_load}
     for v, xv in zip(src, lm._solution):
+        if only is not None and id(v) not in only:
+            continue
         if hasattr(v, "set_value"):
             v.set_value(float(xv))
         else:

@@ -1,32 +1,43 @@
-"""The ``phg`` solver plugin: a per-model (or per-batch) LP / QP solve through the C ABI, with the
-plugin surface ``SPOpt`` uses on its solvers (``mpisppy/spopt.py:876-913`` creation, ``:150-231`` use):
+"""The ``phg`` solver plugin: LP / diagonal-QP solves through the C ABI with the plugin surface
+``SPOpt`` uses on its solvers (``mpisppy/spopt.py:876-913`` creation, ``:99-247`` use):
 
-* ``SolverFactory("phg")`` -> :class:`PHGSolver` (``spopt.py:884``); :func:`register_solver` adds
-  names, and on import the plugin registers itself with Pyomo's ``SolverFactory`` when Pyomo is
-  importable (parity unpinned: Pyomo is absent here);
+* ``SolverFactory("phg")`` -> :class:`PHGSolver` (``spopt.py:884``, one plugin per subproblem);
+  :func:`register_solver` adds names, and on import the plugin registers itself with Pyomo's
+  ``SolverFactory`` when Pyomo is importable (parity unpinned: Pyomo is absent here);
 * ``options`` dict (``spopt.py:171-172``): ``pdhg_eps`` (relative KKT tolerance, default 1e-9),
-  ``pdhg_max_iter``, ``pdhg_check_every``, ``pdhg_layout``;
-* ``solve(model, tee=False, load_solutions=True, save_results=False)`` (``:185-187``) -> a results
+  ``pdhg_max_iter``, ``pdhg_check_every``, ``pdhg_layout``, ``pdhg_warm_start`` (default on: a
+  solve starts from the plugin's previous primal / dual solution, as a persistent CPU solver does);
+* ``solve(model, tee=False, load_solutions=True, save_results=True)`` (``:185-187``) -> a results
   object with ``.solver.status``, ``.solver.termination_condition``, ``len(.solution)``,
-  ``.solution(0).status`` (``sputils.py:29-34``) and ``.Problem[0].Lower_bound / Upper_bound``
-  (``spopt.py:225-230``: the PDHG dual bound and primal objective, in the model's sense);
-* the persistent calls ``set_instance`` (``:933-960``), ``set_objective``, ``update_var``
-  (``:625-777``: re-read at the next solve), ``load_vars`` (``:219``);
-* ``solve_batch(models)``: every model of ONE sparsity pattern in one launch -- the engine's own
-  path (what ``PHBase.solve_loop`` does for all local scenarios at once).
+  ``.solution(0).status`` (``sputils.py:29-34``), ``.solution(0).variable`` (name -> {"Value": v},
+  what Pyomo's ``ModelSolutions.load_from`` reads, ``spopt.py:221``) and
+  ``.Problem[0].Lower_bound / Upper_bound`` (``:225-230``: the dual bound and primal objective in
+  the model's sense);
+* the persistent calls ``set_instance`` (``:933-960``), ``set_objective`` (``:147-160``),
+  ``update_var`` (``:590-640``), ``load_vars`` (``:219``).  With Pyomo importable the class derives
+  from Pyomo's ``PersistentSolver``, so ``sputils.is_persistent`` (``sputils.py:384-386``) sends the
+  reference's ``solve_one`` down its ``set_objective`` / ``load_vars`` branch; :func:`is_persistent`
+  is the same test here;
+* ``solve_batch(models)``: every model of ONE sparsity pattern in one launch.
 
-The batch needs no scenario tree for a plain solve: a model without ``_mpisppy_node_list`` gets a
-one-column ROOT node whose PH terms are switched off (w_on = prox_on = 0), so the solve is the
-model's own LP.  A model whose objective has a DIAGONAL quadratic part (``extract.qdiag``) -- the
-reference PH's subproblem from iteration 1 on, ``f(x) + W.x + rho/2 (x - xbar)^2``
-(``phbase.py:724-750``) as ``SPOpt.solve_one`` hands it to its plugin (``spopt.py:147-231``) --
-is solved as the C ABI's prox-QP: the batch's nonants are the quadratic columns, rho = the
-min-form diagonal, xbar = 0, W off (the linear part, W.x - rho xbar.x included, is already in c),
-prox on.  A concave (min-form negative) diagonal raises.  The GPU engine is the only solver: there
-is no CPU fallback (the library loads or the plugin raises).
+**Models mutated in place.** The reference builds each scenario model ONCE and changes its mutable
+Params (W, xbars, rho, W_on, prox_on) between iterations (``phbase.py:621-638, 716-760``); it then
+calls ``solve(s, load_solutions=False)`` on the SAME object every iteration and, for a
+non-persistent plugin, never calls ``set_objective``.  So every ``solve`` re-reads the objective
+(linear part, diagonal, constant: ``extract.objective_of``) and the column bounds
+(``extract.column_bounds_of``: ``_fix_nonants`` fixes variables in place) -- the matrix is extracted
+once per model.  ONE engine per plugin is kept and reused: it holds the matrix, the bounds and the
+first extraction's cost ``c0``, with EVERY column a plugin-private nonant, so a later objective
+``c + 1/2 sum q_j x_j^2`` enters as the C ABI's PH terms: W = c - c0 (min form), rho = q, xbar = 0,
+both terms on -- ``c0 + W + rho (x - 0)`` is ``c``, the diagonal is ``q``, exactly.  The constant's
+change is added to the objective and the bound on the host.  Only a change of the column bounds
+(or the sense) reloads the engine (``rebuilds`` counts the loads).
 
-Reported bounds (``Problem[0].Lower_bound`` of a min problem) are weak-duality certificates of the
-solve's dual iterate (``phg_opts.safe_bound``), valid also at ``maxIterations``.
+A concave (min-form negative) diagonal raises.  The GPU engine is the only solver: there is no CPU
+fallback (the library loads or the plugin raises).  Reported bounds are weak-duality certificates
+of the solve's dual iterate for every solve (``phg_opts.safe_bound`` = 2): never on the wrong side
+of the optimum, also at ``maxIterations`` (a converged solve's own dual objective can sit
+eps (1 + |p| + |d|) above it).
 """
 import numpy as np
 
@@ -34,15 +45,31 @@ from ..engine import BatchArrays, Engine
 from ..model import LinearModel, VarData
 from ..scenario_tree import ScenarioNode
 from .. import _lib
-from .extract import as_scenario_model, load_values
+from .extract import as_scenario_model, column_bounds_of, load_values, objective_of
+
+try:   # pragma: no cover -- Pyomo is not importable on the build container / GPU box
+    from pyomo.solvers.plugins.solvers.persistent_solver import PersistentSolver as _PersistentBase
+    from pyomo.opt import SolutionStatus as _SolS, SolverStatus as _SolverS, TerminationCondition as _TC
+    _PYOMO = True
+except Exception:
+    _PYOMO = False
+
+    class _PersistentBase:
+        """Stand-in for Pyomo's ``PersistentSolver`` (absent here): the type ``is_persistent`` tests."""
+
+    class _SolverS:
+        ok, warning, error = "ok", "warning", "error"
+
+    class _TC:
+        optimal, maxIterations, error = "optimal", "maxIterations", "error"
+
+    class _SolS:
+        optimal, feasible = "optimal", "feasible"
 
 
-class _Status:
-    ok, warning, error = "ok", "warning", "error"
-
-
-class _Termination:
-    optimal, maxIterations, error = "optimal", "maxIterations", "error"
+def is_persistent(solver):
+    """``sputils.is_persistent`` (``sputils.py:384-386``): an instance of (Pyomo's) PersistentSolver."""
+    return isinstance(solver, _PersistentBase)
 
 
 class _SolverInfo:
@@ -60,22 +87,25 @@ class _Problem:
 
 
 class _Solution:
-    def __init__(self, status, x):
+    def __init__(self, status, x, names):
         self.status = status
         self.x = x
+        # Pyomo's results layout: variable label -> {"Value": v} (ModelSolutions.load_from by name)
+        self.variable = {nm: {"Value": float(v)} for nm, v in zip(names, x)}
 
 
 class Results:
     """Pyomo-results-like object of one solve."""
 
-    def __init__(self, st, iters, kkt, obj, bound, sense, x):
-        tc = {0: _Termination.optimal, 1: _Termination.maxIterations}.get(int(st), _Termination.error)
-        status = {0: _Status.ok, 1: _Status.warning}.get(int(st), _Status.error)
+    def __init__(self, st, iters, kkt, obj, bound, sense, x, names):
+        tc = {0: _TC.optimal, 1: _TC.maxIterations}.get(int(st), _TC.error)
+        status = {0: _SolverS.ok, 1: _SolverS.warning}.get(int(st), _SolverS.error)
         self.solver = _SolverInfo(status, tc, int(iters), float(kkt))
         # bounds in the model's sense: a min problem's dual bound is the lower bound
         self.Problem = [_Problem(float(bound), float(obj), sense)]
         self.problem = self.Problem
-        self._solutions = [_Solution("optimal" if st == 0 else "feasible", x)] if st in (0, 1) else []
+        self._solutions = ([_Solution(_SolS.optimal if st == 0 else _SolS.feasible, x, names)]
+                           if st in (0, 1) else [])
 
     @property
     def solution(self):
@@ -89,9 +119,9 @@ class Results:
 
 
 class _PluginScenario:
-    """The plugin's view of one model: its standard form (attributes forwarded) with the batch's own
-    tree -- the quadratic columns as ROOT nonants -- and unit probability coefficients, without
-    touching the caller's model."""
+    """The plugin's view of one model: its standard form (attributes forwarded) with the plugin's own
+    tree -- every column a ROOT nonant -- and unit probability coefficients, without touching the
+    caller's model."""
 
     def __init__(self, lm, nodes):
         self._lm = lm
@@ -104,18 +134,23 @@ class _PluginScenario:
         return getattr(self._lm, k)
 
 
-class PHGSolver:
-    """Persistent-style plugin over libphg (one engine per instance, rebuilt when the model or the
-    batch shape changes)."""
+class PHGSolver(_PersistentBase):
+    """Persistent-style plugin over libphg: one engine per instance, built at the first solve of a
+    model (or batch) and reused by every later solve of the same model objects."""
 
     name = "phg"
 
     def __init__(self, **kwds):
+        if _PYOMO:   # pragma: no cover -- parity unpinned (Pyomo absent)
+            _PersistentBase.__init__(self, type="phg")
         self.options = dict(kwds.get("options", {}))
         self._models = None
         self._lms = None
         self._engine = None
-        self._dirty = True
+        self._pending_obj = None
+        self._X = None
+        self.rebuilds = 0     # engine loads (matrix + bounds); a PH run on one model needs one
+        self.solves = 0
 
     # ------------------------------------------------------------------ plugin surface
     def available(self, exception_flag=False):
@@ -131,12 +166,15 @@ class PHGSolver:
         self._set([model])
 
     def set_objective(self, obj=None):
-        self._dirty = True
+        """``spopt.py:147-160``: the objective is re-read at the next solve anyway; a Pyomo objective
+        handed here is the one read."""
+        self._pending_obj = obj
 
     def update_var(self, var=None):
-        self._dirty = True
+        """``spopt.py:590-640`` (``_fix_nonants`` / ``_restore_nonants``): bounds are re-read at the
+        next solve."""
 
-    def solve(self, model=None, tee=False, load_solutions=True, save_results=False, **kwds):
+    def solve(self, model=None, tee=False, load_solutions=True, save_results=True, **kwds):
         if model is not None and (self._models is None or len(self._models) != 1 or self._models[0] is not model):
             self._set([model])
         if self._models is None:
@@ -144,13 +182,18 @@ class PHGSolver:
         return self._solve(tee, load_solutions)[0]
 
     def solve_batch(self, models, tee=False, load_solutions=True):
-        self._set(list(models))
+        models = list(models)
+        if self._models is None or len(self._models) != len(models) or any(
+                a is not b for a, b in zip(self._models, models)):
+            self._set(models)
         return self._solve(tee, load_solutions)
 
     def load_vars(self, vars_to_load=None):
-        if self._engine is None:
+        """``spopt.py:219``: the last solve's values into the model's variables (all, or the given
+        ones)."""
+        if self._engine is None or self._X is None:
             raise RuntimeError("PHGSolver.load_vars: nothing solved yet")
-        self._load()
+        self._load(self._X, vars_to_load)
 
     def close(self):
         if self._engine is not None:
@@ -160,77 +203,100 @@ class PHGSolver:
     # ------------------------------------------------------------------ internals
     def _set(self, models):
         self._models = models
-        self._dirty = True
+        self._lms = None          # new model objects: extract their standard forms at the next solve
+        self._X = None
 
-    def _build(self):
-        import torch
+    def _extract(self):
         lms = []
         for md in self._models:
             lm = as_scenario_model(md)
             if not isinstance(lm, LinearModel) or lm.n == 0:
                 raise ValueError("PHGSolver: empty model")
             lms.append(lm)
-        S = len(lms)
-        # min-form diagonal of each model's quadratic objective; the batch's nonants are the columns
-        # quadratic in any model (one shared column list), else the dummy column 0 with PH terms off
-        qmin = []
-        for lm in lms:
-            q = getattr(lm, "_qdiag", None)
-            q = np.zeros(lm.n) if q is None else lm.sense * np.asarray(q, np.float64)
-            if (q < 0).any():
-                raise ValueError(f"PHGSolver: model {lm.name}: the quadratic objective is not convex "
-                                 "(min-form diagonal < 0)")
-            qmin.append(q)
-        qcols = sorted(set(int(j) for q in qmin for j in np.nonzero(q)[0]))
-        self._quadratic = bool(qcols)
-        cols = qcols or [0]
+        self._lms = lms
+        self._sfs = [getattr(lm, "_source_sf", None) for lm in lms]
+        self.close()
+
+    def _current(self):
+        """(c, q, c0, sense, lo, hi) of every model as it stands now (the re-read)."""
+        out = []
+        for md, lm, sf in zip(self._models, self._lms, self._sfs):
+            src = lm if sf is None else md
+            c, q, c0, sense = objective_of(src, sf, self._pending_obj if len(self._models) == 1 else None)
+            lo, hi = column_bounds_of(src, sf)
+            out.append((c, q, c0, sense, lo, hi))
+        self._pending_obj = None
+        return out
+
+    def _build(self, cur):
+        """Load the engine on the models' matrix with the CURRENT bounds; every column is a nonant
+        of the plugin's ROOT node, so later objectives enter as W / rho (module docstring)."""
+        import torch
         views = []
-        for lm in lms:
+        for lm, sf, (c, q, c0, sense, lo, hi) in zip(self._lms, self._sfs, cur):
+            if sf is not None:             # the plugin's own copy: base cost and bounds = the current ones
+                lm._cost = list(c)         # (a LinearModel handed in directly already holds them)
+                lm.obj_offset, lm.sense = c0, sense
+                lm._lo, lm._hi = list(lo), list(hi)
             names = lm.column_names()
-            nodes = [ScenarioNode("ROOT", 1.0, 1, None, [VarData(lm, j, names[j]) for j in cols], lm)]
+            nodes = [ScenarioNode("ROOT", 1.0, 1, None, [VarData(lm, j, names[j]) for j in range(lm.n)], lm)]
             views.append(_PluginScenario(lm, nodes))
+        S = len(views)
         batch = BatchArrays(views, ["ROOT"], [1.0 / S] * S, 0, S, 1)
-        if self._engine is not None:
-            self._engine.close()
+        self.close()
         dev = torch.cuda.current_device()
         self._engine = Engine(batch, device=dev, layout=self.options.get("pdhg_layout", "auto"))
-        if self._quadratic:
-            # prox term rho/2 (x - xbar)^2 with xbar = 0: exactly the diagonal quadratic
-            self._engine.set(_lib.F_RHO, np.stack([q[cols] for q in qmin]).ravel())
-            self._engine.set(_lib.F_XBAR, np.zeros(len(cols)))
-        self._lms = lms
-        self._dirty = False
+        self._engine.set(_lib.F_XBAR, np.zeros(self._lms[0].n))
+        self._base = [(c.copy(), c0, sense, lo.copy(), hi.copy()) for c, q, c0, sense, lo, hi in cur]
+        self._warm = False
+        self.rebuilds += 1
 
     def _solve(self, tee, load_solutions):
-        if self._dirty or self._engine is None:
-            self._build()
+        if self._lms is None:
+            self._extract()
+        cur = self._current()
+        for (c, q, c0, sense, lo, hi) in cur:
+            if (sense * q < 0).any():
+                raise ValueError("PHGSolver: the quadratic objective is not convex (min-form diagonal < 0)")
+        if self._engine is None or any(
+                b[2] != k[3] or not np.array_equal(b[3], k[4]) or not np.array_equal(b[4], k[5])
+                for b, k in zip(self._base, cur)):
+            self._build(cur)
         eng = self._engine
-        eng.solve(0, 1 if self._quadratic else 0, eps=float(self.options.get("pdhg_eps", 1e-9)),
+        # the objective now, as PH terms on the loaded base cost (min form): W = c - c0, rho = q
+        eng.set(_lib.F_W, np.concatenate([sense * (c - b[0]) for (c, q, c0, sense, lo, hi), b in zip(cur, self._base)]))
+        eng.set(_lib.F_RHO, np.concatenate([sense * q for (c, q, c0, sense, lo, hi) in cur]))
+        warm = 1 if (self._warm and self.options.get("pdhg_warm_start", True)) else 0
+        eng.solve(1, 1, eps=float(self.options.get("pdhg_eps", 1e-9)),
                   max_iter=int(self.options.get("pdhg_max_iter", 200000)),
-                  check_every=int(self.options.get("pdhg_check_every", 32)), warm_start=0, safe_bound=True)
+                  check_every=int(self.options.get("pdhg_check_every", 32)), warm_start=warm, safe_bound=2)
         eng.sync()
+        self._warm = True
+        self.solves += 1
         st = eng.get_i32(_lib.I_STATUS)
         it = eng.get_i32(_lib.I_ITERS)
         kkt = eng.get(_lib.F_KKT)
         obj = eng.get(_lib.F_OBJ)
         bnd = eng.get(_lib.F_BOUND)
         X = eng.get(_lib.F_X).reshape(eng.S, -1)
-        sense = self._lms[0].sense
-        out = [Results(st[s], it[s], kkt[s], obj[s], bnd[s], sense, X[s]) for s in range(eng.S)]
+        self._X = X
+        out = []
+        for s, ((c, q, c0, sense, lo, hi), b) in enumerate(zip(cur, self._base)):
+            dk = c0 - b[1]            # the objective constant's change since the load (model sense)
+            out.append(Results(st[s], it[s], kkt[s], obj[s] + dk, bnd[s] + dk, sense, X[s],
+                               self._lms[s].column_names()))
         if tee:
             for s, r in enumerate(out):
                 print(f"[phg] {getattr(self._lms[s], 'name', s)}: {r.solver.termination_condition} "
-                      f"obj={r.Problem[0].Upper_bound if sense == 1 else r.Problem[0].Lower_bound} "
+                      f"obj={r.Problem[0].Upper_bound if cur[s][3] == 1 else r.Problem[0].Lower_bound} "
                       f"iters={r.solver.iterations} kkt={r.solver.kkt:.2e}")
         if load_solutions:
             self._load(X)
         return out
 
-    def _load(self, X=None):
-        if X is None:
-            X = self._engine.get(_lib.F_X).reshape(self._engine.S, -1)
+    def _load(self, X, vars_to_load=None):
         for lm, x in zip(self._lms, X):
-            load_values(lm, x)
+            load_values(lm, x, vars_to_load)
 
 
 _REGISTRY = {"phg": PHGSolver}

@@ -219,3 +219,96 @@ def test_off_diagonal_quadratic_raises():
     d.objective = lambda: _O([(d.x, 1.0)], quadratic=[(d.x, d.y, 1.0)])
     with pytest.raises(ValueError, match="off-diagonal"):
         extract(d)
+
+
+class _Params:
+    pass
+
+
+class PHModel:
+    """ONE scenario model as the reference's PH keeps it for the whole run: built once, its PH terms
+    attached once (``attach_Ws_and_prox`` / ``attach_PH_to_objective``, ``phbase.py:621-760``) with
+    MUTABLE parameters on ``_mpisppy_model`` -- W, xbars, rho, W_on, prox_on -- that PH changes in
+    place between solves.  ``objective()`` is the expression evaluated with the parameters' current
+    values, expanded as ``generate_standard_repn(compute_values=True)`` expands it: linear part,
+    diagonal quadratics (``rho/2 x^2``), constant (``rho/2 xbar^2``); a max model subtracts the PH
+    terms (``phbase.py:757-760``).  ``solutions.load_from(results)`` loads by variable name, as
+    Pyomo's ``ModelSolutions.load_from`` does for a results object without a symbol map."""
+
+    def __init__(self, lm, rho0):
+        a = lm.arrays()
+        self.name = lm.name
+        self.vars = [_V(nm, None if not np.isfinite(lo) else lo, None if not np.isfinite(hi) else hi)
+                     for nm, lo, hi in zip(lm.column_names(), a["col_lo"], a["col_hi"])]
+        self.rows = []
+        for i in range(len(a["row_lo"])):
+            p0, p1 = a["rowptr"][i], a["rowptr"][i + 1]
+            lo, hi = a["row_lo"][i], a["row_hi"][i]
+            self.rows.append(_R(f"r{i}", [(self.vars[j], v) for j, v in zip(a["colidx"][p0:p1], a["vals"][p0:p1])],
+                                None if not np.isfinite(lo) else lo, None if not np.isfinite(hi) else hi))
+        self.cols = [v.col for nd in lm._mpisppy_node_list for v in nd.nonant_vardata_list]
+        self.sense = lm.sense
+        self._c, self._c0 = a["c"].copy(), lm.obj_offset
+        N = len(self.cols)
+        mm = _Params()
+        mm.W, mm.xbars, mm.rho = np.zeros(N), np.zeros(N), np.full(N, float(rho0))
+        mm.W_on, mm.prox_on = 0, 0
+        self._mpisppy_model = mm
+        self.solutions = self._Solutions(self)
+
+    class _Solutions:
+        def __init__(self, model):
+            self._model = model
+
+        def load_from(self, results):
+            if results.solver.status == "error":
+                raise ValueError("cannot load a solution with status error")
+            byname = {v.name: v for v in self._model.vars}
+            for nm, d in results.solution(0).variable.items():
+                byname[nm].value = d["Value"]
+
+    def variables(self):
+        return self.vars
+
+    def constraints(self):
+        return self.rows
+
+    def objective(self):
+        mm = self._mpisppy_model
+        sg = float(self.sense)          # objfct.expr += ph_term (min) / -= ph_term (max)
+        lin = {j: float(self._c[j]) for j in range(len(self._c))}
+        quad, const = [], float(self._c0)
+        for k, j in enumerate(self.cols):
+            lin[j] += sg * (mm.W_on * mm.W[k] - mm.prox_on * mm.rho[k] * mm.xbars[k])
+            quad.append((self.vars[j], self.vars[j], sg * mm.prox_on * mm.rho[k] / 2.0))
+            const += sg * mm.prox_on * mm.rho[k] / 2.0 * mm.xbars[k] ** 2
+        return _O([(self.vars[j], v) for j, v in lin.items()], constant=const, sense=self.sense, quadratic=quad)
+
+
+def test_objective_reread_follows_mutated_params():
+    """The plugin re-reads the objective of a model mutated in place (opt/extract.objective_of): the
+    same StandardForm, the PH parameters changed between reads -- what the reference's solve_one
+    hands a non-persistent plugin every iteration (spopt.py:184-187)."""
+    from mpisppy_amd.opt.extract import column_bounds_of, objective_of
+    m = farmer.scenario_creator("scen1", num_scens=3)
+    d = PHModel(m, 1.0)
+    sf = extract(d)
+    np.testing.assert_array_equal(sf.qdiag, 0.0)
+    np.testing.assert_allclose(sf.c, m.arrays()["c"])
+    mm = d._mpisppy_model
+    mm.W[:] = [1.0, -2.0, 0.5]
+    mm.xbars[:] = [100.0, 200.0, 150.0]
+    mm.rho[:] = [1.0, 2.0, 0.5]
+    mm.W_on = mm.prox_on = 1
+    c, q, c0, sense = objective_of(d, sf)
+    want = m.arrays()["c"].copy()
+    want[d.cols] += m.sense * (mm.W - mm.rho * mm.xbars)
+    np.testing.assert_allclose(c, want)
+    qq = np.zeros(sf.n)
+    qq[d.cols] = m.sense * mm.rho
+    np.testing.assert_allclose(q, qq)
+    assert c0 == pytest.approx(m.obj_offset + m.sense * float(np.sum(mm.rho / 2 * mm.xbars ** 2)))
+    assert sense == m.sense
+    d.vars[d.cols[0]].fixed, d.vars[d.cols[0]].value = True, 42.0
+    lo, hi = column_bounds_of(d, sf)
+    assert lo[d.cols[0]] == hi[d.cols[0]] == 42.0

@@ -20,7 +20,8 @@ from mpisppy_amd.utils.proper_bundler import ProperBundler  # noqa: E402
 from oracle import highs  # noqa: E402
 from oracle import models as om  # noqa: E402
 from oracle import ph as oph  # noqa: E402
-from test_bundles_extract import PHDuck, _Duck  # noqa: E402
+from mpisppy_amd.opt.phg import is_persistent  # noqa: E402
+from test_bundles_extract import PHDuck, PHModel, _Duck  # noqa: E402
 
 
 def _oracle_obj(m):
@@ -141,6 +142,144 @@ def test_reference_ph_loop_through_plugin_reproduces_w_file():
     for vname, xval in list(csv.reader(open(os.path.join(gold, "ref_xbar_file.csv"))))[:3]:
         assert abs(o.xbar[0, nonant_names.index(vname)] - float(xval)) < 5e-6
     o.plugin.close()
+
+
+def _not_good_enough_results(results):
+    """``sputils.not_good_enough_results`` (``sputils.py:29-34``) on the plugin's status values."""
+    return (results is None) or (len(results.solution) == 0) or \
+        (results.solution(0).status == "infeasible") or \
+        (results.solver.termination_condition in ("infeasible", "infeasibleOrUnbounded", "unbounded"))
+
+
+def spopt_solve_one(s, is_minimizing, persistent, update_objective=True, need_solution=True):
+    """``SPOpt.solve_one`` (``spopt.py:99-247``) restated line for line, minus timing, extensions and
+    bundles.  ``persistent`` picks the branch ``sputils.is_persistent(s._solver_plugin)`` picks:
+    ``set_objective`` + ``solve(save_results=False, load_solutions=False)`` + ``load_vars()``, or
+    ``solve(load_solutions=False)`` + ``s.solutions.load_from(results)``."""
+    if update_objective and persistent:                                   # :147-160
+        s._solver_plugin.set_objective(s.objective())
+    solve_keyword_args = dict()
+    if persistent:                                                        # :178-179
+        solve_keyword_args["save_results"] = False
+    try:                                                                  # :184-191
+        results = s._solver_plugin.solve(s, **solve_keyword_args, load_solutions=False)
+        solver_exception = None
+    except Exception as e:
+        results = None
+        solver_exception = e
+    if _not_good_enough_results(results):                                 # :194-214
+        s._mpisppy_data.scenario_feasible = False
+        if solver_exception is not None:
+            raise solver_exception
+    else:
+        try:                                                              # :217-224
+            if persistent:
+                s._solver_plugin.load_vars()
+            else:
+                s.solutions.load_from(results)
+        except Exception as e:
+            if need_solution:
+                raise e
+        if is_minimizing:                                                 # :225-230
+            s._mpisppy_data.outer_bound = results.Problem[0].Lower_bound
+            s._mpisppy_data.inner_bound = results.Problem[0].Upper_bound
+        else:
+            s._mpisppy_data.outer_bound = results.Problem[0].Upper_bound
+            s._mpisppy_data.inner_bound = results.Problem[0].Lower_bound
+        s._mpisppy_data.scenario_feasible = True
+    return results
+
+
+class _SolveOnePH(oph.OraclePH):
+    """The reference's PH (restated by the oracle) on ONE persistent model object per scenario
+    (``PHModel``: W / xbars / rho / W_on / prox_on mutable Params, mutated in place each iteration,
+    ``phbase.py:621-760``), one ``SolverFactory("phg")`` plugin per scenario (``_create_solvers``,
+    ``spopt.py:876-893``), every solve through :func:`spopt_solve_one`."""
+
+    def __init__(self, *a, persistent=True, **kw):
+        super().__init__(*a, **kw)
+        self.persistent = persistent
+        self.models = []
+        for nm in self.names:
+            s = PHModel(farmer.scenario_creator(nm, num_scens=self.S), self.options["defaultPHrho"])
+            s._mpisppy_data = type("D", (), {})()
+            s._solver_plugin = SolverFactory("phg")
+            if persistent:
+                s._solver_plugin.set_instance(s)                          # set_instance_retry
+            self.models.append(s)
+
+    def solve_one(self, k):
+        s = self.models[k]
+        mm = s._mpisppy_model       # PH's in-place updates of the mutable Params
+        mm.W[:] = self.W[k]
+        mm.xbars[:] = self.xbar[k]
+        mm.rho[:] = self.rho[k]
+        mm.W_on, mm.prox_on = self.W_on, self.prox_on
+        spopt_solve_one(s, self.is_minimizing, self.persistent)
+        assert s._mpisppy_data.scenario_feasible
+        self.x[k] = np.array([v.value for v in s.vars])
+        self.obj[k] = s._mpisppy_data.inner_bound if self.is_minimizing else s._mpisppy_data.outer_bound
+        self.outer[k] = s._mpisppy_data.outer_bound if self.is_minimizing else s._mpisppy_data.inner_bound
+        self.feasible[k] = True
+
+
+@pytest.mark.parametrize("persistent", [True, False])
+def test_reference_solve_one_on_mutated_models_reproduces_w_file(persistent):
+    """the plugin under the reference's exact calling convention -- the same model
+    object every iteration with its Params changed in place, ``solve(s, load_solutions=False)`` then
+    ``load_vars()`` (persistent) or ``s.solutions.load_from(results)`` -- reproduces the reference's
+    golden W / xbar files (farmer 3 scenarios, rho 1, 5 iterations; ``test_w_writer.py:83-112``) at
+    5e-6, with ONE engine load per plugin (no rebuild per solve)."""
+    import csv
+    import os
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    o = _SolveOnePH(dict(defaultPHrho=1.0, PHIterLimit=5, convthresh=1e-10), om.farmer_names(3), om.farmer,
+                    dict(crops_multiplier=1, num_scens=3), persistent=persistent)
+    assert is_persistent(o.models[0]._solver_plugin)
+    o.Iter0()
+    o.iterk_loop()
+    sc = om.farmer("scen0", num_scens=3)
+    nonant_names = [sc.colnames[c] for c in sc.nonant_cols()]
+    for sname, vname, wval in list(csv.reader(open(os.path.join(gold, "ref_w_file.csv"))))[:9]:
+        k, i = om.farmer_names(3).index(sname), nonant_names.index(vname)
+        assert abs(o.W[k, i] - float(wval)) < 5e-6, (sname, vname, o.W[k, i], wval)
+    for vname, xval in list(csv.reader(open(os.path.join(gold, "ref_xbar_file.csv"))))[:3]:
+        assert abs(o.xbar[0, nonant_names.index(vname)] - float(xval)) < 5e-6
+    for s in o.models:
+        assert s._solver_plugin.rebuilds == 1, s._solver_plugin.rebuilds
+        assert s._solver_plugin.solves == 6          # Iter0 + 5 PH iterations
+        s._solver_plugin.close()
+
+
+def test_plugin_rereads_fixed_bounds():
+    """``_fix_nonants`` fixes variables in place (``spopt.py:590-620``; a persistent plugin also gets
+    ``update_var``): the next solve honours the fixed values, the one after unfixing frees them
+    again (a bound change reloads the engine; the objective-only changes above do not)."""
+    m = farmer.scenario_creator("scen1", num_scens=3)
+    s = PHModel(m, 1.0)
+    opt = SolverFactory("phg")
+    r0 = opt.solve(s, load_solutions=True)
+    free_obj = r0.Problem[0].Upper_bound
+    x0 = np.array([v.value for v in s.vars])
+    fixv = x0[s.cols] * 0.9
+    for j, v in zip(s.cols, fixv):
+        s.vars[j].fixed, s.vars[j].value = True, float(v)
+        opt.update_var(s.vars[j])
+    r1 = opt.solve(s, load_solutions=True)
+    x1 = np.array([v.value for v in s.vars])
+    np.testing.assert_allclose(x1[s.cols], fixv, rtol=1e-9)
+    fm = farmer.scenario_creator("scen1", num_scens=3)
+    fm._lo = list(fm._lo)
+    fm._hi = list(fm._hi)
+    for j, v in zip(s.cols, fixv):
+        fm._lo[j] = fm._hi[j] = float(v)
+    assert r1.Problem[0].Upper_bound == pytest.approx(_oracle_obj(fm), rel=1e-7)
+    for j in s.cols:
+        s.vars[j].fixed = False
+    r2 = opt.solve(s, load_solutions=True)
+    assert r2.Problem[0].Upper_bound == pytest.approx(free_obj, rel=1e-7)
+    assert opt.rebuilds == 3
+    opt.close()
 
 
 def _ph(names, creator, kw, **extra):
