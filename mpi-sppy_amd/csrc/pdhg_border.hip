@@ -405,6 +405,9 @@ __global__ __launch_bounds__(NT) void pdhg_border_kernel(PdhgArgs a) {
             if (use_avg) products();   // exact products at the new point
         }
     }
+    // a scenario given up (a co-resident workgroup missing: the bounded wait expired) reports status 2;
+    // its x is NOT a consistent iterate -- columns without a linking-row entry may already have taken
+    // the next iteration's primal step -- and callers treat status 2 as a failed solve
     if (!alive) { st = 2; rel_final = NAN; }
 
     // ------------------------------------------------------------------ outputs
@@ -979,6 +982,9 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             if (use_avg) products();
         }
     }
+    // a scenario given up (a co-resident workgroup missing: the bounded wait expired) reports status 2;
+    // its x is NOT a consistent iterate -- columns without a linking-row entry may already have taken
+    // the next iteration's primal step -- and callers treat status 2 as a failed solve
     if (!alive) { st = 2; rel_final = NAN; }
 
     // ------------------------------------------------------------------ outputs

@@ -305,7 +305,8 @@ static int carry_flushed_partials(phg_handle* h, double* dst) {
     if (!h->flushed_partials) return 0;
     h->flushed_partials = false;
     if (!dst || dst == h->convpart) return 0;
-    CK(hipMemcpyAsync(dst, h->convpart, (2 * (size_t)h->P + 2) * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    // the 2P+2 partials and the flag a W update sets (convpart[2P+2])
+    CK(hipMemcpyAsync(dst, h->convpart, (2 * (size_t)h->P + 3) * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     return 0;
 }
 

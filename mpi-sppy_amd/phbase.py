@@ -561,8 +561,10 @@ class PHBase(SPBase):
                     break
                 if self._time_over():
                     break
+                # nothing reads the bounds of the prox-QP solves inside the loop: no
+                # safe-bound pass, as in the pipelined form
                 self.solve_loop(solver_options=self.current_solver_options, dtiming=self.options["display_timing"],
-                                gripe=verbose, verbose=verbose)
+                                gripe=verbose, verbose=verbose, safe_bound=False)
             if self.extobject is not None:
                 self.extobject.enditer()
             if self.spcomm is not None:

@@ -93,7 +93,9 @@ def test_plugin_solves_ph_prox_objective(sense):
         pobj = res.Problem[0].Upper_bound if sense == 1 else -res.Problem[0].Lower_bound
         dbnd = res.Problem[0].Lower_bound if sense == 1 else -res.Problem[0].Upper_bound
         assert pobj == pytest.approx(oobj, rel=1e-7), (pobj, oobj)
-        assert dbnd <= pobj + 1e-9 * abs(pobj) and dbnd == pytest.approx(oobj, rel=1e-7)
+        # a weak-duality certificate: below the optimum (the oracle's, itself accurate to ~1e-9; the
+        # primal objective of a first-order iterate may sit eps below the optimum too)
+        assert dbnd <= oobj + 1e-8 * abs(oobj) and dbnd == pytest.approx(oobj, rel=1e-7)
         x = np.array([v.value for v in d.vars])
         np.testing.assert_allclose(x[d.cols], ox[d.cols], rtol=1e-6, atol=1e-6 * np.abs(ox).max())
     opt.close()

@@ -394,25 +394,25 @@ def test_folded_update_at_full_size_matches_unfolded(monkeypatch):
         assert np.array_equal(W, res[0][1]) and np.array_equal(xb, res[0][2]) and np.array_equal(x, res[0][3])
 
 
-@pytest.mark.parametrize("thr", [1e-10, 5e-2])
+@pytest.mark.parametrize("thr", [1e-10, 5.0])
 def test_field_read_between_head_and_solve_keeps_fold_trajectory(monkeypatch, thr):
     """ADVICE r3 (flush_fold): reading W between phg_ph_head and the solve applies the pending folded
     W update on its own.  With the exchange buffer (pdhg_exchange) its conv partials must reach that
     buffer (not be lost, leaving the already all-reduced ones to be summed again), and after a head
     that found conv below convthresh it must not move W.  The run with a W read after every head
-    (thr 5e-2: PH stops on convthresh) equals the run without: W, xbar, x bit for bit, conv to 1e-13."""
+    (thr 5: PH stops on convthresh at iteration ~14) equals the run without: W, xbar, x bit for bit, conv to 1e-13."""
     monkeypatch.setenv("PHG_FOLD", "1")
     res = []
     for peek in (False, True):
         ph = _farmer_ph(1000, cm=10, PHIterLimit=25, convthresh=thr, pdhg_exchange=True)
         if peek:
-            eng = ph.engine
-            head = eng.ph_head
+            from mpisppy_amd.engine import Engine
+            head = Engine.ph_head
 
-            def head_then_read(convthresh, first, head=head, eng=eng):
-                head(convthresh, first)
-                eng.get(_lib.F_W)
-            eng.ph_head = head_then_read
+            def head_then_read(self, convthresh, first, head=head):
+                head(self, convthresh, first)
+                self.get(_lib.F_W)
+            monkeypatch.setattr(Engine, "ph_head", head_then_read)
         ph.ph_main(finalize=False)
         res.append((list(ph.conv_history), ph.Ws().copy(), ph.xbars().copy(), ph.nonants().copy()))
     assert len(res[1][0]) == len(res[0][0])
