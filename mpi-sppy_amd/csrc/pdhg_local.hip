@@ -66,8 +66,11 @@ constexpr size_t local_lds_bytes() {
 // coefficients re-derived after every check instead of held across it, 168 registers with a few
 // prologue spills -- but measured on MI355X that is 0.345-0.350 ms per farmer-10k launch against
 // 0.342 ms at two waves (the kernel is VALU-issue-bound, not latency-bound), so two it is.
+#ifndef PHG_LOCAL_WAVES
+#define PHG_LOCAL_WAVES 2
+#endif
 template <int LPS, int CPL, int RPL, int D>
-constexpr int local_waves() { return 2; }
+constexpr int local_waves() { return PHG_LOCAL_WAVES; }
 
 // (xs dc) - xbar, each operation rounded on its own (the folded W update must see the bits of the
 // epilogue's xN = xs dc)
@@ -77,7 +80,19 @@ __device__ __forceinline__ double x_minus_xbar(double xs, double dc, double xbar
     return x - xbar;
 }
 
-template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC, unsigned long long BI>
+// The kernel argument block in the kernarg segment (constant address space: scalar loads).  The
+// prologue / epilogue read their pointers through kargs() at the use site -- the laundered pointer
+// keeps the compiler from hoisting those loads out of the work loop and holding ~40 pointers in
+// SGPRs across it (round 3: 167 SGPRs spilled to VGPR lanes, ~900 v_readlane in the prologue)
+typedef const __attribute__((address_space(4))) PdhgArgs* KP;
+__device__ __forceinline__ KP kargs() {
+    KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC, unsigned long long BI,
+          unsigned long long BF>
 __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
     constexpr int G = 64 / LPS;                    // scenarios per wave
@@ -89,8 +104,6 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     const int grp = lane / LPS;
     auto CS = [&](int item) -> double& { return cold[item * 64 + lane]; };
     auto GS = [&](int item) -> double& { return cold[CI::NL * 64 + grp * CI::NG + item]; };
-    const LocalLayout& L = a.loc;
-    const int* col_nonant = a.lay.col_nonant;
     // the primal step is x+ = clamp(x ip + A^T y tip - ctip) with ip = 1 / (1 + tau q),
     // tip = tau ip, ctip = c tip (re-derived whenever tau changes; c itself is read from LDS):
     // 2 instead of 3 fp64 ops per column, for 2 more registers per column -- only where they
@@ -104,7 +117,6 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
 
     // ------------------------------------------------------------------ per-group state
     int s = 0;                                     // scenario of the group's current work item
-    int cj[CPL];
     double x[CPL], aty[CPL], c[CPL], lo[CPL], hi[CPL], ip[CPL], tip[CPL], ctip[CPL], xsum[CPL];
     double y[RPL], ax[RPL], rlo[RPL], rhi[RPL], ysum[RPL];
     double blk[RPL][CPL];
@@ -113,7 +125,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     double cf[DD][CPL];
     double cft[FOLDT ? DD : 1][FOLDT ? CPL : 1];
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) { cj[k] = -1; x[k] = aty[k] = c[k] = lo[k] = hi[k] = ip[k] = tip[k] = ctip[k] = xsum[k] = 0.0; }
+    for (int k = 0; k < CPL; ++k) { x[k] = aty[k] = c[k] = lo[k] = hi[k] = ip[k] = tip[k] = ctip[k] = xsum[k] = 0.0; }
 #pragma unroll
     for (int r = 0; r < RPL; ++r) {
         y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
@@ -140,6 +152,15 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     // 48 + d, upper 52 + d.  Farmer: 5 of the 14 clamps per PDHG iteration (sold / purchased
     // quantities have no upper bound, every row one infinite side)
     auto binf = [](int bit) { return ((BI >> bit) & 1ull) != 0ull; };
+    // BF: bound sides FINITE in every occupied slot of every scenario (host-verified, local_fin_mask;
+    // rows that fixing the nonants frees never count).  fin_side(bit, v) is then a compile-time
+    // constant for every side in BI or BF -- the check's finiteness tests and their selects vanish
+    // (the same values: fin(v) is what they would have returned)
+    auto fin_side = [](int bit, double v) {
+        if (((BI >> bit) & 1ull) != 0ull) return false;
+        if (((BF >> bit) & 1ull) != 0ull) return true;
+        return fin(v);
+    };
     auto clampx = [&](int k, double v) {
         if (!binf(k)) v = vmax(v, lo[k]);
         if (!binf(16 + k)) v = vmin(v, hi[k]);
@@ -246,8 +267,8 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             pr2 += pr * pr;
             const double pu = pr * CS(CI::IDR + r);
             t[2] += pu * pu;
-            if (fin(bl)) t[5] += bl * fmax(yy, 0.0);
-            if (fin(bu)) t[5] += bu * fmin(yy, 0.0);
+            if (fin_side(32 + r, bl)) t[5] += bl * vmax(yy, 0.0);
+            if (fin_side(40 + r, bu)) t[5] += bu * vmin(yy, 0.0);
         }
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
@@ -257,15 +278,15 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             const double ck = FOLD ? CS(CI::C + k) : c[k];
             const double rc_ = ck + qk * xx - atf(k);
             double dres = 0.0;
-            if (!fin(lo[k]) && rc_ > 0.0) dres += rc_;
-            if (!fin(hi[k]) && rc_ < 0.0) dres += rc_;
+            if (!fin_side(k, lo[k]) && rc_ > 0.0) dres += rc_;
+            if (!fin_side(16 + k, hi[k]) && rc_ < 0.0) dres += rc_;
             dr2 += dres * dres;
             const double du = dres * CS(CI::IDC + k);
             t[3] += du * du;
             const double hq = 0.5 * qk * xx * xx;
             t[4] += ck * xx + hq;
-            if (fin(lo[k])) t[5] += lo[k] * fmax(rc_, 0.0);
-            if (fin(hi[k])) t[5] += hi[k] * fmin(rc_, 0.0);
+            if (fin_side(k, lo[k])) t[5] += lo[k] * vmax(rc_, 0.0);
+            if (fin_side(16 + k, hi[k])) t[5] += hi[k] * vmin(rc_, 0.0);
             t[5] -= hq;
         }
         t[0] = fma(GS(CI::SC + CI::W2), pr2, dr2 * GS(CI::SC + CI::IW2));
@@ -283,16 +304,18 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             t[0] = fma(GS(CI::SC + CI::W2), pr * pr, t[0]);
             const double pu = pr * GS(CI::IDRD + d);
             t[2] += pu * pu;
-            if (fin(bl)) t[5] += bl * fmax(yy, 0.0);
-            if (fin(bu)) t[5] += bu * fmin(yy, 0.0);
+            if (fin_side(48 + d, bl)) t[5] += bl * vmax(yy, 0.0);
+            if (fin_side(52 + d, bu)) t[5] += bu * vmin(yy, 0.0);
         }
     };
     // the current iterate (its coupling products are already reduced: lane 0 of the group
     // contributes them) and, with AVG, the average iterate: one group reduction for both
+    // the current iterate's coupling products are already group sums (axd): only its 5 other
+    // values go through the reduction (adding the other lanes' zeros would return axd unchanged)
     auto kkt_both = [&](bool avg, double inv, double* oc, double* oa) {
         double t[2 * KT];
         kkt_part([&](int k) { return x[k]; }, [&](int k) { return aty[k]; }, [&](int r) { return y[r]; },
-                 [&](int r) { return ax[r]; }, [&](int d) { return gl == 0 ? axd[d] : 0.0; }, t);
+                 [&](int r) { return ax[r]; }, [&](int d) { return 0.0; }, t);
         if (avg) {
             kkt_part([&](int k) { return xsum[k] * inv; },
                      [&](int k) {
@@ -302,10 +325,20 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                      [&](int r) { return brow(r, [&](int k) { return xsum[k]; }) * inv; },
                      [&](int d) { return crow(d, [&](int k) { return xsum[k]; }); },
                      t + KT);
-            gsum_many<LPS, 2 * KT>(t);
+            double u[5 + KT] = {t[0], t[2], t[3], t[4], t[5]};
+#pragma unroll
+            for (int q = 0; q < KT; ++q) u[5 + q] = t[KT + q];
+            gsum_many<LPS, 5 + KT>(u);
+            t[0] = u[0]; t[2] = u[1]; t[3] = u[2]; t[4] = u[3]; t[5] = u[4];
+#pragma unroll
+            for (int q = 0; q < KT; ++q) t[KT + q] = u[5 + q];
         } else {
-            gsum_many<LPS, KT>(*reinterpret_cast<double(*)[KT]>(t));
+            double u[5] = {t[0], t[2], t[3], t[4], t[5]};
+            gsum_many<LPS, 5>(u);
+            t[0] = u[0]; t[2] = u[1]; t[3] = u[2]; t[4] = u[3]; t[5] = u[4];
         }
+#pragma unroll
+        for (int d = 0; d < D; ++d) t[cslot(d)] = axd[d];
         kkt_coupling(t, [&](int d) { return yd[d]; }, 1.0);
 #pragma unroll
         for (int u = 0; u < 6; ++u) oc[u] = t[u];
@@ -334,106 +367,162 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     };
 
     // ------------------------------------------------------------------ load one scenario
-    // (the group's lanes only; everything the iteration and the checks read is (re)initialised)
+    // (the group's lanes only; everything the iteration and the checks read is (re)initialised).
+    // Branch-free: the constant data comes from the lane image (coalesced, no index chain), the
+    // slot tables give the columns / rows / nonants of the dynamic data (warm start, W, rho, xbar),
+    // read at clamped indices and masked, so every load of the scenario is in flight at once.  The
+    // arithmetic is the round-3 prologue's, operation for operation (the same bits).
+    constexpr int I_DC = 0, I_C = CPL, I_CL = 2 * CPL, I_CU = 3 * CPL, I_IDR = 4 * CPL, I_RL = 4 * CPL + RPL,
+                  I_RU = 4 * CPL + 2 * RPL, I_B = 4 * CPL + 3 * RPL;
+    constexpr int NB = __builtin_popcount(MB);
+    auto bidx = [](int r, int k) { return __builtin_popcount(MB & ((1u << (r * CPL + k)) - 1u)); };
+    auto cidx = [](int d, int k) { return __builtin_popcount(MC & ((1u << (d * CPL + k)) - 1u)); };
     auto load = [&](int sc) {
         s = sc;
-        const long sn = (long)s * a.n, sN = (long)s * a.N;
+        KP ka = kargs();
+        const int n_ = ka->n, m_ = ka->m, N_ = ka->N, warm = ka->warm, fold = ka->fold_w;
+        const long sn = (long)s * n_, sm = (long)s * m_, sN = (long)s * N_;
+        const double* img = ka->loc.img + (long)s * ka->loc.ni * LPS + gl;
+        const bool wx = (warm & 1) || fold;
+        // slot tables
+        int jj[CPL], kq[CPL], ii[RPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            jj[k] = ka->loc.col_of[gl * CPL + k];
+            kq[k] = ka->loc.slot_kk[gl * CPL + k];
+        }
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) ii[r] = ka->loc.row_of[gl * RPL + r];
+        // every load of the scenario
+        double dd[CPL], cc[CPL], lo_[CPL], hi_[CPL], xw[CPL], wv[CPL], rv[CPL], xb[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            dd[k] = img[(I_DC + k) * LPS];
+            cc[k] = img[(I_C + k) * LPS];
+            lo_[k] = img[(I_CL + k) * LPS];
+            hi_[k] = img[(I_CU + k) * LPS];
+            const long b = sn + (jj[k] >= 0 ? jj[k] : 0);
+            xw[k] = wx ? ka->xs_in[b] : 0.0;
+            const int kk = kq[k] >= 0 ? kq[k] : 0;
+            const long t = sN + kk;
+            wv[k] = ka->W[t];
+            rv[k] = ka->rho_k ? ka->rho_k[kk] : ka->rho[t];
+            xb[k] = ka->xbar[ka->root_only ? kk : ka->xidx[t]];
+        }
+        double idr[RPL], rl_[RPL], ru_[RPL], yw[RPL];
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            idr[r] = img[(I_IDR + r) * LPS];
+            rl_[r] = img[(I_RL + r) * LPS];
+            ru_[r] = img[(I_RU + r) * LPS];
+            yw[r] = (warm & 1) ? ka->ys_in[sm + (ii[r] >= 0 ? ii[r] : 0)] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < RPL; ++r)
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) blk[r][k] = bon(r, k) ? img[(I_B + bidx(r, k)) * LPS] : 0.0;
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) cf[d][k] = con(d, k) ? img[(I_B + NB + cidx(d, k)) * LPS] : 0.0;
+        double ci[DD][3], yc[DD];
+        int irow[DD];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const double* cim = ka->loc.cimg + ((long)s * D + d) * 3;
+            ci[d][0] = cim[0];
+            ci[d][1] = cim[1];
+            ci[d][2] = cim[2];
+            irow[d] = ka->loc.cpl_row[d];
+            yc[d] = (warm & 1) && irow[d] >= 0 ? ka->ys_in[sm + irow[d]] : 0.0;
+        }
+        // columns
         double prox_const = 0.0, c2 = 0.0, dsum = 0.0;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-            seq();
-            const int j = L.col_of[gl * CPL + k];
-            cj[k] = j;
-            x[k] = aty[k] = c[k] = lo[k] = hi[k] = xsum[k] = 0.0;
-            double qs = 0.0;
-            CS(CI::IDC + k) = 1.0;
-            if (j >= 0) {
-                const long b = sn + j;
-                const double dd = a.dc[b];
-                double cc = a.c[b], qq = 0.0;
-                double lo_ = a.cl[b], hi_ = a.cu[b];
-                const int kk = col_nonant[j];
-                if (kk >= 0) {
-                    const long t = sN + kk;
-                    double w = a.W[t];
-                    if (a.fold_w) {   // Update_W (phbase.py:301-326) of the x this solve starts from
-                        // the epilogue's xN = xs * dc, rounded as it was: x - xbar without FMA
-                        // contraction (__dmul_rn / __dsub_rn alone are plain IR operations the
-                        // optimiser fused into fma(xs, dc, -xbar), 1 ulp off the two-launch update)
-                        const double dv = x_minus_xbar(a.xs_in[b], dd, a.xbar[xbar_slot(a, t, kk)]);
-                        w = fma(rho_of(a, t, kk), dv, w);
-                        a.W_rw[t] = w;
-                        dsum += fabs(dv);
+            const bool occ = jj[k] >= 0;
+            const double d = dd[k];
+            double c_ = cc[k], qq = 0.0, clo = lo_[k], chi = hi_[k];
+            const double xs0 = occ ? xw[k] : 0.0;
+            if (kq[k] >= 0) {
+                const long t = sN + kq[k];
+                double w = wv[k];
+                const double r_ = rv[k], xbv = xb[k];
+                if (fold) {   // Update_W (phbase.py:301-326) of the x this solve starts from
+                    // the epilogue's xN = xs * dc, rounded as it was: x - xbar without FMA contraction
+                    const double dv = x_minus_xbar(xs0, d, xbv);
+                    w = fma(r_, dv, w);
+                    ka->W_rw[t] = w;
+                    dsum += fabs(dv);
+                }
+                // ph_terms_w (phg_internal.h) on the preloaded rho / xbar, the same operations
+                if (ka->w_on) c_ += w;
+                if (ka->prox_on) {
+                    c_ -= r_ * xbv;
+                    qq = r_;
+                    prox_const += 0.5 * r_ * xbv * xbv;
+                    if (ka->smooth_on) {
+                        const double p = ka->Psm[t], z = ka->Z[t];
+                        c_ -= p * z;
+                        qq += p;
+                        prox_const += 0.5 * p * z * z;
                     }
-                    ph_terms_w(a, t, kk, w, cc, qq, prox_const);
-                    if (a.fix_nonants) fixed_box(a, t, dd, lo_, hi_);
                 }
-                c2 += cc * cc;
-                CS(CI::IDC + k) = 1.0 / dd;
-                c[k] = cc * dd;
-                qs = qq * dd * dd;
-                lo[k] = lo_;
-                hi[k] = hi_;
-                x[k] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
+                if (ka->fix_nonants) {
+                    const double v = ka->fixed[t];
+                    const double wd = ka->fix_tol * fmax(1.0, fabs(v));
+                    clo = (v - wd) / d;
+                    chi = (v + wd) / d;
+                }
             }
+            c2 += c_ * c_;
+            CS(CI::IDC + k) = occ ? 1.0 / d : 1.0;
+            c[k] = c_ * d;
+            lo[k] = clo;
+            hi[k] = chi;
+            x[k] = clampd((warm & 1) ? xs0 : 0.0, clo, chi);
+            xsum[k] = aty[k] = 0.0;
             CS(CI::XR + k) = x[k];
-            CS(CI::Q + k) = qs;
+            CS(CI::Q + k) = qq * d * d;
         }
+        // rows
         double b2 = 0.0;
-        {
-            const long sm = (long)s * a.m, snz = (long)s * a.nnz;
 #pragma unroll
-            for (int r = 0; r < RPL; ++r) {
-                seq();
-                const int i = L.row_of[gl * RPL + r];
-                y[r] = ax[r] = rlo[r] = rhi[r] = ysum[r] = 0.0;
-                CS(CI::IDR + r) = 0.0;
-                if (i >= 0) {
-                    const long b = sm + i;
-                    CS(CI::IDR + r) = 1.0 / a.dr[b];
-                    row_bounds(a, i, b, rlo[r], rhi[r]);
-                    double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
-                    if (!fin(rlo[r])) yy = fmin(yy, 0.0); else b2 += rlo[r] * rlo[r];
-                    if (!fin(rhi[r])) yy = fmax(yy, 0.0); else b2 += rhi[r] * rhi[r];
-                    y[r] = yy;
-                }
-                CS(CI::YR + r) = y[r];
-                CS(CI::BLO + r) = rlo[r];
-                CS(CI::BHI + r) = rhi[r];
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int p = L.blk_p[(gl * RPL + r) * CPL + k];
-                    blk[r][k] = p >= 0 ? a.vals[snz + p] : 0.0;
-                }
-            }
+        for (int r = 0; r < RPL; ++r) {
+            const bool occ = ii[r] >= 0;
+            double lo = rl_[r], hi = ru_[r];
+            if (ka->fix_nonants && occ && ka->row_fixed && ka->row_fixed[ii[r]]) { lo = -INFINITY; hi = INFINITY; }
+            double yy = occ ? yw[r] : 0.0;
+            if (!fin_side(32 + r, lo)) yy = fmin(yy, 0.0); else b2 += lo * lo;
+            if (!fin_side(40 + r, hi)) yy = fmax(yy, 0.0); else b2 += hi * hi;
+            y[r] = yy;
+            ax[r] = ysum[r] = 0.0;
+            rlo[r] = lo;
+            rhi[r] = hi;
+            CS(CI::IDR + r) = idr[r];
+            CS(CI::YR + r) = y[r];
+            CS(CI::BLO + r) = lo;
+            CS(CI::BHI + r) = hi;
         }
         double b2d = 0.0;
-        {
-            const long sm = (long)s * a.m, snz = (long)s * a.nnz;
 #pragma unroll
-            for (int d = 0; d < D; ++d) {
-                seq();
-                const int i = L.cpl_row[d];
-                yd[d] = axd[d] = dlo[d] = dhi[d] = ydsum[d] = 0.0;
-                GS(CI::IDRD + d) = 0.0;
-                if (i >= 0) {
-                    const long b = sm + i;
-                    GS(CI::IDRD + d) = 1.0 / a.dr[b];
-                    row_bounds(a, i, b, dlo[d], dhi[d]);
-                    double yy = (a.warm & 1) ? a.ys_in[b] : 0.0;
-                    if (!fin(dlo[d])) yy = fmin(yy, 0.0); else b2d += dlo[d] * dlo[d];
-                    if (!fin(dhi[d])) yy = fmax(yy, 0.0); else b2d += dhi[d] * dhi[d];
-                    yd[d] = yy;
-                }
-                GS(CI::YDR + d) = yd[d];
-                GS(CI::DLO + d) = dlo[d];
-                GS(CI::DHI + d) = dhi[d];
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const int p = L.cpl_p[(d * LPS + gl) * CPL + k];
-                    cf[d][k] = p >= 0 ? a.vals[snz + p] : 0.0;
-                }
+        for (int d = 0; d < D; ++d) {
+            const bool occ = irow[d] >= 0;
+            double lo = ci[d][1], hi = ci[d][2];
+            if (ka->fix_nonants && occ && ka->row_fixed && ka->row_fixed[irow[d]]) { lo = -INFINITY; hi = INFINITY; }
+            double yy = yc[d];
+            if (occ) {
+                if (!fin_side(48 + d, lo)) yy = fmin(yy, 0.0); else b2d += lo * lo;
+                if (!fin_side(52 + d, hi)) yy = fmax(yy, 0.0); else b2d += hi * hi;
             }
+            yd[d] = yy;
+            axd[d] = ydsum[d] = 0.0;
+            dlo[d] = lo;
+            dhi[d] = hi;
+            GS(CI::IDRD + d) = ci[d][0];
+            GS(CI::YDR + d) = yd[d];
+            GS(CI::DLO + d) = lo;
+            GS(CI::DHI + d) = hi;
         }
         // ||c'|| (unscaled, incl. PH terms), prox constant, initial primal weight ||c_hat||/||b_hat||
         {
@@ -441,24 +530,25 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
 #pragma unroll
             for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
             gsum_many<LPS, 5>(rr);
-            if (a.fold_w && gl == 0) {
-                a.conv_s[s] = rr[4];
-                a.fold_st[s] = a.status_in[s];
+            if (fold && gl == 0) {
+                ka->conv_s[s] = rr[4];
+                ka->fold_st[s] = ka->status_in[s];
             }
             rr[3] += b2d;
             GS(CI::SC + CI::CNORM) = sqrt(rr[0]);
             GS(CI::SC + CI::PROX) = rr[1];
-            GS(CI::SC + CI::KOFF) = a.gap_const ? a.obj_off[s] + (a.prox_on ? rr[1] : 0.0) : 0.0;
+            GS(CI::SC + CI::KOFF) = ka->gap_const ? ka->obj_off[s] + (ka->prox_on ? rr[1] : 0.0) : 0.0;
             const double cn = sqrt(rr[2]), bn = sqrt(rr[3]);
             omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
-            if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
-            else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);   // blend
+            const double om_in = (warm & 6) ? ka->omega_in[s] : 0.0;
+            if ((warm & 2) && om_in > 0.0) omega = om_in;
+            else if ((warm & 4) && om_in > 0.0) omega = sqrt(omega * om_in);   // blend
         }
-        const double eta = a.eta[s];
-        GS(CI::SC + CI::BNORM) = a.bnorm[s];
+        const double eta = ka->eta[s], bnorm = ka->bnorm[s];
+        GS(CI::SC + CI::BNORM) = bnorm;
         GS(CI::SC + CI::ETA) = eta;
         {
-            const double tp = a.eps * (1.0 + a.bnorm[s]), td = a.eps * (1.0 + GS(CI::SC + CI::CNORM));
+            const double tp = ka->eps * (1.0 + bnorm), td = ka->eps * (1.0 + GS(CI::SC + CI::CNORM));
             GS(CI::SC + CI::TP) = tp * tp;
             GS(CI::SC + CI::TD) = td * td;
         }
@@ -486,52 +576,56 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
 
     // epilogue of a group that has terminated (st 0 optimal, 1 iteration limit, 2 NaN)
     auto finish = [&](bool use_avg, double inv, double rel, double pobj, double dobj, int st) {
+        KP ka = kargs();
         const int sl = launder(s);
-        const long sn = (long)sl * a.n, sm = (long)sl * a.m, sN = (long)sl * a.N;
+        const long sn = (long)sl * ka->n, sm = (long)sl * ka->m, sN = (long)sl * ka->N;
+        const double* img = ka->loc.img + (long)sl * ka->loc.ni * LPS + gl;
+        double* xo = ka->x_out;
+        double* yo = ka->y_out;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-            seq();
-            const int j = launder(cj[k]);
+            const int j = ka->loc.col_of[gl * CPL + k];
+            const int kk = ka->loc.slot_kk[gl * CPL + k];
+            const double dcv = img[(I_DC + k) * LPS];
             if (j >= 0) {
                 const long b = sn + j;
                 const double xv = use_avg ? xsum[k] * inv : x[k];
-                a.xs[b] = xv;
-                const double xu = xv * a.dc[b];
-                if (a.x_out) a.x_out[b] = xu;
-                const int kk = col_nonant[j];
-                if (kk >= 0) a.xN[sN + kk] = xu;
+                ka->xs[b] = xv;
+                const double xu = xv * dcv;
+                if (xo) xo[b] = xu;
+                if (kk >= 0) ka->xN[sN + kk] = xu;
             }
         }
 #pragma unroll
         for (int r = 0; r < RPL; ++r) {
-            seq();
-            const int i = L.row_of[gl * RPL + r];
+            const int i = ka->loc.row_of[gl * RPL + r];
             if (i >= 0) {
                 const long b = sm + i;
                 const double yv = use_avg ? ysum[r] * inv : y[r];
-                a.ys[b] = yv;
-                if (a.y_out) a.y_out[b] = yv * a.dr[b];
+                ka->ys[b] = yv;
+                if (yo) yo[b] = yv * ka->dr[b];
             }
         }
         if (gl == 0) {
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                const int i = L.cpl_row[d];
+                const int i = ka->loc.cpl_row[d];
                 if (i >= 0) {
                     const long b = sm + i;
                     const double yv = use_avg ? ydsum[d] * inv : yd[d];
-                    a.ys[b] = yv;
-                    if (a.y_out) a.y_out[b] = yv * a.dr[b];
+                    ka->ys[b] = yv;
+                    if (yo) yo[b] = yv * ka->dr[b];
                 }
             }
-            const double offs = a.obj_off[sl] + (a.prox_on ? GS(CI::SC + CI::PROX) : 0.0);
-            a.omega[sl] = GS(CI::SC + CI::OMEGA);
-            a.obj[sl] = a.sense * (pobj + offs);
-            a.bound[sl] = a.sense * (dobj + offs);
-            a.kkt[sl] = rel;
-            a.iters[sl] = it;
-            a.iters_acc[sl] += it;
-            a.status[sl] = st;
+            const double offs = ka->obj_off[sl] + (ka->prox_on ? GS(CI::SC + CI::PROX) : 0.0);
+            const double sg = ka->sense;
+            ka->omega[sl] = GS(CI::SC + CI::OMEGA);
+            ka->obj[sl] = sg * (pobj + offs);
+            ka->bound[sl] = sg * (dobj + offs);
+            ka->kkt[sl] = rel;
+            ka->iters[sl] = it;
+            ka->iters_acc[sl] += it;
+            ka->status[sl] = st;
         }
     };
 
@@ -553,6 +647,8 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     // PdhgArgs::prof: cycles in the PDHG iterations, in the checks (of which the KKT part and the
     // restart block), in loads; checks (uniform per wave)
     unsigned long long pf_it = 0, pf_chk = 0, pf_load = 0, pf_n = 0, pf_t1 = 0, pf_kkt = 0, pf_rst = 0;
+    // and the wave's start / end on the 100 MHz constant clock (s_memrealtime): the occupancy timeline
+    const unsigned long long pf_w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
     for (;;) {
         unsigned long long pf_t0 = 0;
         if (a.prof) {
@@ -564,7 +660,8 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             if (need) {
                 const int w = fetch();
                 if (w < a.S) {
-                    load(a.order ? a.order[w] : w);
+                    const int* ord = kargs()->order;
+                    load(ord ? ord[w] : w);
                     live = true;
                 } else {
                     valid = false;
@@ -759,9 +856,10 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         }
         if (a.prof) pf_rst += clock64() - pf_r0;
     }
-    if (a.prof && lane < 6) {   // (lane-indexed: a vector store)
+    if (a.prof && lane < 8) {   // (lane-indexed: a vector store)
+        const unsigned long long pf_w1 = __builtin_amdgcn_s_memrealtime();
         const unsigned long long v = lane == 0 ? pf_it : lane == 1 ? pf_chk : lane == 2 ? pf_load : lane == 3 ? pf_kkt
-                                   : lane == 4 ? pf_rst : pf_n;
+                                   : lane == 4 ? pf_rst : lane == 5 ? pf_n : lane == 6 ? pf_w0 : pf_w1;
         a.prof[(size_t)blockIdx.x * 8 + lane] = v;
     }
     if constexpr (PERSIST) {
@@ -777,24 +875,79 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     }
 }
 
+// ----------------------------------------------------------------------------- lane image
+// LocalLayout::img / cimg of a batch (phg_load_batch, after prep_kernel has scaled it): one
+// workgroup per scenario; the item order is the kernel's (I_DC ... I_B, then the MB / MC entries in
+// slot order).  Empty slots: dc 1, everything else 0.
+__global__ __launch_bounds__(256) void local_image_kernel(PdhgArgs a, int LPS, int CPL, int RPL, int D, unsigned MB,
+                                                          unsigned MC, double* img, double* cimg) {
+    const int s = blockIdx.x;
+    const int NB = __builtin_popcount(MB), NC = __builtin_popcount(MC);
+    const int ni = 4 * CPL + 3 * RPL + NB + NC;
+    const long sn = (long)s * a.n, sm = (long)s * a.m, snz = (long)s * a.nnz;
+    const LocalLayout& L = a.loc;
+    for (int e = threadIdx.x; e < ni * LPS; e += 256) {
+        const int item = e / LPS, gl = e % LPS;
+        double v = 0.0;
+        if (item < 4 * CPL) {
+            const int f = item / CPL, k = item % CPL;
+            const int j = L.col_of[gl * CPL + k];
+            if (j < 0) v = f == 0 ? 1.0 : 0.0;
+            else v = f == 0 ? a.dc[sn + j] : f == 1 ? a.c[sn + j] : f == 2 ? a.cl[sn + j] : a.cu[sn + j];
+        } else if (item < 4 * CPL + 3 * RPL) {
+            const int f = (item - 4 * CPL) / RPL, r = (item - 4 * CPL) % RPL;
+            const int i = L.row_of[gl * RPL + r];
+            if (i >= 0) v = f == 0 ? 1.0 / a.dr[sm + i] : f == 1 ? a.rl[sm + i] : a.ru[sm + i];
+        } else {
+            int q = item - (4 * CPL + 3 * RPL);
+            const bool cpl = q >= NB;
+            unsigned msk = cpl ? MC : MB;
+            if (cpl) q -= NB;
+            for (int u = 0; u < q; ++u) msk &= msk - 1u;   // drop the q lowest set bits
+            const int bit = __builtin_ctz(msk);
+            const int k = bit % CPL, rd = bit / CPL;
+            const int p = cpl ? L.cpl_p[(rd * LPS + gl) * CPL + k] : L.blk_p[(gl * RPL + rd) * CPL + k];
+            if (p >= 0) v = a.vals[snz + p];
+        }
+        img[((long)s * ni + item) * LPS + gl] = v;
+    }
+    if (threadIdx.x < 3 * D) {
+        const int d = threadIdx.x / 3, f = threadIdx.x % 3;
+        const int i = L.cpl_row[d];
+        double v = 0.0;
+        if (i >= 0) v = f == 0 ? 1.0 / a.dr[sm + i] : f == 1 ? a.rl[sm + i] : a.ru[sm + i];
+        cimg[((long)s * D + d) * 3 + f] = v;
+    }
+}
+
+// items per lane of variant v's image (LocalLayout::ni)
+int pdhg_local_image_items(int v);
+
+hipError_t pdhg_local_image_launch(int v, const PdhgArgs& a, double* img, double* cimg, hipStream_t stream);
+
 // ----------------------------------------------------------------------------- dispatch
 struct LocalVariant {
     int LPS, CPL, RPL, D;
     unsigned MB, MC;           // compiled-in block / coupling slot masks (all ones: generic)
     unsigned long long BI;     // compiled-in infinite bound sides (0: generic)
+    unsigned long long BF;     // compiled-in finite bound sides (0: tested at run time)
     size_t lds;                // dynamic LDS per wave (Cold layout)
     void (*fn)(PdhgArgs);
     void (*fn_persist)(PdhgArgs);
 };
 
-#define PHG_LM(a_, b_, c_, d_, mb_, mc_, bi_)                                                   \
-    {a_, b_, c_, d_, mb_, mc_, bi_, local_lds_bytes<a_, b_, c_, d_>(),                             \
-     pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_, bi_>,                                      \
-     pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_, bi_>}
-#define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u, 0ull)
+#define PHG_LM(a_, b_, c_, d_, mb_, mc_, bi_, bf_)                                              \
+    {a_, b_, c_, d_, mb_, mc_, bi_, bf_, local_lds_bytes<a_, b_, c_, d_>(),                        \
+     pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_, bi_, bf_>,                                 \
+     pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_, bi_, bf_>}
+#define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u, 0ull, 0ull)
 // farmer's infinite sides: columns 2, 3 (QuantitySuperQuotaSold, QuantityPurchased) above; row 0
 // (cattle feed, >=) above, row 1 (limit sold, <= 0) below; the total-acreage row (<=) below
 #define PHG_FARMER_BI ((1ull << 18) | (1ull << 19) | (1ull << 40) | (1ull << 33) | (1ull << 48))
+// farmer's finite sides (local_fin_mask): every column lower bound, DevotedAcreage / SubQuota upper
+// bounds, the cattle-feed row's lower and the limit-sold row's upper side (the acreage coupling row
+// is freed when the nonants are fixed, so it stays a run-time test)
+#define PHG_FARMER_BF 0x2010003000full
 // shapes ordered by preference: fewest lanes per scenario first, then smallest register footprint;
 // the generic kernel of every shape first, then pattern-specialised ones
 static const LocalVariant kLocalVariants[] = {
@@ -810,15 +963,20 @@ static const LocalVariant kLocalVariants[] = {
     // farmer (examples/farmer/farmer.py:157-203): per crop lane, columns DevotedAcreage, SubQuota,
     // SuperQuota, Purchased; rows cattle feed (all four) and limit sold (no Purchased); the
     // total-acreage coupling row on DevotedAcreage only
-    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, 0ull),
-    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, 0ull),
-    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, 0ull),
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull),
     // ... and its infinite bound sides
-    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI),
-    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI),
-    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI),
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull),
+    // ... and its finite ones
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF),
 };
 #undef PHG_FARMER_BI
+#undef PHG_FARMER_BF
 #undef PHG_L
 #undef PHG_LM
 constexpr int kLocalShapes = 9;   // the generic entries; the planner walks these
@@ -827,7 +985,7 @@ int pdhg_local_num_variants() { return kLocalShapes; }
 
 // the variant to run for shape v and the layout's slot masks: the specialised entry of that shape
 // with the fewest slots that still covers every occupied one, else the generic kernel
-int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi) {
+int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi, unsigned long long bf) {
     const LocalVariant& S0 = kLocalVariants[v];
     int best = v, bits = __builtin_popcount(S0.MB) + __builtin_popcount(S0.MC);
     int inf = 0;
@@ -836,8 +994,9 @@ int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long b
         const LocalVariant& V = kLocalVariants[u];
         if (V.LPS != S0.LPS || V.CPL != S0.CPL || V.RPL != S0.RPL || V.D != S0.D) continue;
         if ((mb & ~V.MB) || (mc & ~V.MC) || (V.BI & ~bi)) continue;   // every dropped clamp must be a no-op
+        if (V.BF & ~bf) continue;                                      // every side assumed finite must be
         const int b = __builtin_popcount(V.MB) + __builtin_popcount(V.MC);
-        const int f = __builtin_popcountll(V.BI);
+        const int f = __builtin_popcountll(V.BI) + __builtin_popcountll(V.BF);
         if (b < bits || (b == bits && f > inf)) { best = u; bits = b; inf = f; }
     }
     return best;
@@ -877,6 +1036,18 @@ hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream) {
     } else {
         hipLaunchKernelGGL(V.fn, dim3(grid), dim3(64), lds, stream, a);
     }
+    return hipGetLastError();
+}
+
+int pdhg_local_image_items(int v) {
+    const LocalVariant& V = kLocalVariants[v];
+    return 4 * V.CPL + 3 * V.RPL + __builtin_popcount(V.MB) + __builtin_popcount(V.MC);
+}
+
+hipError_t pdhg_local_image_launch(int v, const PdhgArgs& a, double* img, double* cimg, hipStream_t stream) {
+    const LocalVariant& V = kLocalVariants[v];
+    hipLaunchKernelGGL(local_image_kernel, dim3(a.S), dim3(256), 0, stream, a, V.LPS, V.CPL, V.RPL, V.D, V.MB, V.MC,
+                       img, cimg);
     return hipGetLastError();
 }
 

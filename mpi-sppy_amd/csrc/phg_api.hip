@@ -29,7 +29,9 @@ hipError_t prep_launch(const PrepArgs& a, hipStream_t stream);
 hipError_t schedule_launch(const int* iters, int S, int unit, int* order, hipStream_t st);
 int pdhg_local_num_variants();
 void pdhg_local_variant_shape(int v, int* out4);
-int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi);
+int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi, unsigned long long bf);
+int pdhg_local_image_items(int v);
+hipError_t pdhg_local_image_launch(int v, const PdhgArgs& a, double* img, double* cimg, hipStream_t stream);
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 int pdhg_block_num_variants();
@@ -739,6 +741,58 @@ static unsigned long long local_inf_mask(const phg_batch* b, const LocalPlan& P,
     return m;
 }
 
+// Bound sides that are FINITE in every occupied slot of every scenario (the kernel's restart /
+// termination check then tests them at compile time, pdhg_local.hip BF).  Fixing the nonants keeps a
+// finite column side finite (fixed_box); a row all of whose columns are nonants becomes free when
+// they are fixed (row_bounds), so such rows never count as finite here.  Same bit layout as BI.
+static unsigned long long local_fin_mask(const phg_batch* b, const LocalPlan& P, int LPS, int CPL, int RPL, int D) {
+    std::vector<char> isn(b->n, 0);
+    for (int k = 0; k < b->N; ++k) isn[b->nonant_col[k]] = 1;
+    auto all_fin = [&](const double* v, int stride, int idx) {
+        for (int s = 0; s < b->S; ++s)
+            if (!(std::fabs(v[(size_t)s * stride + idx]) < 1e300)) return false;
+        return true;
+    };
+    auto fixable = [&](int i) {   // every column of row i a nonant
+        for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
+            if (!isn[b->colidx[p]]) return false;
+        return b->rowptr[i + 1] > b->rowptr[i];
+    };
+    unsigned long long m = 0;
+    for (int k = 0; k < CPL && k < 16; ++k) {
+        bool lo = true, hi = true, any = false;
+        for (int l = 0; l < LPS; ++l) {
+            const int j = P.col_of[l * CPL + k];
+            if (j < 0) continue;
+            any = true;
+            lo = lo && all_fin(b->col_lo, b->n, j);
+            hi = hi && all_fin(b->col_hi, b->n, j);
+        }
+        if (any && lo) m |= 1ull << k;
+        if (any && hi) m |= 1ull << (16 + k);
+    }
+    for (int r = 0; r < RPL && r < 8; ++r) {
+        bool lo = true, hi = true, any = false;
+        for (int l = 0; l < LPS; ++l) {
+            const int i = P.row_of[l * RPL + r];
+            if (i < 0) continue;
+            any = true;
+            const bool fx = fixable(i);
+            lo = lo && !fx && all_fin(b->row_lo, b->m, i);
+            hi = hi && !fx && all_fin(b->row_hi, b->m, i);
+        }
+        if (any && lo) m |= 1ull << (32 + r);
+        if (any && hi) m |= 1ull << (40 + r);
+    }
+    for (int d = 0; d < D && d < 4; ++d) {
+        const int i = P.cpl_row[d];
+        if (i < 0 || fixable(i)) continue;
+        if (all_fin(b->row_lo, b->m, i)) m |= 1ull << (48 + d);
+        if (all_fin(b->row_hi, b->m, i)) m |= 1ull << (52 + d);
+    }
+    return m;
+}
+
 static void local_slot_masks(const LocalPlan& plan, const int* sh, unsigned* mb, unsigned* mc) {
     const int LPS = sh[0], CPL = sh[1], RPL = sh[2], D = sh[3];
     *mb = *mc = 0;
@@ -777,7 +831,8 @@ static int build_local_layout(phg_handle* h, const phg_batch* b) {
         // PHG_LOCAL_GENERIC=1 keeps the generic kernel (A/B of the specialisation)
         const char* gen = std::getenv("PHG_LOCAL_GENERIC");
         const unsigned long long bi = local_inf_mask(b, plan, LPS, CPL, RPL, D);
-        h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc, bi);
+        const unsigned long long bf = local_fin_mask(b, plan, LPS, CPL, RPL, D);
+        h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc, bi, bf);
         h->local_masks[0] = mb;
         h->local_masks[1] = mc;
         std::memcpy(h->lshape, sh, sizeof sh);
@@ -787,6 +842,13 @@ static int build_local_layout(phg_handle* h, const phg_batch* b) {
         if (dput(h, &p, plan.blk_p.data(), plan.blk_p.size())) return -1; h->loc.blk_p = p;
         if (dput(h, &p, plan.cpl_row.data(), plan.cpl_row.size())) return -1; h->loc.cpl_row = p;
         if (dput(h, &p, plan.cpl_p.data(), plan.cpl_p.size())) return -1; h->loc.cpl_p = p;
+        {   // nonant index of every column slot (the prologue's W / rho / xbar reads)
+            std::vector<int> col_nonant(b->n, -1), kk(plan.col_of.size(), -1);
+            for (int q = 0; q < b->N; ++q) col_nonant[b->nonant_col[q]] = q;
+            for (size_t e = 0; e < kk.size(); ++e)
+                if (plan.col_of[e] >= 0) kk[e] = col_nonant[plan.col_of[e]];
+            if (dput(h, &p, kk.data(), kk.size())) return -1; h->loc.slot_kk = p;
+        }
         return 0;
     }
     g_err = "phg_load_batch: the pattern has no lane-local layout (blocks too large or too many coupling rows)";
@@ -2003,7 +2065,12 @@ int phg_plan(const phg_batch* b_in, int32_t* out8) {
         out8[6] = lanes;
         unsigned mb, mc;
         local_slot_masks(plan, sh, &mb, &mc);
-        out8[7] = pdhg_local_pick_masked(v, mb, mc, local_inf_mask(b, plan, sh[0], sh[1], sh[2], sh[3]));
+        const unsigned long long bi = local_inf_mask(b, plan, sh[0], sh[1], sh[2], sh[3]);
+        const unsigned long long bf = local_fin_mask(b, plan, sh[0], sh[1], sh[2], sh[3]);
+        out8[7] = pdhg_local_pick_masked(v, mb, mc, bi, bf);
+        if (const char* e = std::getenv("PHG_LOCAL_DEBUG"); e && std::atoi(e))
+            fprintf(stderr, "phg_plan: shape %d x %d x %d x %d MB 0x%x MC 0x%x BI 0x%llx BF 0x%llx variant %d\n",
+                    sh[0], sh[1], sh[2], sh[3], mb, mc, bi, bf, out8[7]);
     }
     return 0;
 }
@@ -2229,6 +2296,20 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
         if (dput(h, &dp, ih.data(), ih.size())) return -1; sb.ihi = dp;
         sb.nf = (int)fc.size();
         if (dput(h, &ip, fc.data(), std::max<size_t>(1, fc.size()))) return -1; sb.free_col = ip;
+    }
+    if (h->local_variant >= 0) {   // the lane image of the scaled batch (LocalLayout::img)
+        const int ni = pdhg_local_image_items(h->local_variant);
+        const int D = std::max(1, h->lshape[3]);
+        double *img, *cimg;
+        if (dalloc(h, &img, (size_t)S * ni * h->lshape[0])) return -1;
+        if (dalloc(h, &cimg, (size_t)S * D * 3)) return -1;
+        PdhgArgs ia{};
+        ia.S = S; ia.n = n; ia.m = m; ia.nnz = nnz;
+        ia.loc = h->loc;
+        ia.dc = h->dc; ia.c = h->c; ia.cl = h->cl; ia.cu = h->cu; ia.dr = h->dr; ia.rl = h->rl; ia.ru = h->ru;
+        ia.vals = h->vals;
+        CK(pdhg_local_image_launch(h->local_variant, ia, img, cimg, h->stream));
+        h->loc.img = img; h->loc.cimg = cimg; h->loc.ni = ni;
     }
     if (h->block_variant >= 0 && build_block_values(h, raw)) return -1;
     if (raw) {
@@ -2456,11 +2537,41 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             std::vector<unsigned long long> hb(pcap);
             CK(hipMemcpyAsync(hb.data(), pbuf, pcap * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
             CK(hipStreamSynchronize(h->stream));
-            double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (size_t i = 0; i < pcap; ++i) t[i % 8] += (double)hb[i];
+            double t[6] = {0, 0, 0, 0, 0, 0};
+            for (size_t i = 0; i < pcap; ++i)
+                if (i % 8 < 6) t[i % 8] += (double)hb[i];
+            // occupancy timeline from the waves' start / end stamps (100 MHz): the launch span, the mean
+            // number of resident waves over it, and the span's last part with fewer than half the
+            // peak resident (the tail)
+            std::vector<std::pair<unsigned long long, int>> ev;
+            for (size_t w = 0; w * 8 + 7 < pcap; ++w)
+                if (hb[w * 8 + 7] > hb[w * 8 + 6] && hb[w * 8 + 6] > 0) {
+                    ev.push_back({hb[w * 8 + 6], +1});
+                    ev.push_back({hb[w * 8 + 7], -1});
+                }
+            std::sort(ev.begin(), ev.end());
+            double span = 0, area = 0, tail = 0;
+            int peak = 0;
+            if (!ev.empty()) {
+                int cur = 0;
+                for (auto& e : ev) peak = std::max(peak, cur += e.second);
+                cur = 0;
+                unsigned long long prev = ev[0].first, tail0 = 0;
+                for (auto& e : ev) {
+                    area += (double)cur * (double)(e.first - prev);
+                    const int before = cur;
+                    cur += e.second;
+                    if (before * 2 >= peak && cur * 2 < peak) tail0 = e.first;   // last drop below half
+                    if (cur * 2 >= peak) tail0 = 0;
+                    prev = e.first;
+                }
+                span = (double)(ev.back().first - ev[0].first);
+                tail = tail0 ? (double)(ev.back().first - tail0) : 0.0;
+            }
             fprintf(stderr,
                     "PHG_LOCAL_PROF iter_cycles %.6e check_cycles %.6e load_cycles %.6e kkt_cycles %.6e restart_cycles %.6e "
-                    "checks %.0f\n", t[0], t[1], t[2], t[3], t[4], t[5]);
+                    "checks %.0f span_us %.2f mean_resident %.1f peak_resident %d tail_below_half_us %.2f\n",
+                    t[0], t[1], t[2], t[3], t[4], t[5], span / 100.0, span > 0 ? area / span : 0.0, peak, tail / 100.0);
         }
     }
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));

@@ -37,6 +37,16 @@ struct LocalLayout {
     const int* blk_p;       // [LPS*RPL*CPL]  CSR position of entry (row slot, col slot) or -1
     const int* cpl_row;     // [D]            coupling rows (-1 = unused)
     const int* cpl_p;       // [D*LPS*CPL]    CSR position of coupling entry on (lane, col slot) or -1
+    // the scenario's constant data in lane order, built once per batch after the preconditioning
+    // (pdhg_local.hip local_image_kernel), so the prologue reads it with coalesced, index-free loads:
+    // img [S][ni][LPS]: per column slot dc, c (min form, unscaled), scaled lower / upper bound; per row
+    // slot 1/dr (0: empty slot), scaled lower / upper bound; the occupied block entries, then the
+    // occupied coupling entries (pattern masks MB / MC), scaled.  cimg [S][D][3]: per coupling row
+    // 1/dr, scaled lower / upper bound.  slot_kk [LPS*CPL]: nonant index of the slot's column (-1)
+    const double* img;
+    const double* cimg;
+    const int* slot_kk;
+    int ni;
 };
 
 // Workgroup-per-scenario layout (pdhg_block.hip).  Owner slots: column j -> (slot j / NT,
