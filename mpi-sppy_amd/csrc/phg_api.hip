@@ -1085,10 +1085,14 @@ static int build_block_layout(phg_handle* h, const phg_batch* b, const std::vect
         }
         return m > 0 ? slot + 1 : 1 << 20;
     };
+    // PHG_BLOCK_MINNT: skip the variants with fewer threads (A/B of the workgroup size)
+    const char* emn = std::getenv("PHG_BLOCK_MINNT");
+    const int min_nt = emn ? std::atoi(emn) : 0;
     int sh[12], chosen = -1;
     for (int v = 0; v < pdhg_block_num_variants(); ++v) {
         pdhg_block_variant_shape(v, sh);
         if (sh[10]) continue;   // unit twins: chosen by build_block_values
+        if (sh[0] < min_nt) continue;
         if (sh[11] && (seg_off || seg_plan(sh[0], sh[11] / 1) > sh[2])) continue;
         if ((sh[9] != 0) != psum && sh[9] != 0) continue;
         const int NT = sh[0], CPL = sh[1], RPL = sh[2], PPT = sh[3], QPT = sh[4], RE = sh[5], CE = sh[6], CL = sh[7];
