@@ -92,7 +92,7 @@ __device__ __forceinline__ KP kargs() {
 }
 
 template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC, unsigned long long BI,
-          unsigned long long BF>
+          unsigned long long BF, unsigned QM>
 __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
     constexpr int G = 64 / LPS;                    // scenarios per wave
@@ -174,8 +174,27 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         if (!binf(blo)) t = vmin(t, nlo);
         return g - t;
     };
-    // row r of the block times a column vector f(k) (first term a product, then FMAs)
+    // One-sided rows (compile time: one side in BF, the other in BI -- never a row the fixing of the
+    // nonants frees): the row's A x is held in offset form w = A x - b (b its finite bound), which the
+    // row sum forms for free (its FMA chain starts from -b, roff), so the dual step is
+    //   y+ = max(y - sig (2 w+ - w), 0)   (lower bound)  /  min(..., 0)  (upper bound)
+    // -- 3 instructions instead of 4 (the same projection; its roundings differ in the last bits)
+    auto one_lo = [&](int r) { return ((BF >> (32 + r)) & 1ull) && ((BI >> (40 + r)) & 1ull); };
+    auto one_hi = [&](int r) { return ((BF >> (40 + r)) & 1ull) && ((BI >> (32 + r)) & 1ull); };
+    auto one_sided = [&](int r) { return one_lo(r) || one_hi(r); };
+    double roff[RPL];
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) roff[r] = 0.0;
+    // row r of the block times a column vector f(k) (first term a product, then FMAs; one-sided rows
+    // in offset form: every term an FMA onto -b)
     auto brow = [&](int r, auto f) {
+        if (one_sided(r)) {
+            double acc = roff[r];
+#pragma unroll
+            for (int k = 0; k < CPL; ++k)
+                if (bon(r, k)) acc = fma(blk[r][k], f(k), acc);
+            return acc;
+        }
         double acc = 0.0;
         bool first = true;
 #pragma unroll
@@ -227,10 +246,14 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
 #pragma unroll
         for (int d = 0; d < D; ++d) { dlo[d] = -sig * GS(CI::DLO + d); dhi[d] = -sig * GS(CI::DHI + d); }
     };
+    // QM: the column slots that can carry a quadratic term (a nonant's prox / smoothing diagonal, set
+    // on the host from the slot tables); every other slot has q = 0 at compile time: ip = 1 without
+    // the division, no q terms in the checks (the same values: 1 / (1 + tau 0) = 1, q x = 0)
+    auto qon = [](int k) { return ((QM >> k) & 1u) != 0u; };
     auto step_coefs = [&]() {
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-            ip[k] = 1.0 / (1.0 + tau * CS(CI::Q + k));
+            ip[k] = qon(k) ? 1.0 / (1.0 + tau * CS(CI::Q + k)) : 1.0;
             if constexpr (FOLD) {
                 tip[k] = tau * ip[k];
                 ctip[k] = CS(CI::C + k) * tip[k];
@@ -263,7 +286,8 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             seq();
             const double axx = axf(r), yy = yf(r);
             const double bl = CS(CI::BLO + r), bu = CS(CI::BHI + r);
-            const double pr = axx - clampd(axx, bl, bu);
+            // (one-sided rows: axx is the offset form A x - b)
+            const double pr = one_lo(r) ? vmin(axx, 0.0) : one_hi(r) ? vmax(axx, 0.0) : axx - clampd(axx, bl, bu);
             pr2 += pr * pr;
             const double pu = pr * CS(CI::IDR + r);
             t[2] += pu * pu;
@@ -274,20 +298,20 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         for (int k = 0; k < CPL; ++k) {
             seq();
             const double xx = xf(k);
-            const double qk = CS(CI::Q + k);
+            const double qk = qon(k) ? CS(CI::Q + k) : 0.0;
             const double ck = FOLD ? CS(CI::C + k) : c[k];
-            const double rc_ = ck + qk * xx - atf(k);
+            const double rc_ = qon(k) ? ck + qk * xx - atf(k) : ck - atf(k);
             double dres = 0.0;
             if (!fin_side(k, lo[k]) && rc_ > 0.0) dres += rc_;
             if (!fin_side(16 + k, hi[k]) && rc_ < 0.0) dres += rc_;
             dr2 += dres * dres;
             const double du = dres * CS(CI::IDC + k);
             t[3] += du * du;
-            const double hq = 0.5 * qk * xx * xx;
-            t[4] += ck * xx + hq;
+            const double hq = qon(k) ? 0.5 * qk * xx * xx : 0.0;
+            t[4] += qon(k) ? ck * xx + hq : ck * xx;
             if (fin_side(k, lo[k])) t[5] += lo[k] * vmax(rc_, 0.0);
             if (fin_side(16 + k, hi[k])) t[5] += hi[k] * vmin(rc_, 0.0);
-            t[5] -= hq;
+            if (qon(k)) t[5] -= hq;
         }
         t[0] = fma(GS(CI::SC + CI::W2), pr2, dr2 * GS(CI::SC + CI::IW2));
 #pragma unroll
@@ -322,7 +346,11 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                          return bcol(k, [&](int r) { return ysum[r]; }, [&](int d) { return ydsum[d]; }) * inv;
                      },
                      [&](int r) { return ysum[r] * inv; },
-                     [&](int r) { return brow(r, [&](int k) { return xsum[k]; }) * inv; },
+                     [&](int r) {
+                         // (offset form on the one-sided rows, as the current iterate's ax)
+                         return one_sided(r) ? fma(brow(r, [&](int k) { return xsum[k]; }) - roff[r], inv, roff[r])
+                                             : brow(r, [&](int k) { return xsum[k]; }) * inv;
+                     },
                      [&](int d) { return crow(d, [&](int k) { return xsum[k]; }); },
                      t + KT);
             double u[5 + KT] = {t[0], t[2], t[3], t[4], t[5]};
@@ -499,6 +527,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             ax[r] = ysum[r] = 0.0;
             rlo[r] = lo;
             rhi[r] = hi;
+            roff[r] = one_lo(r) ? -lo : one_hi(r) ? -hi : 0.0;
             CS(CI::IDR + r) = idr[r];
             CS(CI::YR + r) = y[r];
             CS(CI::BLO + r) = lo;
@@ -582,43 +611,55 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         const double* img = ka->loc.img + (long)sl * ka->loc.ni * LPS + gl;
         double* xo = ka->x_out;
         double* yo = ka->y_out;
+        // every load first (tables, scaling), then the stores: a store may alias a later load, so
+        // interleaving them would serialise one round trip per element
+        int jj[CPL], kq[CPL], ii[RPL], irow[DD];
+        double dcv[CPL];
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-            const int j = ka->loc.col_of[gl * CPL + k];
-            const int kk = ka->loc.slot_kk[gl * CPL + k];
-            const double dcv = img[(I_DC + k) * LPS];
-            if (j >= 0) {
-                const long b = sn + j;
+            jj[k] = ka->loc.col_of[gl * CPL + k];
+            kq[k] = ka->loc.slot_kk[gl * CPL + k];
+            dcv[k] = img[(I_DC + k) * LPS];
+        }
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) ii[r] = ka->loc.row_of[gl * RPL + r];
+#pragma unroll
+        for (int d = 0; d < D; ++d) irow[d] = ka->loc.cpl_row[d];
+        const double offs = ka->obj_off[sl] + (ka->prox_on ? GS(CI::SC + CI::PROX) : 0.0);
+        const double sg = ka->sense;
+        double* xs_ = ka->xs;
+        double* xN_ = ka->xN;
+        double* ys_ = ka->ys;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            if (jj[k] >= 0) {
+                const long b = sn + jj[k];
                 const double xv = use_avg ? xsum[k] * inv : x[k];
-                ka->xs[b] = xv;
-                const double xu = xv * dcv;
+                xs_[b] = xv;
+                const double xu = xv * dcv[k];
                 if (xo) xo[b] = xu;
-                if (kk >= 0) ka->xN[sN + kk] = xu;
+                if (kq[k] >= 0) xN_[sN + kq[k]] = xu;
             }
         }
 #pragma unroll
         for (int r = 0; r < RPL; ++r) {
-            const int i = ka->loc.row_of[gl * RPL + r];
-            if (i >= 0) {
-                const long b = sm + i;
+            if (ii[r] >= 0) {
+                const long b = sm + ii[r];
                 const double yv = use_avg ? ysum[r] * inv : y[r];
-                ka->ys[b] = yv;
+                ys_[b] = yv;
                 if (yo) yo[b] = yv * ka->dr[b];
             }
         }
         if (gl == 0) {
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                const int i = ka->loc.cpl_row[d];
-                if (i >= 0) {
-                    const long b = sm + i;
+                if (irow[d] >= 0) {
+                    const long b = sm + irow[d];
                     const double yv = use_avg ? ydsum[d] * inv : yd[d];
-                    ka->ys[b] = yv;
+                    ys_[b] = yv;
                     if (yo) yo[b] = yv * ka->dr[b];
                 }
             }
-            const double offs = ka->obj_off[sl] + (ka->prox_on ? GS(CI::SC + CI::PROX) : 0.0);
-            const double sg = ka->sense;
             ka->omega[sl] = GS(CI::SC + CI::OMEGA);
             ka->obj[sl] = sg * (pobj + offs);
             ka->bound[sl] = sg * (dobj + offs);
@@ -706,8 +747,14 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
 #pragma unroll
             for (int r = 0; r < RPL; ++r) {
                 // y+ = max(g + sig lo, 0) + min(g + sig hi, 0) = g - clamp(g, -sig hi, -sig lo)
-                const double g = y[r] - sig * (2.0 * axn[r] - ax[r]);
-                y[r] = dproj(g, rhi[r], rlo[r], 32 + r, 40 + r);
+                if (one_lo(r)) {
+                    y[r] = vmax(fma(-sig, fma(2.0, axn[r], -ax[r]), y[r]), 0.0);
+                } else if (one_hi(r)) {
+                    y[r] = vmin(fma(-sig, fma(2.0, axn[r], -ax[r]), y[r]), 0.0);
+                } else {
+                    const double g = y[r] - sig * (2.0 * axn[r] - ax[r]);
+                    y[r] = dproj(g, rhi[r], rlo[r], 32 + r, 40 + r);
+                }
                 ax[r] = axn[r];
                 if constexpr (SUM) ysum[r] += y[r];
             }
@@ -931,16 +978,17 @@ struct LocalVariant {
     unsigned MB, MC;           // compiled-in block / coupling slot masks (all ones: generic)
     unsigned long long BI;     // compiled-in infinite bound sides (0: generic)
     unsigned long long BF;     // compiled-in finite bound sides (0: tested at run time)
+    unsigned QM;               // column slots that can hold a quadratic term (all ones: generic)
     size_t lds;                // dynamic LDS per wave (Cold layout)
     void (*fn)(PdhgArgs);
     void (*fn_persist)(PdhgArgs);
 };
 
-#define PHG_LM(a_, b_, c_, d_, mb_, mc_, bi_, bf_)                                              \
-    {a_, b_, c_, d_, mb_, mc_, bi_, bf_, local_lds_bytes<a_, b_, c_, d_>(),                        \
-     pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_, bi_, bf_>,                                 \
-     pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_, bi_, bf_>}
-#define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u, 0ull, 0ull)
+#define PHG_LM(a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_)                                         \
+    {a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_, local_lds_bytes<a_, b_, c_, d_>(),                   \
+     pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_, bi_, bf_, qm_>,                            \
+     pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_, bi_, bf_, qm_>}
+#define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u, 0ull, 0ull, (1u << b_) - 1u)
 // farmer's infinite sides: columns 2, 3 (QuantitySuperQuotaSold, QuantityPurchased) above; row 0
 // (cattle feed, >=) above, row 1 (limit sold, <= 0) below; the total-acreage row (<=) below
 #define PHG_FARMER_BI ((1ull << 18) | (1ull << 19) | (1ull << 40) | (1ull << 33) | (1ull << 48))
@@ -963,17 +1011,17 @@ static const LocalVariant kLocalVariants[] = {
     // farmer (examples/farmer/farmer.py:157-203): per crop lane, columns DevotedAcreage, SubQuota,
     // SuperQuota, Purchased; rows cattle feed (all four) and limit sold (no Purchased); the
     // total-acreage coupling row on DevotedAcreage only
-    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull),
-    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull),
-    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull),
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull, 0xFu),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull, 0xFu),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, 0ull, 0ull, 0xFu),
     // ... and its infinite bound sides
-    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull),
-    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull),
-    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull),
-    // ... and its finite ones
-    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF),
-    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF),
-    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF),
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull, 0xFu),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull, 0xFu),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull, 0xFu),
+    // ... its finite ones, and the nonant (DevotedAcreage) in column slot 0 only
+    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
+    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
+    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
 };
 #undef PHG_FARMER_BI
 #undef PHG_FARMER_BF
@@ -985,7 +1033,8 @@ int pdhg_local_num_variants() { return kLocalShapes; }
 
 // the variant to run for shape v and the layout's slot masks: the specialised entry of that shape
 // with the fewest slots that still covers every occupied one, else the generic kernel
-int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi, unsigned long long bf) {
+int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi, unsigned long long bf,
+                           unsigned qm) {
     const LocalVariant& S0 = kLocalVariants[v];
     int best = v, bits = __builtin_popcount(S0.MB) + __builtin_popcount(S0.MC);
     int inf = 0;
@@ -995,8 +1044,9 @@ int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long b
         if (V.LPS != S0.LPS || V.CPL != S0.CPL || V.RPL != S0.RPL || V.D != S0.D) continue;
         if ((mb & ~V.MB) || (mc & ~V.MC) || (V.BI & ~bi)) continue;   // every dropped clamp must be a no-op
         if (V.BF & ~bf) continue;                                      // every side assumed finite must be
+        if (qm & ~V.QM) continue;                                      // every quadratic slot kept
         const int b = __builtin_popcount(V.MB) + __builtin_popcount(V.MC);
-        const int f = __builtin_popcountll(V.BI) + __builtin_popcountll(V.BF);
+        const int f = __builtin_popcountll(V.BI) + __builtin_popcountll(V.BF) + (32 - __builtin_popcount(V.QM));
         if (b < bits || (b == bits && f > inf)) { best = u; bits = b; inf = f; }
     }
     return best;

@@ -29,7 +29,8 @@ hipError_t prep_launch(const PrepArgs& a, hipStream_t stream);
 hipError_t schedule_launch(const int* iters, int S, int unit, int* order, hipStream_t st);
 int pdhg_local_num_variants();
 void pdhg_local_variant_shape(int v, int* out4);
-int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi, unsigned long long bf);
+int pdhg_local_pick_masked(int v, unsigned mb, unsigned mc, unsigned long long bi, unsigned long long bf,
+                           unsigned qm);
 int pdhg_local_image_items(int v);
 hipError_t pdhg_local_image_launch(int v, const PdhgArgs& a, double* img, double* cimg, hipStream_t stream);
 void pdhg_local_variant_masks(int v, unsigned* out2);
@@ -793,6 +794,19 @@ static unsigned long long local_fin_mask(const phg_batch* b, const LocalPlan& P,
     return m;
 }
 
+// column slots holding a nonant in some lane (pdhg_local.hip QM: only they can carry a quadratic term)
+static unsigned local_quad_mask(const phg_batch* b, const LocalPlan& P, int LPS, int CPL) {
+    std::vector<char> isn(b->n, 0);
+    for (int k = 0; k < b->N; ++k) isn[b->nonant_col[k]] = 1;
+    unsigned m = 0;
+    for (int l = 0; l < LPS; ++l)
+        for (int k = 0; k < CPL && k < 32; ++k) {
+            const int j = P.col_of[l * CPL + k];
+            if (j >= 0 && isn[j]) m |= 1u << k;
+        }
+    return m;
+}
+
 static void local_slot_masks(const LocalPlan& plan, const int* sh, unsigned* mb, unsigned* mc) {
     const int LPS = sh[0], CPL = sh[1], RPL = sh[2], D = sh[3];
     *mb = *mc = 0;
@@ -832,7 +846,8 @@ static int build_local_layout(phg_handle* h, const phg_batch* b) {
         const char* gen = std::getenv("PHG_LOCAL_GENERIC");
         const unsigned long long bi = local_inf_mask(b, plan, LPS, CPL, RPL, D);
         const unsigned long long bf = local_fin_mask(b, plan, LPS, CPL, RPL, D);
-        h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc, bi, bf);
+        const unsigned qm = local_quad_mask(b, plan, LPS, CPL);
+        h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc, bi, bf, qm);
         h->local_masks[0] = mb;
         h->local_masks[1] = mc;
         std::memcpy(h->lshape, sh, sizeof sh);
@@ -2071,10 +2086,11 @@ int phg_plan(const phg_batch* b_in, int32_t* out8) {
         local_slot_masks(plan, sh, &mb, &mc);
         const unsigned long long bi = local_inf_mask(b, plan, sh[0], sh[1], sh[2], sh[3]);
         const unsigned long long bf = local_fin_mask(b, plan, sh[0], sh[1], sh[2], sh[3]);
-        out8[7] = pdhg_local_pick_masked(v, mb, mc, bi, bf);
+        const unsigned qm = local_quad_mask(b, plan, sh[0], sh[1]);
+        out8[7] = pdhg_local_pick_masked(v, mb, mc, bi, bf, qm);
         if (const char* e = std::getenv("PHG_LOCAL_DEBUG"); e && std::atoi(e))
-            fprintf(stderr, "phg_plan: shape %d x %d x %d x %d MB 0x%x MC 0x%x BI 0x%llx BF 0x%llx variant %d\n",
-                    sh[0], sh[1], sh[2], sh[3], mb, mc, bi, bf, out8[7]);
+            fprintf(stderr, "phg_plan: shape %d x %d x %d x %d MB 0x%x MC 0x%x BI 0x%llx BF 0x%llx QM 0x%x variant %d\n",
+                    sh[0], sh[1], sh[2], sh[3], mb, mc, bi, bf, qm, out8[7]);
     }
     return 0;
 }
