@@ -259,7 +259,7 @@ def main():
     # in the next solve's prologue; then the standalone two-kernel update (node sums + W update,
     # the sequential statements) for its own roofline
     W_saved = eng.get(_lib.F_W)
-    fold = eng.set_fold(os.environ.get("PHG_FOLD", "0") != "0")
+    fold = eng.set_fold(os.environ.get("PHG_FOLD", "1") != "0")
     eng.timing_reset(solves=False, updates=True)
     for _ in range(args.steps):
         step()

@@ -97,8 +97,6 @@ static int fail(const std::string& msg) {
             return fail(std::string(#call) + ": " + hipGetErrorString(e_));                   \
     } while (0)
 
-// batches from this many nonant values up take the folded PH update by default (phg_set_fold)
-static constexpr long kFoldMinSN = 10000000;
 
 struct phg_handle {
     int device = 0;
@@ -217,11 +215,12 @@ struct phg_handle {
     int gap_const = 1;
     int sum_stride = 1;        // PdhgArgs::sum_stride (PHG_SUM_STRIDE)
     // folded PH update (phg_ph_head -> the next phg_solve's prologue does Update_W), lane-local
-    // layout without smoothing / variable probability.  OFF by default (PHG_FOLD=1 / phg_set_fold):
-    // measured on farmer 10k it slows the PDHG launch by ~9 us (the prologue's dependent W-update
-    // chain in every wave) for a ~2.5 us shorter update -- 0.3465 vs 0.340 ms per PH iteration; at
-    // S N = 1e8 (S = 1e6, N = 100) 797 vs 847 us per update (tools/ph_update_sweep.py)
-    int fold = -1;             // -1: the size policy of phg_load_batch (on when S N >= kFoldMinSN)
+    // layout without smoothing / variable probability.  ON by default since round 4 (PHG_FOLD=0 /
+    // phg_set_fold turn it off): the branch-free prologue loads W with the scenario's other data, so
+    // the fold no longer lengthens the PDHG launch (farmer 10k: 0.2851 ms either way) and it drops the
+    // W-update launch and its second read of x (0.3108 vs 0.3138 ms per PH iteration, time to conv
+    // 0.850 vs 0.864 s); round 3 (dependent prologue chain) measured it 9 us slower on farmer
+    int fold = -1;             // -1: on (phg_load_batch), unless PHG_FOLD / phg_set_fold said otherwise
     bool fold_w_pending = false;      // xbar of update k is in place, its W update not yet applied
     bool xn_external = false;         // PHG_F_XN was set by the caller: xN != xs dc until the next solve
     bool fold_conv_pending = false;   // the last solve did a folded update: its conv partials are
@@ -2126,11 +2125,10 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
     CK(hipSetDevice(h->device));
     const int S = b->S, n = b->n, m = b->m, nnz = b->nnz, N = b->N;
     h->S = S; h->n = n; h->m = m; h->nnz = nnz; h->N = N; h->L = b->L; h->N_tot = b->N_tot;
-    // the folded PH update by batch size (no PHG_FOLD / phg_set_fold before the load): it pays where
-    // the update streams (S N = 1e8: 477 vs 650 us per update, 5.59 vs 5.76 ms per PH iteration with
-    // the solve) and costs where the PDHG launch is latency-bound (farmer 10k, S N = 3e5: 0.3465 vs
-    // 0.340 ms per PH iteration)
-    if (h->fold < 0) h->fold = (long)S * N >= kFoldMinSN ? 1 : 0;
+    // the folded PH update by default (no PHG_FOLD / phg_set_fold before the load): it pays where
+    // the update streams (S N = 1e8: 477 vs 650 us per update) and, with the round-4 prologue, on the
+    // latency-bound farmer 10k too (0.3108 vs 0.3138 ms per PH iteration)
+    if (h->fold < 0) h->fold = 1;
     h->n_nodes = b->n_nodes; h->P = std::max(1, b->virt_nproc);
     h->n_pad = (n + 1) & ~1;
     h->sense = b->sense >= 0 ? 1.0 : -1.0;
