@@ -80,17 +80,6 @@ __device__ __forceinline__ double x_minus_xbar(double xs, double dc, double xbar
     return x - xbar;
 }
 
-// The kernel argument block in the kernarg segment (constant address space: scalar loads).  The
-// prologue / epilogue read their pointers through kargs() at the use site -- the laundered pointer
-// keeps the compiler from hoisting those loads out of the work loop and holding ~40 pointers in
-// SGPRs across it (round 3: 167 SGPRs spilled to VGPR lanes, ~900 v_readlane in the prologue)
-typedef const __attribute__((address_space(4))) PdhgArgs* KP;
-__device__ __forceinline__ KP kargs() {
-    KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return p;
-}
-
 template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC, unsigned long long BI,
           unsigned long long BF, unsigned QM>
 __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_local_kernel(PdhgArgs a) {

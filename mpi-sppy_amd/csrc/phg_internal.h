@@ -264,6 +264,18 @@ struct PdhgArgs {
     const int* status_in;   // [S] statuses of the solve being warm-started from (front copy)
 };
 
+// The kernel argument block in the kernarg segment (constant address space: scalar loads).  Cold code
+// (prologues, epilogues, checks) reads its pointers through kargs() at the use site -- the laundered
+// pointer keeps the compiler from hoisting those loads out of the work loop and holding dozens of
+// pointers in SGPRs across it (round 3's lane-local kernel spilled 167 SGPRs to VGPR lanes and
+// restored them with ~900 v_readlane in its prologue)
+typedef const __attribute__((address_space(4))) PdhgArgs* KP;
+__device__ __forceinline__ KP kargs() {
+    KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
 // relative-gap denominator of the termination test (PdhgArgs::gap_const): K = the objective constant
 __device__ __forceinline__ double gap_den(double p, double d, double K) {
     return 1.0 + fabs(p + K) + fabs(d + K);
@@ -368,13 +380,16 @@ struct PhArgs {
 // kk = the nonant's index in its scenario (t = s N + kk): two-stage batches (root_only) read xbar[kk]
 // and, with rho the same in every scenario (rho_k), rho_k[kk] -- no dependent index load, no S*N
 // stream for rho
-__device__ __forceinline__ int xbar_slot(const PdhgArgs& a, long t, int kk) {
+template <class A>
+__device__ __forceinline__ int xbar_slot(const A& a, long t, int kk) {
     return a.root_only ? kk : a.xidx[t];
 }
-__device__ __forceinline__ double rho_of(const PdhgArgs& a, long t, int kk) {
+template <class A>
+__device__ __forceinline__ double rho_of(const A& a, long t, int kk) {
     return a.rho_k ? a.rho_k[kk] : a.rho[t];
 }
-__device__ __forceinline__ void ph_terms_w(const PdhgArgs& a, long t, int kk, double w, double& cc, double& qq,
+template <class A>
+__device__ __forceinline__ void ph_terms_w(const A& a, long t, int kk, double w, double& cc, double& qq,
                                            double& pc) {
     if (a.w_on) cc += w;
     if (a.prox_on) {
@@ -391,7 +406,8 @@ __device__ __forceinline__ void ph_terms_w(const PdhgArgs& a, long t, int kk, do
         }
     }
 }
-__device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, int kk, double& cc, double& qq, double& pc) {
+template <class A>
+__device__ __forceinline__ void ph_terms(const A& a, long t, int kk, double& cc, double& qq, double& pc) {
     ph_terms_w(a, t, kk, a.w_on ? a.W[t] : 0.0, cc, qq, pc);
 }
 
@@ -399,7 +415,8 @@ __device__ __forceinline__ void ph_terms(const PdhgArgs& a, long t, int kk, doub
 // 0 fixes exactly; a small positive tolerance plays the part of a CPU solver's primal feasibility
 // tolerance when a candidate from a first-order solve meets a first-stage row only to ~1e-10
 // (phg_opts.fix_tol)
-__device__ __forceinline__ void fixed_box(const PdhgArgs& a, long t, double d, double& lo, double& hi) {
+template <class A>
+__device__ __forceinline__ void fixed_box(const A& a, long t, double d, double& lo, double& hi) {
     const double v = a.fixed[t];
     const double w = a.fix_tol * fmax(1.0, fabs(v));
     lo = (v - w) / d;
@@ -411,7 +428,8 @@ __device__ __forceinline__ void fixed_box(const PdhgArgs& a, long t, double d, d
 // infeasible when it is violated beyond its feasibility tolerance; the caller checks that on the
 // host, cylinders.evaluate_xhat).  Kept as a row with a first-order solver it would be an equality
 // between constants that round-off makes infeasible, sending the dual iterates off along the ray.
-__device__ __forceinline__ void row_bounds(const PdhgArgs& a, int i, long b, double& lo, double& hi) {
+template <class A>
+__device__ __forceinline__ void row_bounds(const A& a, int i, long b, double& lo, double& hi) {
     if (a.fix_nonants && a.row_fixed && a.row_fixed[i]) { lo = -INFINITY; hi = INFINITY; return; }
     lo = a.rl[b];
     hi = a.ru[b];
