@@ -213,7 +213,11 @@ struct phg_handle {
     SafeBoundArgs sb{};
     // relative-gap test on the whole objective (PdhgArgs::gap_const); PHG_GAP_RAW=1 turns it off
     int gap_const = 1;
-    int sum_stride = 1;        // PdhgArgs::sum_stride (PHG_SUM_STRIDE)
+    // PdhgArgs::sum_stride (PHG_SUM_STRIDE=1/2/3).  2 by default since round 4: the average iterate's
+    // running sums take every second iterate -- farmer 10k: 0.268 vs 0.285 ms per PDHG launch (7 of
+    // ~62 instructions per PDHG iteration saved in every other iteration), the same 286 PDHG
+    // iterations per solve, time to conv 0.845 vs 0.852 s; round 3 measured it within noise
+    int sum_stride = 2;
     // folded PH update (phg_ph_head -> the next phg_solve's prologue does Update_W), lane-local
     // layout without smoothing / variable probability.  ON by default since round 4 (PHG_FOLD=0 /
     // phg_set_fold turn it off): the branch-free prologue loads W with the scenario's other data, so
@@ -340,7 +344,8 @@ int phg_create(int device, phg_handle** out) {
     CK(hipSetDevice(device));
     phg_handle* h = new phg_handle();
     h->device = device;
-    if (const char* ev = std::getenv("PHG_LOCAL_PERSIST")) h->persist = std::atoi(ev) != 0;
+    // (PHG_LOCAL_PERSIST, the persistent work-queue grid, is no longer honoured: measured slower in
+    // round 1 and found to hang in round 4 -- the kernel's gate return skips its queue re-arm)
     if (const char* ev = std::getenv("PHG_AVG_EVERY")) h->avg_every = std::max(1, std::atoi(ev));
     if (const char* ev = std::getenv("PHG_FUSE")) h->no_fuse = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_GAP_RAW")) h->gap_const = std::atoi(ev) == 0;

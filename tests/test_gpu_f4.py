@@ -110,6 +110,9 @@ class _PluginPH(oph.OraclePH):
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
         self.plugin = SolverFactory("phg")
+        # a fresh model object per call: every solve is cold, and the fixture's 5e-6 on W sits inside
+        # what eps 1e-9 (relative KKT on objectives of ~1e5) leaves the iterate free to move
+        self.plugin.options["pdhg_eps"] = 1e-11
         self.models = [farmer.scenario_creator(nm, num_scens=self.S) for nm in self.names]
 
     def solve_one(self, k):
