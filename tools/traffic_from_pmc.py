@@ -14,7 +14,7 @@ import sys
 KERNELS = {"local": r"pdhg_local_kernel", "gather": r"pdhg_kernel<", "block": r"pdhg_block_kernel",
            "mfma": r"pdhg_mfma_kernel", "stream": r"pdhg_stream_kernel", "border": r"pdhg_border(_reg)?_kernel",
            "wave": r"pdhg_wave_kernel"}
-AUX = {"node_sums": r"node_sums_kernel", "w_update": r"w_update_kernel"}
+AUX = {"node_sums": r"node_sums_kernel", "w_update": r"w_update_kernel", "xbar_head": r"xbar_head_kernel"}
 
 
 def per_launch_kb(path, pattern, counter):
