@@ -150,10 +150,10 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     auto drow_of = [](unsigned msk, int R) {
         return (msk >> R) & 1u ? __builtin_popcount(msk & ((1u << R) - 1u)) : -1;
     };
-    auto unit_fma = [&](int cd, int d, int drow0, double acc) {
+    auto unit_fma = [&](int cd, int d, int drow0, double acc, int tq) {
         const unsigned cu = (unsigned)(unsigned short)cd;
         const double v = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(smem) + (cu & 0xFFF8u));
-        if (d >= 0) return fma(dl[(drow0 + d) * NT + t], v, acc);
+        if (d >= 0) return fma(dl[(drow0 + d) * NT + tq], v, acc);
         // +-1.0 built from the sign bit: fma(+-1, v, acc), the delta form's bits
         return fma(__hiloint2double((int)(0x3FF00000u | (cu << 31)), 0), v, acc);
     };
@@ -253,7 +253,12 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
 
     // ------------------------------------------------------------------ SpMVs through LDS
     // A x for the x currently in xl: pieces -> rp, barrier, row owners add their pieces
+    // tq: the thread index laundered at every product, so the per-thread LDS addresses of the pieces
+    // are re-formed in the iteration (one add each) instead of being hoisted out of the PDHG loop --
+    // held across it they spilled (netdes: 5 scratch reloads per PDHG iteration, the HBM traffic of
+    // round 3's 14.3 KB per scenario-iteration)
     auto spmv_ax = [&](double (&out)[RPL]) {
+        const int tq = launder(t);
         int off = 0;
 #pragma unroll
         for (int ps = 0; ps < PPT; ++ps) {
@@ -265,8 +270,8 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
                 const int kk = B.rk[ps];
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
-                    const int e = off + k * NT + t;
-                    if constexpr (UN) acc = unit_fma(codes[e], drow_of(rdm, off / NT + k), 0, acc);
+                    const int e = off + k * NT + tq;
+                    if constexpr (UN) acc = unit_fma(codes[e], drow_of(rdm, off / NT + k), 0, acc, tq);
                     else acc = fma(rval(e, off / NT + k), xl[B.ridx[e]], acc);
                 }
                 off += kk * NT;
@@ -299,6 +304,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
     };
     // A^T y for the y currently in yl
     auto spmv_aty = [&](double (&out)[CPL]) {
+        const int tq = launder(t);
         int off = 0;
 #pragma unroll
         for (int ps = 0; ps < QPT; ++ps) {
@@ -310,8 +316,8 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
                 const int kk = B.ck[ps];
 #pragma unroll 2
                 for (int k = 0; k < kk; ++k) {
-                    const int e = off + k * NT + t;
-                    if constexpr (UN) acc = unit_fma(codes[B.er + e], drow_of(cdm, off / NT + k), B.nd_r, acc);
+                    const int e = off + k * NT + tq;
+                    if constexpr (UN) acc = unit_fma(codes[B.er + e], drow_of(cdm, off / NT + k), B.nd_r, acc, tq);
                     else acc = fma(cval(e, off / NT + k), yl[B.cidx[e]], acc);
                 }
                 off += kk * NT;
