@@ -59,7 +59,8 @@ def parse():
     ap.add_argument("--layout", default="auto", choices=["auto", "gather", "local", "block", "mfma", "stream", "border", "wave"],
                     help="PDHG data layout (include/phg.h: phg_set_layout)")
     ap.add_argument("--no-schedule", action="store_true", help="launch scenarios in index order")
-    ap.add_argument("--check-every", type=int, default=32, help="PDHG restart/termination check interval")
+    ap.add_argument("--check-every", type=int, default=None,
+                    help="PDHG restart/termination check interval (default: by layout, phbase.check_every_default)")
     ap.add_argument("--beta-art", type=float, default=0.0, help="artificial restart fraction (0: default)")
     ap.add_argument("--theta", type=float, default=0.0, help="primal weight smoothing (0: default)")
     ap.add_argument("--keep-omega", default="blend", choices=["fresh", "carry", "blend"],
