@@ -457,9 +457,22 @@ __global__ __launch_bounds__(NT) void pdhg_border_kernel(PdhgArgs a) {
 // for the gathers, so a PDHG iteration touches memory only for the linking-row exchange -- the
 // memory-resident kernel above moves each iteration's vectors through L2 / HBM (PMC: ~1.7 TB per
 // UC launch at S = 64).  Needs C_max, R_max <= E NT (the host picks E, or this variant is not used).
-template <int NT, int E>
+template <int NT, int E, bool PROF>
 __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
+    // PROF (PHG_BORDER_PROF=1, diagnostic): wall-clock split of a PDHG iteration as wave 0 of each
+    // workgroup sees it (s_memrealtime, 100 MHz), [10] per workgroup: primal, publish + local dual,
+    // hop-1 wait, row sums + mid, hop-2 wait, linking dual + settle + A^T y, checks, the rest
+    // (queue, prologue, outputs), PDHG iterations, scenarios
+    unsigned long long pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pf_last = 0, pf_it = 0, pf_sc = 0;
+    if constexpr (PROF) pf_last = __builtin_amdgcn_s_memrealtime();
+    auto PF = [&](int i) {
+        if constexpr (PROF) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            pf[i] += now - pf_last;
+            pf_last = now;
+        }
+    };
     __shared__ double red[16 * (NT / 64)];
     __shared__ int s_w;
     extern __shared__ double dyn[];
@@ -610,13 +623,17 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         const int nown = (NL - kw + K - 1) / K;
         for (int u = t; u < nown * K; u += NT) xtmp[u] = gget(g1 + ((long)(kw + K * (u / K)) * K + u % K) * 2, ep);
         __syncthreads();
+        PF(2);
         if (t < nown) {
             double acc = xtmp[t * K];
             for (int q = 1; q < K; ++q) acc += xtmp[t * K + q];
             gput(g2 + (long)(kw + K * t) * 2, ep, acc);
         }
         mid();
-        return t < NL ? gget(g2 + (long)t * 2, ep) : 0.0;
+        PF(3);
+        const double r = t < NL ? gget(g2 + (long)t * 2, ep) : 0.0;
+        PF(4);
+        return r;
     };
     auto settle = [&]() {   // after an exchange: one workgroup barrier, then the give-up flag
         __syncthreads();
@@ -829,7 +846,9 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         xs[e] += xn;
         Xl[t + e * NT] = xn;
     };
+    PF(7);
     while (alive) {
+        PF(6);
         // pre: the columns without a linking entry took this iteration's primal step already, during
         // the previous iteration's second hop (never across a check: their A^T y is final there)
         bool pre = false;
@@ -838,6 +857,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             for (int e = 0; e < E; ++e)
                 if (cv_[e] && !(pre && loc_[e])) primal(e);
             __syncthreads();
+            PF(0);
             // the iteration's one cross-workgroup step, overlapped: the linking-row partials go out
             // first; the local rows' dual step runs during hop 1, the A^T y of the columns without a
             // linking-row entry during hop 2 (it needs only the local y, visible after the exchange's
@@ -856,6 +876,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
                     ys[e] += yn;
                     Yl[t + e * NT] = yn;
                 }
+            PF(1);
             pre = kk + 1 < chk;
             const double axn_l = ex_complete(ep, axl, [&]() {
 #pragma unroll
@@ -879,6 +900,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
 #pragma unroll
             for (int e = 0; e < E; ++e)
                 if (cv_[e] && !loc_[e]) aty[e] = aty_col(yl, t + e * NT);
+            PF(5);
         }
         if (!alive) break;
         it += chk;
@@ -1024,9 +1046,24 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         a.iters_acc[s] += it;
         a.status[s] = st;
     }
+    if constexpr (PROF) {
+        PF(7);
+        pf_it += it;
+        ++pf_sc;
+    }
     if (!alive) break;
     __syncthreads();
     }   // scenario queue
+    if constexpr (PROF) {   // lane u of wave 0 stores item u (vector stores)
+        const int lane = t & 63;
+        if (t < 64) {
+            unsigned long long v = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v = lane == u ? pf[u] : v;
+            v = lane == 8 ? pf_it : (lane == 9 ? pf_sc : v);
+            if (lane < 10) a.prof[(size_t)blockIdx.x * 10 + lane] = v;
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------- dispatch
@@ -1067,8 +1104,9 @@ hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream) {
     const size_t lds = a.bd.reg ? std::max(pdhg_border_lds_bytes(a.bd), kOnePerCuLds) : pdhg_border_lds_bytes(a.bd);
     PdhgArgs copy = a;
     void* args[] = {&copy};
-    const void* fn = a.bd.reg ? (const void*)pdhg_border_reg_kernel<kBorderRegNT, 2>
-                              : (const void*)pdhg_border_kernel<kBorderNT>;
+    const void* fn = !a.bd.reg ? (const void*)pdhg_border_kernel<kBorderNT>
+                     : a.prof ? (const void*)pdhg_border_reg_kernel<kBorderRegNT, 2, true>
+                              : (const void*)pdhg_border_reg_kernel<kBorderRegNT, 2, false>;
     if (L.K == 1 || !coop_launch_enabled()) return hipLaunchKernel(fn, grid, block, args, lds, stream);
     return hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)lds, stream);
 }

@@ -2538,7 +2538,43 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             h->fold_conv_pending = true;
         }
     }
-    if (h->border_layout) CK(pdhg_border_launch(a, h->stream));
+    if (h->border_layout) {
+        // PHG_BORDER_PROF=1 (diagnostic, register-resident variant): wall-clock split of a PDHG
+        // iteration per workgroup (pdhg_border.hip), printed to stderr after every launch
+        static const bool bprof = [] { const char* e = std::getenv("PHG_BORDER_PROF"); return e && std::atoi(e); }();
+        static unsigned long long* pbuf = nullptr;
+        static size_t pcap = 0;
+        const size_t nwg = (size_t)h->st.slots * h->st.K;
+        const bool on = bprof && h->bd.reg;
+        if (on && pcap < nwg * 10) {
+            if (pbuf) CK(hipFree(pbuf));
+            CK(hipMalloc((void**)&pbuf, nwg * 10 * sizeof(unsigned long long)));
+            pcap = nwg * 10;
+        }
+        if (on) CK(hipMemsetAsync(pbuf, 0, pcap * sizeof(unsigned long long), h->stream));
+        a.prof = on ? pbuf : nullptr;
+        CK(pdhg_border_launch(a, h->stream));
+        if (on) {
+            std::vector<unsigned long long> hb(nwg * 10);
+            CK(hipMemcpyAsync(hb.data(), pbuf, hb.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+            CK(hipStreamSynchronize(h->stream));
+            double t[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            double span = 0.0;
+            for (size_t w = 0; w < nwg; ++w) {
+                double tot = 0.0;
+                for (int u = 0; u < 10; ++u) t[u] += (double)hb[w * 10 + u];
+                for (int u = 0; u < 8; ++u) tot += (double)hb[w * 10 + u];
+                span = std::max(span, tot);
+            }
+            const double it = std::max(1.0, t[8]);
+            fprintf(stderr,
+                    "PHG_BORDER_PROF K %d slots %d iters %.0f scen %.0f max_wg_us %.1f us_per_iter: primal %.3f "
+                    "publish_dual %.3f hop1 %.3f rowsum_mid %.3f hop2 %.3f link_aty %.3f checks %.3f other %.3f\n",
+                    h->st.K, h->st.slots, t[8] / h->st.K, t[9] / h->st.K, span / 100.0, t[0] / 100.0 / it,
+                    t[1] / 100.0 / it, t[2] / 100.0 / it, t[3] / 100.0 / it, t[4] / 100.0 / it, t[5] / 100.0 / it,
+                    t[6] / 100.0 / it, t[7] / 100.0 / it);
+        }
+    }
     else if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));
     else if (h->mfma_variant >= 0) CK(pdhg_mfma_launch(h->mfma_variant, a, h->stream));
     else if (h->local_variant >= 0) {

@@ -213,7 +213,8 @@ struct PdhgArgs {
     double* ys;             // [S*m]
     double* omega;          // [S]
     // diagnostic (PHG_LOCAL_PROF, lane-local kernel only): per wave [8] {iteration cycles, check
-    // cycles, load cycles, KKT cycles, restart-block cycles, checks}; null = off
+    // cycles, load cycles, KKT cycles, restart-block cycles, checks}; PHG_BORDER_PROF, the bordered
+    // register-resident kernel: per workgroup [10] (pdhg_border.hip); null = off
     unsigned long long* prof;
     // outputs
     double* x_out;          // [S*n] unscaled, or null: left to phg_get / eval (xs * dc, see unscale_launch)

@@ -48,9 +48,10 @@ def check_every_default(layout):
     """PDHG restart / termination check interval by kernel layout (measured on MI355X): 64 for the
     one-wave-per-scenario gather kernel (tiny subproblems: hydro 2 000, 6.2 vs 5.3 M solves/s, the
     slowest scenario 704 vs 1 024 PDHG iterations, time to PH conv 0.029 vs 0.34 s over the same
-    ~104 PH iterations), 32 elsewhere (farmer: 40 / 48 / 64 cost time to conv; the MFMA kernel at 64
-    missed a hydro parity objective in round 2)."""
-    return 64 if layout == "gather" else 32
+    ~104 PH iterations) and the workgroup-block kernel (netdes 1 024: 19.9 vs 22.0 ms per PH
+    iteration, sslp 4 096: 5.50 vs 5.65 ms), 32 elsewhere (farmer: 40 / 48 / 64 cost time to conv;
+    the MFMA kernel at 64 missed a hydro parity objective in round 2)."""
+    return 64 if layout in ("gather", "block") else 32
 
 
 class PHBase(SPBase):

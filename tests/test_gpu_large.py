@@ -159,7 +159,8 @@ def test_border_matches_block_kernel(monkeypatch):
     o.Update_W()
     res = {}
     for layout in ("block", "border"):
-        ph = PH(_opts(pdhg_layout=layout), uc.scenario_names_creator(3), uc.scenario_creator, scenario_creator_kwargs=kw)
+        # the same check interval on both (the default is by layout: phbase.check_every_default)
+        ph = PH(_opts(pdhg_layout=layout, pdhg_check_every=32), uc.scenario_names_creator(3), uc.scenario_creator, scenario_creator_kwargs=kw)
         ph.PH_Prep()
         assert ph.engine.layout == layout
         ph.Iter0()
@@ -300,7 +301,8 @@ def test_wave_kernel_matches_block_kernel():
     o.Update_W()
     res = {}
     for layout in ("wave", "block"):
-        ph = PH(_opts(pdhg_layout=layout), sslp.scenario_names_creator(S), sslp.scenario_creator)
+        # the same check interval on both (the default is by layout: phbase.check_every_default)
+        ph = PH(_opts(pdhg_layout=layout, pdhg_check_every=32), sslp.scenario_names_creator(S), sslp.scenario_creator)
         ph.PH_Prep()
         assert ph.engine.layout == layout
         ph.Iter0()
