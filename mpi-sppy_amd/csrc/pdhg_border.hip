@@ -35,7 +35,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     __shared__ double red[16 * (NT / 64)];
     __shared__ int s_w;
-    extern __shared__ double dyn[];
+    extern __shared__ __attribute__((aligned(16))) double dyn[];   // (16 B: vector gathers)
     const StreamLayout& L = a.st;
     const BorderLayout& B = a.bd;
     const int K = L.K;
@@ -491,13 +491,16 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     double* Yl = Xl + B.C_max;                       // [R_max] y of the local rows
     double* yl = Yl + B.R_max;                       // [NL]
     double* ylx = yl + NL;                           // [NL]
-    double* xtmp = ylx + NL;                         // [max(NL + K, 16 K)] staged cross-workgroup partials
-    int* lrp = reinterpret_cast<int*>(xtmp + B.xtmp_len);   // [R_max + 1]
-    int* lci = lrp + B.R_max + 1;                    // [nrz_max] local column position
-    int* lkp = lci + B.nrz_max;                      // [NL + 1]
-    int* lkc = lkp + NL + 1;                         // [nlz_max] local column position
-    int* lcp = lkc + B.nlz_max;                      // [C_max + 1]
-    int* lri = lcp + B.C_max + 1;                    // [ncz_max] local row position, or -(l + 1)
+    double* xtmp = ylx + NL;                         // [xtmp_len] staged cross-workgroup partials
+    // every row / column segment padded to a multiple of 4 entries (value 0, index 0: the host's
+    // build_border_layout), the index arrays 16-byte aligned: a gather reads 4 indices and 4 values
+    // per step with vector LDS loads and issues the 4 x / y loads together
+    int* lci = reinterpret_cast<int*>(xtmp + B.xtmp_len);   // [nrz_max] local column position
+    int* lkc = lci + B.nrz_max;                      // [nlz_max] local column position
+    int* lri = lkc + B.nlz_max;                      // [ncz_max] local row position, or -(l + 1)
+    int* lrp = lri + B.ncz_max;                      // [R_max + 1]
+    int* lkp = lrp + B.R_max + 1;                    // [NL + 1]
+    int* lcp = lkp + NL + 1;                         // [C_max + 1]
     for (int q = t; q <= nr; q += NT) lrp[q] = B.rptr[G.rp0 + q];
     for (int q = t; q < G.nrz; q += NT) lci[q] = B.rcl[G.rz0 + q];
     for (int q = t; q <= NL; q += NT) lkp[q] = B.lptr[G.lp0 + q];
@@ -571,12 +574,11 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         if (t < V) gput(g + ((long)kw * 16 + t) * 2, ep, v[t]);
         for (int u = t; u < V * K; u += NT) xtmp[u] = gget(g + ((long)(u / V) * 16 + u % V) * 2, ep);
         __syncthreads();
+        // value u's K partials in workgroup order by thread u (in place), then read by every thread
+        if (t < V) xtmp[t] = ordered_sum(xtmp + t, V, K);
+        __syncthreads();
 #pragma unroll
-        for (int u = 0; u < V; ++u) {
-            double acc = xtmp[u];
-            for (int q = 1; q < K; ++q) acc += xtmp[q * V + u];
-            v[u] = acc;
-        }
+        for (int u = 0; u < V; ++u) v[u] = xtmp[u];
         __syncthreads();
         if (s_dead) alive = false;
     };
@@ -593,11 +595,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         const int nown = (NL - kw + K - 1) / K;   // rows kw, kw + K, ...
         for (int u = t; u < nown * K; u += NT) xtmp[u] = gget(g1 + ((long)(kw + K * (u / K)) * K + u % K) * 2, ep);
         __syncthreads();
-        if (t < nown) {
-            double acc = xtmp[t * K];
-            for (int q = 1; q < K; ++q) acc += xtmp[t * K + q];
-            gput(g2 + (long)(kw + K * t) * 2, ep, acc);
-        }
+        if (t < nown) gput(g2 + (long)(kw + K * t) * 2, ep, ordered_sum(xtmp + t * K, 1, K));
         return t < NL ? gget(g2 + (long)t * 2, ep) : 0.0;
     };
     // the same exchange split around independent work (the PDHG iteration): ex_publish stores this
@@ -624,11 +622,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         for (int u = t; u < nown * K; u += NT) xtmp[u] = gget(g1 + ((long)(kw + K * (u / K)) * K + u % K) * 2, ep);
         __syncthreads();
         PF(2);
-        if (t < nown) {
-            double acc = xtmp[t * K];
-            for (int q = 1; q < K; ++q) acc += xtmp[t * K + q];
-            gput(g2 + (long)(kw + K * t) * 2, ep, acc);
-        }
+        if (t < nown) gput(g2 + (long)(kw + K * t) * 2, ep, ordered_sum(xtmp + t * K, 1, K));
         mid();
         PF(3);
         const double r = t < NL ? gget(g2 + (long)t * 2, ep) : 0.0;
@@ -639,24 +633,41 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         __syncthreads();
         if (s_dead) alive = false;
     };
-    auto ax_loc = [&](int q) {   // A x of local row q from Xl
+    // sum over a padded segment [p0, p1) of val[p] * vec[idx[p]], 4 entries per step, in entry order
+    // (a padding entry adds fma(0, v, acc) = acc: the same bits as the unpadded loop)
+    auto gather4 = [&](const double* val, const int* idx, const double* vec, int p0, int p1) {
         double acc = 0.0;
-        for (int p = lrp[q]; p < lrp[q + 1]; ++p) acc = fma(lrv[p], Xl[lci[p]], acc);
+        for (int p = p0; p < p1; p += 4) {
+            const int4 ix = *reinterpret_cast<const int4*>(idx + p);
+            const double2 v0 = *reinterpret_cast<const double2*>(val + p);
+            const double2 v1 = *reinterpret_cast<const double2*>(val + p + 2);
+            const double x0 = vec[ix.x], x1 = vec[ix.y], x2 = vec[ix.z], x3 = vec[ix.w];
+            acc = fma(v0.x, x0, acc);
+            acc = fma(v0.y, x1, acc);
+            acc = fma(v1.x, x2, acc);
+            acc = fma(v1.y, x3, acc);
+        }
         return acc;
     };
-    auto ax_link = [&]() {
-        double acc = 0.0;
-        if (t < NL)
-            for (int p = lkp[t]; p < lkp[t + 1]; ++p) acc = fma(lkv[p], Xl[lkc[p]], acc);
-        return acc;
-    };
+    auto ax_loc = [&](int q) { return gather4(lrv, lci, Xl, lrp[q], lrp[q + 1]); };   // A x of local row q from Xl
+    auto ax_link = [&]() { return t < NL ? gather4(lkv, lkc, Xl, lkp[t], lkp[t + 1]) : 0.0; };
     auto aty_col = [&](const double* ylv, int q) {
         double acc = 0.0;
-        for (int p = lcp[q]; p < lcp[q + 1]; ++p) {
-            const int r = lri[p];
-            // two LDS reads and a select (a select of the two pointers compiles to a flat load)
+        // a row index r >= 0 is a local row (Yl), r < 0 linking row -r - 1 (ylv): two LDS reads and a
+        // select per entry (a select of the two pointers compiles to a flat load)
+        auto yof = [&](int r) {
             const double yloc = Yl[r >= 0 ? r : 0], ylnk = ylv[r >= 0 ? 0 : -r - 1];
-            acc = fma(lcv[p], r >= 0 ? yloc : ylnk, acc);
+            return r >= 0 ? yloc : ylnk;
+        };
+        for (int p = lcp[q]; p < lcp[q + 1]; p += 4) {
+            const int4 ix = *reinterpret_cast<const int4*>(lri + p);
+            const double2 v0 = *reinterpret_cast<const double2*>(lcv + p);
+            const double2 v1 = *reinterpret_cast<const double2*>(lcv + p + 2);
+            const double y0 = yof(ix.x), y1 = yof(ix.y), y2 = yof(ix.z), y3 = yof(ix.w);
+            acc = fma(v0.x, y0, acc);
+            acc = fma(v0.y, y1, acc);
+            acc = fma(v1.x, y2, acc);
+            acc = fma(v1.y, y3, acc);
         }
         return acc;
     };
@@ -686,11 +697,12 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     if (!alive || wi >= a.S) break;
     const int s = a.order ? a.order[wi] : wi;
     const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
-    if (L.vstride != 0 || !vals_loaded) {
+    if (L.vstride != 0 || !vals_loaded) {   // (position -1: a padding entry, value 0)
         const double* rvs = L.rvals + (long)s * L.vstride;
-        for (int q = t; q < G.nrz; q += NT) lrv[q] = rvs[B.rperm[G.rz0 + q]];
-        for (int q = t; q < G.nlz; q += NT) lkv[q] = rvs[B.lperm[G.lz0 + q]];
-        for (int q = t; q < G.ncz; q += NT) lcv[q] = rvs[B.cperm[G.cz0 + q]];
+        auto val = [&](int pp) { return pp >= 0 ? rvs[pp] : 0.0; };
+        for (int q = t; q < G.nrz; q += NT) lrv[q] = val(B.rperm[G.rz0 + q]);
+        for (int q = t; q < G.nlz; q += NT) lkv[q] = val(B.lperm[G.lz0 + q]);
+        for (int q = t; q < G.ncz; q += NT) lcv[q] = val(B.cperm[G.cz0 + q]);
         vals_loaded = true;
     }
     double* XR = L.xr + sn;          // restart points (owner-only, touched at restarts)

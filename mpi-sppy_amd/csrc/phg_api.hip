@@ -1498,6 +1498,8 @@ static int uf_find(std::vector<int>& p, int x) {
     return x;
 }
 
+static int pad4(int len) { return (len + 3) & ~3; }
+
 static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vector<int>& colptr,
                                const std::vector<int>& csc_row, const std::vector<int>& csc_p, int cap) {
     const int n = b->n, m = b->m, S = std::max(1, b->S);
@@ -1560,24 +1562,47 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
         }
         B.nlink = (int)link_rows.size();
         if (B.nlink > 1024) return SIZE_MAX;
-        std::vector<int> nc(K, 0), nr(K, 0), nrz(K, 0), nlz(K, 0), ncz(K, 0);
-        for (int j = 0; j < n; ++j) { nc[gof[j]]++; ncz[gof[j]] += colptr[j + 1] - colptr[j]; }
-        for (int i = 0; i < m; ++i) {
-            if (rgrp[i] >= 0) { nr[rgrp[i]]++; nrz[rgrp[i]] += rp[i + 1] - rp[i]; }
-            else for (int p = rp[i]; p < rp[i + 1]; ++p) nlz[gof[ci[p]]]++;
+        // entry counts per group, and padded to 4 per row / column segment (register variant)
+        std::vector<int> nc(K, 0), nr(K, 0), nrz(K, 0), nlz(K, 0), ncz(K, 0), nrz4(K, 0), nlz4(K, 0), ncz4(K, 0);
+        std::vector<int> lcnt(K, 0);
+        for (int j = 0; j < n; ++j) {
+            const int len = colptr[j + 1] - colptr[j];
+            nc[gof[j]]++;
+            ncz[gof[j]] += len;
+            ncz4[gof[j]] += pad4(len);
         }
-        B.C_max = *std::max_element(nc.begin(), nc.end());
-        B.R_max = *std::max_element(nr.begin(), nr.end());
-        B.nrz_max = *std::max_element(nrz.begin(), nrz.end());
-        B.nlz_max = *std::max_element(nlz.begin(), nlz.end());
-        B.ncz_max = *std::max_element(ncz.begin(), ncz.end());
+        for (int i = 0; i < m; ++i) {
+            if (rgrp[i] >= 0) {
+                nr[rgrp[i]]++;
+                nrz[rgrp[i]] += rp[i + 1] - rp[i];
+                nrz4[rgrp[i]] += pad4(rp[i + 1] - rp[i]);
+            } else {
+                std::fill(lcnt.begin(), lcnt.end(), 0);
+                for (int p = rp[i]; p < rp[i + 1]; ++p) lcnt[gof[ci[p]]]++;
+                for (int k = 0; k < K; ++k) { nlz[k] += lcnt[k]; nlz4[k] += pad4(lcnt[k]); }
+            }
+        }
+        auto vmax = [](const std::vector<int>& v) { return *std::max_element(v.begin(), v.end()); };
+        B.C_max = vmax(nc);
+        B.R_max = vmax(nr);
         // register-resident variant (at most 2 owned columns and 2 rows per thread of 512)
         const int per = std::max(B.C_max, B.R_max);
         B.reg = (allow_reg && per <= pdhg_border_max_per_thread()) ? 2 : 0;
-        B.xtmp_len = std::max(B.nlink + K, 16 * K);
-        size_t bytes = pdhg_border_lds_bytes(B);
-        if (B.reg && bytes > budget) {   // the memory-resident variant needs less LDS
-            B.reg = 0;
+        size_t bytes = SIZE_MAX;
+        if (B.reg) {   // padded segments; an even count of doubles ahead of the (16-byte) int region
+            B.nrz_max = vmax(nrz4);
+            B.nlz_max = vmax(nlz4);
+            B.ncz_max = vmax(ncz4);
+            B.xtmp_len = std::max(B.nlink + K, 16 * K);
+            B.xtmp_len += (B.C_max + B.R_max + B.xtmp_len) & 1;
+            bytes = pdhg_border_lds_bytes(B);
+            if (bytes > budget) B.reg = 0;   // the memory-resident variant needs less LDS
+        }
+        if (!B.reg) {
+            B.nrz_max = vmax(nrz);
+            B.nlz_max = vmax(nlz);
+            B.ncz_max = vmax(ncz);
+            B.xtmp_len = std::max(B.nlink + K, 16 * K);
             bytes = pdhg_border_lds_bytes(B);
         }
         return bytes;
@@ -1610,6 +1635,9 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
     // concatenated per-group arrays
     std::vector<int> col_list, row_list, rptr, rcol, rperm, lptr, lcol, lperm, cptr, crow, cperm;
     std::vector<int> rcl, lcl, crl, lpos_col(n, -1), lpos_row(m, -1);
+    // the register variant's segments are padded to 4 entries (position -1: value 0, index 0) for its
+    // 4-wide gathers (pdhg_border.hip); the memory-resident kernel reads them unpadded
+    const bool pad = B.reg != 0;
     groups.assign(K, BorderGroup{});
     for (int k = 0; k < K; ++k) {
         BorderGroup& G = groups[k];
@@ -1629,6 +1657,7 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
             const int i = row_list[G.r0 + q];
             rptr.push_back((int)rcol.size() - G.rz0);
             for (int p = rp[i]; p < rp[i + 1]; ++p) { rcol.push_back(ci[p]); rcl.push_back(lpos_col[ci[p]]); rperm.push_back(p); }
+            while (pad && ((int)rcol.size() - G.rz0) % 4) { rcol.push_back(0); rcl.push_back(0); rperm.push_back(-1); }
         }
         rptr.push_back((int)rcol.size() - G.rz0);
         G.nrz = (int)rcol.size() - G.rz0;
@@ -1639,6 +1668,7 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
             lptr.push_back((int)lcol.size() - G.lz0);
             for (int p = rp[i]; p < rp[i + 1]; ++p)
                 if (gof[ci[p]] == k) { lcol.push_back(ci[p]); lcl.push_back(lpos_col[ci[p]]); lperm.push_back(p); }
+            while (pad && ((int)lcol.size() - G.lz0) % 4) { lcol.push_back(0); lcl.push_back(0); lperm.push_back(-1); }
         }
         lptr.push_back((int)lcol.size() - G.lz0);
         G.nlz = (int)lcol.size() - G.lz0;
@@ -1653,6 +1683,7 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
                 crl.push_back(linkidx[r] >= 0 ? -(linkidx[r] + 1) : lpos_row[r]);
                 cperm.push_back(csc_p[e]);
             }
+            while (pad && ((int)crow.size() - G.cz0) % 4) { crow.push_back(0); crl.push_back(0); cperm.push_back(-1); }
         }
         cptr.push_back((int)crow.size() - G.cz0);
         G.ncz = (int)crow.size() - G.cz0;

@@ -61,7 +61,24 @@ __device__ __forceinline__ bool scen_barrier(unsigned* cnt, unsigned target, int
     return s_ok != 0;
 }
 
-// workgroup sum of V values (V <= 16), same bits in every thread; fixed order
+// p[0] + p[s] + ... + p[(cnt - 1) s] added in that order (the same bits as the plain loop), the
+// LDS loads issued eight at a time instead of one dependent load per add; cnt >= 1
+__device__ __forceinline__ double ordered_sum(const double* p, int s, int cnt) {
+    double acc = p[0];
+    int q = 1;
+    for (; q + 8 <= cnt; q += 8) {
+        double r[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = p[(q + i) * s];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc += r[i];
+    }
+    for (; q < cnt; ++q) acc += p[q * s];
+    return acc;
+}
+
+// workgroup sum of V values (V <= 16), same bits in every thread; fixed order: wave partials in
+// wave order, added by thread k < V for value k (in place, red[k NW]) and read back by every thread
 template <int NT, int V>
 __device__ __forceinline__ void wg_sum(double (&v)[V], double* red) {
     constexpr int NW = NT / 64;
@@ -72,13 +89,18 @@ __device__ __forceinline__ void wg_sum(double (&v)[V], double* red) {
 #pragma unroll
         for (int k = 0; k < V; ++k) red[k * NW + w] = v[k];
     __syncthreads();
+    if (threadIdx.x < V) {
+        double r[NW];
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-        double t = red[k * NW];
-#pragma unroll 1
-        for (int u = 1; u < NW; ++u) t += red[k * NW + u];
-        v[k] = t;
+        for (int u = 0; u < NW; ++u) r[u] = red[threadIdx.x * NW + u];
+        double t = r[0];
+#pragma unroll
+        for (int u = 1; u < NW; ++u) t += r[u];
+        red[threadIdx.x * NW] = t;
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = red[k * NW];
     __syncthreads();
 }
 
