@@ -336,7 +336,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_kernel(PdhgArgs a) {
 
         const double inv = 1.0 / (double)cnt;
         const double l_axs = exchange(ax_link(XS));   // A x of the linking rows at the average
-        if (t < NL) ylx[t] = l_ys;
+        if (t < NL) yl[t] = l_ys;
         __syncthreads();
         double oc[6], oa[6];
         kkt_part(false, 0.0, 0.0, oc);
@@ -489,9 +489,8 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     double* lcv = lkv + B.nlz_max;                   // [ncz_max]
     double* Xl = lcv + B.ncz_max;                    // [C_max] x of the owned columns (local position)
     double* Yl = Xl + B.C_max;                       // [R_max] y of the local rows
-    double* yl = Yl + B.R_max;                       // [NL]
-    double* ylx = yl + NL;                           // [NL]
-    double* xtmp = ylx + NL;                         // [xtmp_len] staged cross-workgroup partials
+    double* yl = Yl + B.R_max;                       // [NL] linking rows' y, right after the local rows'
+    double* xtmp = yl + NL;                          // [xtmp_len] staged cross-workgroup partials
     // every row / column segment padded to a multiple of 4 entries (value 0, index 0: the host's
     // build_border_layout), the index arrays 16-byte aligned: a gather reads 4 indices and 4 values
     // per step with vector LDS loads and issues the 4 x / y loads together
@@ -506,7 +505,11 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     for (int q = t; q <= NL; q += NT) lkp[q] = B.lptr[G.lp0 + q];
     for (int q = t; q < G.nlz; q += NT) lkc[q] = B.lcl[G.lz0 + q];
     for (int q = t; q <= nc; q += NT) lcp[q] = B.cptr[G.cp0 + q];
-    for (int q = t; q < G.ncz; q += NT) lri[q] = B.crl[G.cz0 + q];
+    // column entries' rows as positions in Yl: local row r, or R_max + l for linking row l
+    for (int q = t; q < G.ncz; q += NT) {
+        const int r = B.crl[G.cz0 + q];
+        lri[q] = r >= 0 ? r : B.R_max - r - 1;
+    }
     // owned elements of this thread (fixed for the launch)
     int jc[E], ir[E];
     bool cv_[E], rv_[E];
@@ -651,26 +654,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     };
     auto ax_loc = [&](int q) { return gather4(lrv, lci, Xl, lrp[q], lrp[q + 1]); };   // A x of local row q from Xl
     auto ax_link = [&]() { return t < NL ? gather4(lkv, lkc, Xl, lkp[t], lkp[t + 1]) : 0.0; };
-    auto aty_col = [&](const double* ylv, int q) {
-        double acc = 0.0;
-        // a row index r >= 0 is a local row (Yl), r < 0 linking row -r - 1 (ylv): two LDS reads and a
-        // select per entry (a select of the two pointers compiles to a flat load)
-        auto yof = [&](int r) {
-            const double yloc = Yl[r >= 0 ? r : 0], ylnk = ylv[r >= 0 ? 0 : -r - 1];
-            return r >= 0 ? yloc : ylnk;
-        };
-        for (int p = lcp[q]; p < lcp[q + 1]; p += 4) {
-            const int4 ix = *reinterpret_cast<const int4*>(lri + p);
-            const double2 v0 = *reinterpret_cast<const double2*>(lcv + p);
-            const double2 v1 = *reinterpret_cast<const double2*>(lcv + p + 2);
-            const double y0 = yof(ix.x), y1 = yof(ix.y), y2 = yof(ix.z), y3 = yof(ix.w);
-            acc = fma(v0.x, y0, acc);
-            acc = fma(v0.y, y1, acc);
-            acc = fma(v1.x, y2, acc);
-            acc = fma(v1.y, y3, acc);
-        }
-        return acc;
-    };
+    auto aty_col = [&](int q) { return gather4(lcv, lri, Yl, lcp[q], lcp[q + 1]); };   // A^T y of column q (Yl, yl)
     bool vals_loaded = false;
     // owned columns with no linking-row entry (their A^T y needs only the local y)
     __syncthreads();   // lcp / lri in LDS
@@ -679,24 +663,66 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     for (int e = 0; e < E; ++e) {
         loc_[e] = true;
         if (cv_[e])
-            for (int p = lcp[t + e * NT]; p < lcp[t + e * NT + 1]; ++p) loc_[e] = loc_[e] && lri[p] >= 0;
+            for (int p = lcp[t + e * NT]; p < lcp[t + e * NT + 1]; ++p) loc_[e] = loc_[e] && lri[p] < B.R_max;
     }
+
+    // Split solves (BorderLayout::slice > 0; the launch has more scenarios than slots): a fresh
+    // scenario still running after slice x check_every PDHG iterations while the queue's first pass
+    // is not exhausted is suspended at that check -- its iterate, running sums, restart point and
+    // restart / step state saved -- and re-queued behind the first pass, so a slot that drew a heavy
+    // scenario late does not hold the launch: every scenario starts within the first pass, and the
+    // heavy ones then run to the end one per slot.  Resuming restores the state and recomputes A x /
+    // A^T y with the same gathers and sums: the same iterates, bits and iteration counts as an
+    // uninterrupted solve.  Queue codes: s (fresh), S + s (resumed), 2 S (no work left).
+    auto requeued = [&](int j) -> int {   // the j-th suspended scenario, or 2 S once every scenario is done
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (true) {
+            if (j < a.S) {
+                const int v = __hip_atomic_load(B.requeue + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v != 0) return a.S + v - 1;
+            }
+            if (__hip_atomic_load(L.ctrl + kCtrlDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)a.S ||
+                __hip_atomic_load(L.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+                return 2 * a.S;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {   // 30 s (100 MHz): give up
+                __hip_atomic_store(L.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return 2 * a.S;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+    };
 
     while (true) {
     if (kw == 0 && t == 0) {
         const unsigned w = __hip_atomic_fetch_add(L.ctrl + kCtrlHead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_w = (int)w;
-        if (K > 1) __hip_atomic_store(mbox, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int code = 2 * a.S;
+        if ((int)w < a.S) code = a.order ? a.order[w] : (int)w;
+        else if (B.slice > 0) code = requeued((int)w - a.S);
+        s_w = code;
+        if (K > 1) __hip_atomic_store(mbox, (unsigned)code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (K > 1) {
         barrier();
         if (kw != 0 && t == 0) s_w = (int)__hip_atomic_load(mbox, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    const int wi = s_w;
-    if (!alive || wi >= a.S) break;
-    const int s = a.order ? a.order[wi] : wi;
+    const int code = s_w;
+    if (!alive || code >= 2 * a.S) break;
+    const bool resumed = code >= a.S;
+    const int s = resumed ? code - a.S : code;
+    if (resumed) {   // the suspending slot's stores (released before it re-queued s): acquire
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
     const long sn = (long)s * a.n, sm = (long)s * a.m, sN = (long)s * a.N;
+    // PROF: per scenario {first start, end, iterations, splits} after the workgroup items
+    unsigned long long* pf_scen = a.prof ? a.prof + (size_t)gridDim.x * 10 + (size_t)s * 4 : nullptr;
+    if constexpr (PROF)
+        if (kw == 0 && t == 0 && !resumed) pf_scen[0] = __builtin_amdgcn_s_memrealtime();
+    double* SV = B.susp + (long)s * 8;   // suspended state: omega, kkt_restart, kkt_prev, it, since, cnt
     if (L.vstride != 0 || !vals_loaded) {   // (position -1: a padding entry, value 0)
         const double* rvs = L.rvals + (long)s * L.vstride;
         auto val = [&](int pp) { return pp >= 0 ? rvs[pp] : 0.0; };
@@ -733,8 +759,13 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             qs[e] = qq * d * d;
             lo[e] = lo_;
             hi[e] = hi_;
-            x[e] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
-            XR[j] = x[e];
+            if (resumed) {   // (XR holds the suspended solve's restart point)
+                x[e] = a.xs[b];
+                xs[e] = L.xsum[b];
+            } else {
+                x[e] = clampd((a.warm & 1) ? a.xs_in[b] : 0.0, lo_, hi_);
+                XR[j] = x[e];
+            }
             Xl[t + e * NT] = x[e];
         }
         y[e] = ys[e] = axo[e] = rlo[e] = rhi[e] = 0.0;
@@ -744,8 +775,13 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             double yy = (a.warm & 1) ? a.ys_in[sm + i] : 0.0;
             if (!fin(rlo[e])) yy = fmin(yy, 0.0); else b2 += rlo[e] * rlo[e];
             if (!fin(rhi[e])) yy = fmax(yy, 0.0); else b2 += rhi[e] * rhi[e];
+            if (resumed) {
+                yy = a.ys[sm + i];
+                ys[e] = L.ysum[sm + i];
+            } else {
+                YR[i] = yy;
+            }
             y[e] = yy;
-            YR[i] = yy;
             Yl[t + e * NT] = yy;
         }
     }
@@ -759,7 +795,12 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         if (!fin(l_lo)) yy = fmin(yy, 0.0); else if (kw == 0) b2 += l_lo * l_lo;
         if (!fin(l_hi)) yy = fmax(yy, 0.0); else if (kw == 0) b2 += l_hi * l_hi;
         l_y = l_yr = yy;
-        yl[t] = yy;
+        if (resumed) {   // (the linking rows' restart point is kept in YR by the suspending slot)
+            l_y = a.ys[sm + l_i];
+            l_ys = L.ysum[sm + l_i];
+            l_yr = YR[l_i];
+        }
+        yl[t] = l_y;
     }
     double omega, cnorm;
     {
@@ -771,6 +812,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         omega = (cn > 1e-10 && bn > 1e-10) ? cn / bn : 1.0;
         if ((a.warm & 2) && a.omega_in[s] > 0.0) omega = a.omega_in[s];
         else if ((a.warm & 4) && a.omega_in[s] > 0.0) omega = sqrt(omega * a.omega_in[s]);
+        if (resumed) omega = SV[0];
     }
     const double bnorm = a.bnorm[s], eta = a.eta[s];
     double tau = eta / omega, sig = eta * omega;
@@ -787,7 +829,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         settle();
 #pragma unroll
         for (int e = 0; e < E; ++e)
-            if (cv_[e]) aty[e] = aty_col(yl, t + e * NT);
+            if (cv_[e]) aty[e] = aty_col(t + e * NT);
     };
     products();
 
@@ -840,13 +882,20 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         return sqrt(w * w * o[0] + o[1] / (w * w) + g * g);
     };
     double kkt_restart, kkt_prev = INFINITY;
-    {
+    int it = 0, since = 0, cnt = 0, st = 1;
+    if (resumed) {
+        kkt_restart = SV[1];
+        kkt_prev = SV[2];
+        it = (int)SV[3];
+        since = (int)SV[4];
+        cnt = (int)SV[5];
+    } else {
         double o[6];
         kkt_part(false, 0.0, nullptr, nullptr, 0.0, o);
         scen_sum(o);
         kkt_restart = wkkt_of(o, omega);
     }
-    int it = 0, since = 0, cnt = 0, st = 1;
+    bool suspend = false;
     double rel_final = INFINITY, pobj = 0.0, dobj = 0.0;
     bool use_avg_final = false;
     const int chk = a.check_every;
@@ -894,7 +943,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
 #pragma unroll
                 for (int e = 0; e < E; ++e)
                     if (cv_[e] && loc_[e]) {
-                        aty[e] = aty_col(yl, t + e * NT);
+                        aty[e] = aty_col(t + e * NT);
                         // the next iteration's primal step of this column: its A^T y is complete
                         // (no linking row), and every read of Xl of this iteration has passed the
                         // exchange's barrier
@@ -911,7 +960,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             settle();
 #pragma unroll
             for (int e = 0; e < E; ++e)
-                if (cv_[e] && !loc_[e]) aty[e] = aty_col(yl, t + e * NT);
+                if (cv_[e] && !loc_[e]) aty[e] = aty_col(t + e * NT);
             PF(5);
         }
         if (!alive) break;
@@ -920,7 +969,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         cnt += chk;
 
         const double inv = 1.0 / (double)cnt;
-        // products at the average: stage the running sums in Xl / Yl / ylx, gather, restore
+        // products at the average: stage the running sums in Xl / Yl / yl, gather, restore
         double axa[E], ata[E];
         __syncthreads();   // every ATY gather of the last iteration is done with Yl
 #pragma unroll
@@ -928,12 +977,12 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             if (cv_[e]) Xl[t + e * NT] = xs[e];
             if (rv_[e]) Yl[t + e * NT] = ys[e];
         }
-        if (t < NL) ylx[t] = l_ys;
+        if (t < NL) yl[t] = l_ys;
         __syncthreads();
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             axa[e] = rv_[e] ? ax_loc(t + e * NT) : 0.0;
-            ata[e] = cv_[e] ? aty_col(ylx, t + e * NT) : 0.0;
+            ata[e] = cv_[e] ? aty_col(t + e * NT) : 0.0;
         }
         const double l_axs = exchange(ax_link());
         settle();   // every gather of the staged sums is done
@@ -943,16 +992,24 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             if (cv_[e]) Xl[t + e * NT] = x[e];
             if (rv_[e]) Yl[t + e * NT] = y[e];
         }
+        if (t < NL) yl[t] = l_y;
         double oc[6], oa[6];
         kkt_part(false, 0.0, nullptr, nullptr, 0.0, oc);
         kkt_part(true, inv, axa, ata, l_axs, oa);
         {
-            double both[12];
+            // [12]: 1 when workgroup 0 decides to suspend the solve at this check (split solves):
+            // the same decision in every workgroup of the slot
+            double both[13];
 #pragma unroll
             for (int u = 0; u < 6; ++u) { both[u] = oc[u]; both[6 + u] = oa[u]; }
+            both[12] = 0.0;
+            if (B.slice > 0 && !resumed && kw == 0 && t == 0 && it >= B.slice * chk &&
+                __hip_atomic_load(L.ctrl + kCtrlHead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)a.S)
+                both[12] = 1.0;
             scen_sum(both);   // (its workgroup barriers also publish the restored Xl / Yl)
 #pragma unroll
             for (int u = 0; u < 6; ++u) { oc[u] = both[u]; oa[u] = both[6 + u]; }
+            suspend = both[12] > 0.5;
         }
         const double rel_cur = rel_of(oc), rel_avg = rel_of(oa);
         const bool nan = !(rel_cur == rel_cur);
@@ -962,6 +1019,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             pobj = use_avg_final ? oa[4] : oc[4];
             dobj = use_avg_final ? oa[5] : oc[5];
             st = nan ? 2 : ((rel_cur <= a.eps || rel_avg <= a.eps) ? 0 : 1);
+            suspend = false;   // terminated at this check: nothing to resume
             break;
         }
         const double k_cur = wkkt_of(oc, omega), k_avg = wkkt_of(oa, omega);
@@ -1015,11 +1073,54 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             kkt_prev = INFINITY;
             if (use_avg) products();
         }
+        if (suspend) break;
     }
     // a scenario given up (a co-resident workgroup missing: the bounded wait expired) reports status 2;
     // its x is NOT a consistent iterate -- columns without a linking-row entry may already have taken
     // the next iteration's primal step -- and callers treat status 2 as a failed solve
     if (!alive) { st = 2; rel_final = NAN; }
+
+    if (alive && suspend) {   // save the solve's state, release it, re-queue the scenario
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (cv_[e]) {
+                a.xs[sn + jc[e]] = x[e];
+                L.xsum[sn + jc[e]] = xs[e];
+            }
+            if (rv_[e]) {
+                a.ys[sm + ir[e]] = y[e];
+                L.ysum[sm + ir[e]] = ys[e];
+            }
+        }
+        if (kw == 0 && t < NL) {
+            a.ys[sm + l_i] = l_y;
+            L.ysum[sm + l_i] = l_ys;
+            YR[l_i] = l_yr;
+        }
+        if (kw == 0 && t == 0) {
+            SV[0] = omega;
+            SV[1] = kkt_restart;
+            SV[2] = kkt_prev;
+            SV[3] = (double)it;
+            SV[4] = (double)since;
+            SV[5] = (double)cnt;
+            if constexpr (PROF) pf_scen[3] += 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        barrier();   // every workgroup of the slot has released its part
+        if (kw == 0 && t == 0) {
+            const unsigned j = __hip_atomic_fetch_add(L.ctrl + kCtrlTail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(B.requeue + j, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!alive) break;
+        __syncthreads();
+        continue;
+    }
 
     // ------------------------------------------------------------------ outputs
     const double inv = cnt > 0 ? 1.0 / (double)cnt : 0.0;
@@ -1057,6 +1158,11 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         a.iters[s] = it;
         a.iters_acc[s] += it;
         a.status[s] = st;
+        if (B.slice > 0) __hip_atomic_fetch_add(L.ctrl + kCtrlDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (PROF) {
+            pf_scen[1] = __builtin_amdgcn_s_memrealtime();
+            pf_scen[2] = (unsigned long long)it;
+        }
     }
     if constexpr (PROF) {
         PF(7);
@@ -1088,7 +1194,7 @@ size_t pdhg_border_granule_words(const BorderLayout& B, const StreamLayout& L) {
 
 size_t pdhg_border_lds_bytes(const BorderLayout& B) {
     if (B.reg)   // register-resident: x / y in LDS, no column / row lists
-        return (size_t)(B.nrz_max + B.nlz_max + B.ncz_max + B.C_max + B.R_max + 2 * B.nlink + B.xtmp_len) * sizeof(double) +
+        return (size_t)(B.nrz_max + B.nlz_max + B.ncz_max + B.C_max + B.R_max + B.nlink + B.xtmp_len) * sizeof(double) +
                (size_t)(B.R_max + 1 + B.nrz_max + B.nlink + 1 + B.nlz_max + B.C_max + 1 + B.ncz_max) * sizeof(int);
     return (size_t)(B.nrz_max + B.nlz_max + B.ncz_max + 2 * B.nlink) * sizeof(double) +
            (size_t)(B.C_max + B.R_max + B.R_max + 1 + B.nrz_max + B.nlink + 1 + B.nlz_max + B.C_max + 1 + B.ncz_max) *
@@ -1108,6 +1214,10 @@ hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream) {
     const StreamLayout& L = a.st;
     hipError_t e = hipMemsetAsync(L.ctrl, 0, (size_t)(kCtrlBar + 3 * L.slots) * sizeof(unsigned), stream);
     if (e != hipSuccess) return e;
+    if (a.bd.reg && a.bd.slice > 0) {   // split solves: the re-queue starts empty
+        e = hipMemsetAsync(a.bd.requeue, 0, (size_t)a.S * sizeof(int), stream);
+        if (e != hipSuccess) return e;
+    }
     if (a.bd.reg && L.K > 1) {   // tagged granules start from tag 0 every launch
         e = hipMemsetAsync(a.bd.plink, 0, pdhg_border_granule_words(a.bd, L) * sizeof(unsigned long long), stream);
         if (e != hipSuccess) return e;

@@ -1594,7 +1594,7 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
             B.nlz_max = vmax(nlz4);
             B.ncz_max = vmax(ncz4);
             B.xtmp_len = std::max(B.nlink + K, 16 * K);
-            B.xtmp_len += (B.C_max + B.R_max + B.xtmp_len) & 1;
+            B.xtmp_len += (B.C_max + B.R_max + B.nlink + B.xtmp_len) & 1;
             bytes = pdhg_border_lds_bytes(B);
             if (bytes > budget) B.reg = 0;   // the memory-resident variant needs less LDS
         }
@@ -1723,6 +1723,21 @@ static int build_border_layout(phg_handle* h, const phg_batch* b, const std::vec
     if (dalloc(h, &d, Sm)) return -1; L.axo = d;
     if (dalloc(h, &d, Sm)) return -1; L.yr = d;
     if (dalloc(h, &d, (size_t)L.slots * K * 16)) return -1; L.part = d;
+    // split solves (pdhg_border.hip): with more scenarios than slots, a solve past slice x
+    // check_every iterations during the first pass is suspended and re-queued (PHG_BORDER_SLICE,
+    // 0 = off)
+    B.slice = 0;
+    if (B.reg && b->S > L.slots) {
+        B.slice = 8;
+        if (const char* es = std::getenv("PHG_BORDER_SLICE")) B.slice = std::max(0, std::atoi(es));
+    }
+    if (B.slice > 0) {
+        int* rq;
+        if (dalloc(h, &rq, (size_t)b->S)) return -1;
+        B.requeue = rq;
+        if (dalloc(h, &d, (size_t)b->S * 8)) return -1;
+        B.susp = d;
+    }
     unsigned* u;
     if (dalloc(h, &u, (size_t)kCtrlBar + 3 * (size_t)L.slots)) return -1; L.ctrl = u;
     int* e;
@@ -2577,16 +2592,25 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         static size_t pcap = 0;
         const size_t nwg = (size_t)h->st.slots * h->st.K;
         const bool on = bprof && h->bd.reg;
-        if (on && pcap < nwg * 10) {
+        const size_t need = nwg * 10 + (size_t)h->S * 4;   // + per scenario {start, end, iterations, splits}
+        if (on && pcap < need) {
             if (pbuf) CK(hipFree(pbuf));
-            CK(hipMalloc((void**)&pbuf, nwg * 10 * sizeof(unsigned long long)));
-            pcap = nwg * 10;
+            CK(hipMalloc((void**)&pbuf, need * sizeof(unsigned long long)));
+            pcap = need;
         }
         if (on) CK(hipMemsetAsync(pbuf, 0, pcap * sizeof(unsigned long long), h->stream));
         a.prof = on ? pbuf : nullptr;
         CK(pdhg_border_launch(a, h->stream));
+        // PHG_BORDER_STATS=1 (diagnostic, read every launch): the number of split (suspended and
+        // re-queued) solves of the launch, to stderr (synchronises the stream)
+        if (h->bd.slice > 0 && std::getenv("PHG_BORDER_STATS")) {
+            unsigned tail = 0;
+            CK(hipMemcpyAsync(&tail, h->st.ctrl + kCtrlTail, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+            CK(hipStreamSynchronize(h->stream));
+            fprintf(stderr, "PHG_BORDER_SPLIT slice %d suspended %u of %d\n", h->bd.slice, tail, h->S);
+        }
         if (on) {
-            std::vector<unsigned long long> hb(nwg * 10);
+            std::vector<unsigned long long> hb(need);
             CK(hipMemcpyAsync(hb.data(), pbuf, hb.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
             CK(hipStreamSynchronize(h->stream));
             double t[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -2604,6 +2628,25 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
                     h->st.K, h->st.slots, t[8] / h->st.K, t[9] / h->st.K, span / 100.0, t[0] / 100.0 / it,
                     t[1] / 100.0 / it, t[2] / 100.0 / it, t[3] / 100.0 / it, t[4] / 100.0 / it, t[5] / 100.0 / it,
                     t[6] / 100.0 / it, t[7] / 100.0 / it);
+            // per scenario: the launch's first start and last end, the heaviest scenario's start offset,
+            // span and time per iteration, and the latest first start
+            const unsigned long long* sc = hb.data() + nwg * 10;
+            unsigned long long t0 = ~0ull, t1 = 0, late = 0;
+            int hv = 0;
+            double splits = 0;
+            for (int q = 0; q < h->S; ++q) {
+                t0 = std::min(t0, sc[q * 4]);
+                t1 = std::max(t1, sc[q * 4 + 1]);
+                if (sc[q * 4 + 2] > sc[hv * 4 + 2]) hv = q;
+                splits += (double)sc[q * 4 + 3];
+            }
+            for (int q = 0; q < h->S; ++q) late = std::max(late, sc[q * 4] - t0);
+            const double hdur = (double)(sc[hv * 4 + 1] - sc[hv * 4]) / 100.0;
+            fprintf(stderr,
+                    "PHG_BORDER_SCEN span_us %.1f heaviest s%d iters %llu start_us %.1f span_us %.1f us_per_iter %.3f "
+                    "latest_start_us %.1f splits %.0f\n",
+                    (double)(t1 - t0) / 100.0, hv, sc[hv * 4 + 2], (double)(sc[hv * 4] - t0) / 100.0, hdur,
+                    hdur / std::max(1.0, (double)sc[hv * 4 + 2]), (double)late / 100.0, splits);
         }
     }
     else if (h->stream_layout) CK(pdhg_stream_launch(a, h->stream));

@@ -165,9 +165,16 @@ struct BorderLayout {
                                      // (register variant: tagged 8-byte granules, two per partial)
     int reg;                         // 0: memory-resident kernel; E = 2: register-resident, E elements per thread
     int xtmp_len;                    // register variant: LDS doubles staging cross-workgroup partials
+    // register variant, split solves (pdhg_border.hip): a solve still running after slice x
+    // check_every iterations during the queue's first pass is suspended and re-queued (0: off)
+    int slice;
+    int* requeue;                    // [S] suspended scenarios + 1, in suspension order (zeroed per launch)
+    double* susp;                    // [S][8] suspended solves' scalar state
 };
 
 constexpr int kCtrlHead = 0;     // StreamLayout::ctrl: queue head
+constexpr int kCtrlTail = 1;     //   re-queued (suspended) scenarios so far (bordered split solves)
+constexpr int kCtrlDone = 2;     //   scenarios finished (bordered split solves)
 constexpr int kCtrlBar = 16;     //   then 2 words per slot (barrier counter), then 1 per slot (mailbox)
 
 struct PdhgArgs {

@@ -141,6 +141,45 @@ def test_netdes_delta_values(monkeypatch):
     np.testing.assert_allclose(res["delta"][1][:4], o.obj, rtol=1e-6)
 
 
+def test_border_split_solves_match_uninterrupted(monkeypatch, capfd):
+    """Split solves (pdhg_border.hip, BorderLayout::slice): with more scenarios than slots, a solve
+    still running after slice x check_every PDHG iterations while the queue's first pass lasts is
+    suspended at that check and re-queued; resuming restores its iterate, running sums, restart point
+    and restart / step state and recomputes A x / A^T y with the same gathers, so Iter0 and three PH
+    iterations give bit-identical objectives, bounds, iteration counts and nonants to
+    uninterrupted solves.
+    24 scenarios of a 24-unit x 12-period UC LP on 16 slots (PHG_STREAM_K=16); slice 1 suspends at
+    the first check past 32 iterations, and the launch reports how many solves it split."""
+    monkeypatch.setenv("PHG_STREAM_K", "16")
+    monkeypatch.setenv("PHG_BORDER_STATS", "1")
+    S = 24
+    kw = {"num_gens": 24, "num_periods": 12, "num_scens": S}
+    res = {}
+    for sl in ("0", "1"):
+        monkeypatch.setenv("PHG_BORDER_SLICE", sl)
+        ph = PH(_opts(pdhg_layout="border", pdhg_check_every=32, pdhg_max_iter=20000), uc.scenario_names_creator(S),
+                uc.scenario_creator, scenario_creator_kwargs=kw)
+        ph.PH_Prep()
+        assert ph.engine.layout == "border" and ph.engine.variant >= 600   # the register-resident kernel
+        capfd.readouterr()
+        ph.Iter0()
+        r = [ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get(_lib.F_BOUND).copy(),
+             ph.engine.get_i32(_lib.I_ITERS).copy(), ph.nonants().copy()]
+        for _ in range(3):   # (warm-started PH solves end near the first checks: a termination at the
+            ph.Compute_Xbar()   # check that would suspend must not suspend)
+            ph.Update_W()
+            ph.solve_loop()
+            r += [ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get(_lib.F_BOUND).copy(),
+                  ph.engine.get_i32(_lib.I_ITERS).copy(), ph.nonants().copy(), ph.engine.get_i32(_lib.I_STATUS).copy()]
+        err = capfd.readouterr().err
+        split = [int(ln.split()[4]) for ln in err.splitlines() if ln.startswith("PHG_BORDER_SPLIT")]
+        res[sl] = (r, split)
+    (ra, sa), (rb, sb) = res["0"], res["1"]
+    assert sa == [] and len(sb) >= 2 and sb[0] > 0, (sa, sb)
+    for a, b in zip(ra, rb):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_border_matches_block_kernel(monkeypatch):
     """The bordered block-diagonal kernel (pdhg_border.hip: 16 workgroups per scenario, one block
     per unit, the 24-nonzero demand / reserve rows as linking rows) runs the same arithmetic as the
