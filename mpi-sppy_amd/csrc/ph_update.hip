@@ -10,6 +10,7 @@
 // all-reduce (RCCL) of the 2*N_tot node sums and of the 2*P+2 convergence partials happens
 // between / after the kernels (see include/phg.h).
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "phg_internal.h"
@@ -134,6 +135,7 @@ __device__ __forceinline__ void finish_k(unsigned* counter, unsigned* done, int 
 // nonant) -> coalesced rows of xN, 8 rows in flight per thread.  The last K workgroups then add
 // every node's segment partials in segment order (element range split K ways):
 // nodesum[e] = sum p x, nodesum[N_tot + e] = sum p x^2 (the buffer the cross-GPU all-reduce sums).
+template <bool NTL = false>
 __device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
     __shared__ double sh[2 * 512];
     const int tid = threadIdx.x;
@@ -150,7 +152,16 @@ __device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
         double s1a = 0.0, s1b = 0.0, s2a = 0.0, s2b = 0.0;
         if (so < q2) {
             const long kg = sg.kofs + k0 + 2 * k2;
-            auto ld = [&](int s) { return *reinterpret_cast<const double2*>(a.xN + (long)s * a.N + kg); };
+            auto ld = [&](int s) {
+                const double2* p = reinterpret_cast<const double2*>(a.xN + (long)s * a.N + kg);
+                if constexpr (NTL) {   // (x is read once here)
+                    typedef double d2v __attribute__((ext_vector_type(2)));
+                    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+                    return double2(v.x, v.y);
+                } else {
+                    return *p;
+                }
+            };
             auto pr = [&](int s) { return a.pc[(long)s * a.L + sg.level]; };
             int s = sg.s0 + so;
             constexpr int R = 8;
@@ -330,11 +341,12 @@ __device__ void fold_conv_segment(const PhArgs& a, int b) {
 // the last workgroup's part of convergence_diff (declared here, defined below)
 __device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart);
 
+template <bool NTL>
 __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
     // folded update pending: its conv segments ride along (the packed buffer's partials region)
     if (a.fold_conv && blockIdx.y == 0)
         for (int b = blockIdx.x; b < a.n_cseg; b += gridDim.x) fold_conv_segment(a, b);
-    node_sum_partials(a);
+    node_sum_partials<NTL>(a);
     const int K = min(a.n_final, (int)(gridDim.x * gridDim.y));
     const int rank = last_k_workgroups(a.ticket, K);
     if (rank < 0) return;
@@ -736,7 +748,13 @@ hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double*
 }
 
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
-    hipLaunchKernelGGL(node_sums_kernel, dim3(a.n_seg, (a.maxk + 255) / 256), dim3(256), 0, st, a, nodesum);
+    // nontemporal loads of x (read once here) when x is far larger than the caches: S N = 1e8 (1e6 x
+    // 100), node sums 159.6 vs 177.2 us (4.5 -> 5.2 TB/s); farmer 10k (x just written by the solve,
+    // cache-resident) keeps plain loads.  PHG_NODESUM_NT=0 / 1 forces either
+    static const int ntenv = [] { const char* e = std::getenv("PHG_NODESUM_NT"); return e ? std::atoi(e) : -1; }();
+    const bool ntl = ntenv >= 0 ? ntenv == 1 : (long)a.S * a.N >= 10000000L;
+    if (ntl) hipLaunchKernelGGL(node_sums_kernel<true>, dim3(a.n_seg, (a.maxk + 255) / 256), dim3(256), 0, st, a, nodesum);
+    else hipLaunchKernelGGL(node_sums_kernel<false>, dim3(a.n_seg, (a.maxk + 255) / 256), dim3(256), 0, st, a, nodesum);
     return hipGetLastError();
 }
 
