@@ -181,13 +181,23 @@ __device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
                     ub[u] += p[u] * xv[u].y * xv[u].y;
                 }
             }
-            for (; s < sg.s1; s += q2) {
-                const double2 xv = ld(s);
-                const double p = pr(s);
-                ta[0] += p * xv.x;
-                tb[0] += p * xv.y;
-                ua[0] += p * xv.x * xv.x;
-                ub[0] += p * xv.y * xv.y;
+            // the remainder (fewer than R rows of this lane): every load issued first, then the rows
+            // added in order into accumulator 0 (the same order, the same bits as one row at a time;
+            // small batches are all remainder: one round trip instead of one per row)
+            {
+                double2 xv[R];
+                double p[R];
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+                    if (s + u * q2 < sg.s1) { xv[u] = ld(s + u * q2); p[u] = pr(s + u * q2); }
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+                    if (s + u * q2 < sg.s1) {
+                        ta[0] += p[u] * xv[u].x;
+                        tb[0] += p[u] * xv[u].y;
+                        ua[0] += p[u] * xv[u].x * xv[u].x;
+                        ub[0] += p[u] * xv[u].y * xv[u].y;
+                    }
             }
             s1a = ((ta[0] + ta[1]) + (ta[2] + ta[3])) + ((ta[4] + ta[5]) + (ta[6] + ta[7]));
             s1b = ((tb[0] + tb[1]) + (tb[2] + tb[3])) + ((tb[4] + tb[5]) + (tb[6] + tb[7]));
@@ -234,11 +244,17 @@ __device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
 #pragma unroll
                 for (int u = 0; u < R; ++u) { t1[u] += p[u] * xv[u]; t2[u] += p[u] * xv[u] * xv[u]; }
             }
-            for (; s < sg.s1; s += q) {
-                double p, xv;
-                px(s, p, xv);
-                t1[0] += p * xv;
-                t2[0] += p * xv * xv;
+            {   // the remainder: loads first, then added in row order (as in the pairs path)
+                double p[R], xv[R];
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+                    if (s + u * q < sg.s1) px(s + u * q, p[u], xv[u]);
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+                    if (s + u * q < sg.s1) {
+                        t1[0] += p[u] * xv[u];
+                        t2[0] += p[u] * xv[u] * xv[u];
+                    }
             }
             s1 = ((t1[0] + t1[1]) + (t1[2] + t1[3])) + ((t1[4] + t1[5]) + (t1[6] + t1[7]));
             s2 = ((t2[0] + t2[1]) + (t2[2] + t2[3])) + ((t2[4] + t2[5]) + (t2[6] + t2[7]));
@@ -257,9 +273,9 @@ __device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
 }
 
 // final node sums of elements [e_lo, e_hi) (rank `rank` of K): per node, its segments' partials in
-// segment order (written with the given store: plain, or sc1 when other workgroups of the same
-// launch read them)
-template <bool PUBLISH>
+// segment order, written with the given store -- MODE 0: plain; 1: sc1, and x-bar / x-sq-bar too
+// (ph_step_kernel); 2: sc1, node sums only (other workgroups of the same launch read them)
+template <int MODE>
 __device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum, int rank, int K) {
     const int tid = threadIdx.x;
     // elements [e_lo, e_hi) of this rank; T lanes per element (power of two <= 64), each summing
@@ -293,11 +309,13 @@ __device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum,
             t2 += __shfl_xor(t2, o, 64);
         }
         if (e < e_hi && sub == 0) {
-            if (PUBLISH) {
+            if (MODE >= 1) {
                 publish(&nodesum[e], t1);
                 publish(&nodesum[a.N_tot + e], t2);
-                publish(&a.xbar[e], t1);
-                publish(&a.xsqbar[e], t2);
+                if (MODE == 1) {
+                    publish(&a.xbar[e], t1);
+                    publish(&a.xsqbar[e], t2);
+                }
             } else {
                 nodesum[e] = t1;
                 nodesum[a.N_tot + e] = t2;
@@ -341,8 +359,12 @@ __device__ void fold_conv_segment(const PhArgs& a, int b) {
 // the last workgroup's part of convergence_diff (declared here, defined below)
 __device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart);
 
-template <bool NTL>
-__global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum) {
+// HEADX (phg_ph_step on one GPU with the folded update): the x-bar head rides along -- the last of
+// the K ranks to finish (every node sum published) reduces the conv partials, computes conv
+// exactly as xbar_head_kernel does from the same buffer, publishes the gate and, unless conv is
+// below head_thr, copies the node sums into x-bar / x-sq-bar: one launch instead of two.
+template <bool NTL, bool HEADX>
+__global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum, double head_thr, int first) {
     // folded update pending: its conv segments ride along (the packed buffer's partials region)
     if (a.fold_conv && blockIdx.y == 0)
         for (int b = blockIdx.x; b < a.n_cseg; b += gridDim.x) fold_conv_segment(a, b);
@@ -350,12 +372,45 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
     const int K = min(a.n_final, (int)(gridDim.x * gridDim.y));
     const int rank = last_k_workgroups(a.ticket, K);
     if (rank < 0) return;
-    node_sum_final<false>(a, nodesum, rank, K);
-    if (a.fold_conv && rank == K - 1) {
+    if constexpr (!HEADX) {
+        node_sum_final<0>(a, nodesum, rank, K);
+        if (a.fold_conv && rank == K - 1) {
+            __syncthreads();
+            conv_partials_final(a, nodesum + 2 * (long)a.N_tot);
+        }
+        finish_k(a.ticket, a.ticket + 2, K);
+    } else {
+        __shared__ double red256[256];
+        __shared__ int s_last;
+        node_sum_final<2>(a, nodesum, rank, K);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        conv_partials_final(a, nodesum + 2 * (long)a.N_tot);
+        if (threadIdx.x == 0) {
+            const unsigned prev = __hip_atomic_fetch_add(a.ticket + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = prev == (unsigned)K - 1;
+            if (s_last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        if (!s_last) return;
+        double* convpart = nodesum + 2 * (long)a.N_tot;
+        if (a.fold_conv) conv_partials_final(a, convpart);
+        __syncthreads();
+        const double conv = first ? INFINITY : conv_value_block(convpart, a.P, red256);
+        if (threadIdx.x == 0) publish_gate(conv, convpart, a.P, a.gate, a.gate_host, a.gate_seq);
+        if (conv >= head_thr)
+            for (long j = threadIdx.x; j < a.N_tot; j += 256) {
+                a.xbar[j] = nodesum[j];
+                a.xsqbar[j] = nodesum[a.N_tot + j];
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) {   // every rank is past both counters: re-arm them for the next launch
+            __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.ticket + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    finish_k(a.ticket, a.ticket + 2, K);
 }
 
 // fixed-order sum of v[first..last) by all 256 threads of the workgroup (same result in every thread)
@@ -606,7 +661,7 @@ __global__ __launch_bounds__(256) void ph_step_kernel(PhArgs a, double* packed, 
     const int K = min(min(128, a.n_cseg), (int)(gridDim.x * gridDim.y));
     const int rank = last_k_workgroups(a.fticket, K);
     if (rank < 0) return;
-    node_sum_final<true>(a, nodesum, rank, K);
+    node_sum_final<1>(a, nodesum, rank, K);
     // the K ranks meet: every node sum / x-bar published (sc1 stores, drained) before the W update
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -753,8 +808,20 @@ hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
     // cache-resident) keeps plain loads.  PHG_NODESUM_NT=0 / 1 forces either
     static const int ntenv = [] { const char* e = std::getenv("PHG_NODESUM_NT"); return e ? std::atoi(e) : -1; }();
     const bool ntl = ntenv >= 0 ? ntenv == 1 : (long)a.S * a.N >= 10000000L;
-    if (ntl) hipLaunchKernelGGL(node_sums_kernel<true>, dim3(a.n_seg, (a.maxk + 255) / 256), dim3(256), 0, st, a, nodesum);
-    else hipLaunchKernelGGL(node_sums_kernel<false>, dim3(a.n_seg, (a.maxk + 255) / 256), dim3(256), 0, st, a, nodesum);
+    const dim3 grid(a.n_seg, (a.maxk + 255) / 256);
+    if (ntl) hipLaunchKernelGGL((node_sums_kernel<true, false>), grid, dim3(256), 0, st, a, nodesum, 0.0, 0);
+    else hipLaunchKernelGGL((node_sums_kernel<false, false>), grid, dim3(256), 0, st, a, nodesum, 0.0, 0);
+    return hipGetLastError();
+}
+
+// node sums + the x-bar head of the folded pipelined iteration in one launch (node_sums_kernel
+// HEADX; one GPU: packed is the handle's own buffer, nothing is exchanged between the two)
+hipError_t node_sums_head_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st) {
+    static const int ntenv = [] { const char* e = std::getenv("PHG_NODESUM_NT"); return e ? std::atoi(e) : -1; }();
+    const bool ntl = ntenv >= 0 ? ntenv == 1 : (long)a.S * a.N >= 10000000L;
+    const dim3 grid(a.n_seg, (a.maxk + 255) / 256);
+    if (ntl) hipLaunchKernelGGL((node_sums_kernel<true, true>), grid, dim3(256), 0, st, a, packed, thr, first);
+    else hipLaunchKernelGGL((node_sums_kernel<false, true>), grid, dim3(256), 0, st, a, packed, thr, first);
     return hipGetLastError();
 }
 

@@ -56,6 +56,7 @@ hipError_t pdhg_mfma_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t piece_gather_launch(const double* vals, int nnz, const int* perm, int E, int S, double* out,
                                hipStream_t st);
 hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st);
+hipError_t node_sums_head_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st);
 hipError_t broadcast_row_launch(const double* row, int N, int S, double* out, hipStream_t st);
 hipError_t unscale_launch(const double* sv, const double* d, long cnt, double* out, hipStream_t st);
 hipError_t w_update_launch(const PhArgs& a, const double* nodesum, double* convpart, hipStream_t st);
@@ -986,7 +987,9 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
         long loads = 0;
         for (int g = 0; g < b->n_nodes; ++g)   // nodes without local scenarios have no segments
             if (node_level[g] >= 0) loads += 2L * (first[g + 1] - first[g]) * b->level_len[node_level[g]];
-        a.n_final = (int)std::min<long>(128, std::max<long>(1, (loads + 2047) / 2048));
+        long per = 2048;   // PHG_NFINAL_LOADS: partial loads per final workgroup (tuning knob)
+        if (const char* ev = std::getenv("PHG_NFINAL_LOADS")) per = std::max(1L, std::atol(ev));
+        a.n_final = (int)std::min<long>(128, std::max<long>(1, (loads + per - 1) / per));
     }
     {
         NodeSeg* p;
@@ -2801,6 +2804,33 @@ int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fu
     const PhArgs& p = h->ph;
     const bool fusable = p.root_only && p.P == 1 && !p.smooth_on && !p.pcv && !h->no_fuse && !fold_active(h);
     if (out_fused) *out_fused = fusable ? 1 : 0;
+    // the folded update on one GPU: node sums + x-bar head in one launch (node_sums_kernel HEADX)
+    // with phg_node_sums' and phg_ph_head's bookkeeping; PHG_FUSE_HEAD=0: the two launches
+    const char* efh = std::getenv("PHG_FUSE_HEAD");   // (read per call: tests switch it)
+    const bool fuse_head = !(efh && std::atoi(efh) == 0);
+    if (!fusable && fuse_head && fold_active(h)) {
+        CK(hipSetDevice(h->device));
+        if (h->fold_w_pending && flush_fold(h)) return -1;
+        if (!h->t_open && timing_event(h, 1, 0)) return -1;
+        if (timing_event(h, 2, 0)) return -1;
+        PhArgs a = h->ph;
+        a.fold_conv = h->fold_conv_pending ? 1 : 0;
+        a.conv_s = h->conv_s;
+        a.fold_st = h->fold_st;
+        a.gate = h->gate;
+        a.gate_host = h->gate_host;
+        a.gate_seq = (double)(++h->gate_seq);
+        CK(node_sums_head_launch(a, h->packed, convthresh, first, h->stream));
+        h->fold_conv_pending = false;
+        if (carry_flushed_partials(h, nullptr)) return -1;
+        if (timing_event(h, 2, 1)) return -1;
+        if (timing_event(h, 1, 1)) return -1;
+        h->t_open = false;
+        h->fold_w_pending = true;
+        h->fold_thr = first ? -INFINITY : convthresh;
+        h->gate_fused = false;
+        return 0;
+    }
     if (!fusable) {
         if (phg_node_sums(h, nullptr)) return -1;
         return phg_ph_head(h, nullptr, convthresh, first);
