@@ -44,6 +44,11 @@ def parse():
                     help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes, 2000 hydro, 64 uc")
     ap.add_argument("--cm", type=int, default=10)
     ap.add_argument("--rho", type=float, default=1.0)
+    ap.add_argument("--uc-rho", default="default", choices=["cost", "default"],
+                    help="uc: --rho everywhere (default: the per-PH-iteration numbers of rounds 1-4) or the "
+                         "reference UC's cost-based rho setter (examples/uc/uc_funcs.py:112-132, 0.1 x the "
+                         "unit's cost at mid output, as uc_cylinders.py passes it): PH converges ~17x further in "
+                         "60 s, each early PH iteration's solves ~15x heavier (DESIGN.md (d))")
     ap.add_argument("--eps", type=float, default=None,
                     help="PDHG relative KKT tolerance (default 1e-9; uc 1e-6: at n ~ 2e4 PDHG needs > 2e5 "
                          "iterations per solve for 1e-9)")
@@ -130,6 +135,8 @@ def _case_setup(args, S, farmer, hydro, netdes, sslp, uc=None):
     elif args.case == "uc":
         names, creator, ckw = uc.scenario_names_creator(S), uc.scenario_creator, {"num_scens": S}
         desc = "synthetic UC-shaped LP relaxation (85 generators x 48 periods, N = 4080)"
+        if args.uc_rho == "cost":
+            desc += ", cost-based rho (the reference's uc rho setter)"
     else:
         names, creator, ckw = netdes.scenario_names_creator(S), netdes.scenario_creator, {"num_scens": S}
         desc = "netdes network-50-30-H-01 LP relaxation"
@@ -217,7 +224,9 @@ def main():
             "pdhg_exchange": force_dist}
     args.creator_kwargs = ckw
     t_setup = time.perf_counter()
-    ph = PH(dict(opts), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw, all_nodenames=nodenames)
+    rho_setter = uc.rho_setter if args.case == "uc" and args.uc_rho == "cost" else None
+    ph = PH(dict(opts), names, creator, mpicomm=comm, scenario_creator_kwargs=ckw, all_nodenames=nodenames,
+            rho_setter=rho_setter)
     ph.PH_Prep()
     t_iter0 = time.perf_counter()
     ph.Iter0()
@@ -479,7 +488,8 @@ def main():
         names_c, creator_c, ckw_c, nodenames_c, _ = _case_setup(args, S_c, farmer, hydro, netdes, sslp, uc)
         copts = dict(opts, PHIterLimit=args.conv_iters, convthresh=1e-4,
                      time_limit=None if args.case == "farmer" else args.conv_time)
-        ph2 = PH(copts, names_c, creator_c, mpicomm=comm, scenario_creator_kwargs=ckw_c, all_nodenames=nodenames_c)
+        ph2 = PH(copts, names_c, creator_c, mpicomm=comm, scenario_creator_kwargs=ckw_c, all_nodenames=nodenames_c,
+                 rho_setter=rho_setter)
         ph2.PH_Prep()
         torch.cuda.synchronize()
         if comm is not None:

@@ -85,8 +85,28 @@ def scenario_creator(scenario_name, num_gens=85, num_periods=48, num_scens=None)
           [(su[(g, t)], sc[g]) for g, t in idx]
     m.set_objective(obj, lm.minimize)
     m._mpisppy_node_list = [ScenarioNode("ROOT", 1.0, 1, None, [m.UnitOn], m)]
+    m._uc_shape = (G, T)
     m._mpisppy_probability = 1.0 / num_scens if num_scens else "uniform"
     return m
+
+
+def scenario_rhos(scenario_instance, rho_scale_factor=0.1):
+    """The reference UC's cost-based rho (``examples/uc/uc_funcs.py:112-132``, the setter
+    ``uc_cylinders.py:93`` passes to PH): rho of UnitOn[g,t] = rho_scale_factor x the cost of running
+    unit g at the midpoint of its output range -- egret's ComputeProductionCosts(avg_power) +
+    MinimumProductionCost there, this model's mc_g avg_power + nl_g here."""
+    G, T = scenario_instance._uc_shape
+    pmax, mc, _, _, _ = _gen_data(G, T)
+    pmin = 0.3 * pmax
+    nl = 0.1 * mc * pmax
+    avg_power = pmin + (pmax - pmin) / 2.0
+    return [(scenario_instance.UnitOn[(g, t)], rho_scale_factor * (mc[g] * avg_power[g] + nl[g]))
+            for t in range(T) for g in range(G)]
+
+
+def rho_setter(scenario_instance, **kwargs):
+    """``uc_funcs._rho_setter`` (``uc_funcs.py:112-114``)."""
+    return scenario_rhos(scenario_instance, **kwargs)
 
 
 def scenario_names_creator(num_scens, start=None):
