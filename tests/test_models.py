@@ -143,3 +143,21 @@ def test_uc_sizes():
     # scenarios differ in demand (right-hand side) and derates (matrix values)
     a, b = m.arrays(), uc.scenario_creator("Scenario3").arrays()
     assert not np.array_equal(a["row_lo"], b["row_lo"]) and not np.array_equal(a["vals"], b["vals"])
+
+
+def test_uc_rho_setter_restates_reference_cost_rho():
+    """examples/uc.py rho_setter restates uc_funcs.py:112-132: one rho per UnitOn[g,t] nonant, 0.1 x
+    the unit's cost at the midpoint of its output range (mc_g (pmin + (pmax - pmin) / 2) + nl_g),
+    the same for every period and scenario; PHBase maps the returned vardata onto the nonant order."""
+    from mpisppy_amd.examples import uc
+    m = uc.scenario_creator("Scenario3", num_gens=6, num_periods=8, num_scens=4)
+    rr = uc.rho_setter(m)
+    nonants = m._mpisppy_node_list[0].nonant_vardata_list
+    assert len(rr) == len(nonants) == 48
+    assert {id(v) for v, _ in rr} == {id(v) for v in nonants}
+    pmax, mc, _, _, _ = uc._gen_data(6, 8)
+    want = 0.1 * (mc * 0.65 * pmax + 0.1 * mc * pmax)
+    for v, r in rr:
+        g = next(g for g in range(6) for t in range(8) if m.UnitOn[(g, t)] is v)
+        assert r == pytest.approx(want[g], rel=1e-15)
+    assert uc.rho_setter(uc.scenario_creator("Scenario1", num_gens=6, num_periods=8, num_scens=4))[5][1] == rr[5][1]
