@@ -43,7 +43,9 @@ def parse():
     ap.add_argument("--scen", type=int, default=None,
                     help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes, 2000 hydro, 64 uc")
     ap.add_argument("--cm", type=int, default=10)
-    ap.add_argument("--rho", type=float, default=1.0)
+    ap.add_argument("--rho", type=float, default=None,
+                    help="PH default rho (default 1.0; netdes 10000, the reference's netdes_demo.bash:6 "
+                         "--default-rho: PH conv < 1e-4 in 33 s there, 4.3e-3 after 60 s at 1.0)")
     ap.add_argument("--uc-rho", default="default", choices=["cost", "default"],
                     help="uc: --rho everywhere (default: the per-PH-iteration numbers of rounds 1-4) or the "
                          "reference UC's cost-based rho setter (examples/uc/uc_funcs.py:112-132, 0.1 x the "
@@ -213,6 +215,8 @@ def main():
         args.scen = default_scen
     if args.eps is None:
         args.eps = 1e-6 if args.case == "uc" else 1e-9
+    if args.rho is None:
+        args.rho = 10000.0 if args.case == "netdes" else 1.0
     S = args.scen * world
     names, creator, ckw, nodenames, desc = _case_setup(args, S, farmer, hydro, netdes, sslp, uc)
     opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
