@@ -28,6 +28,10 @@
 #include "wave_ops.h"
 #include "stream_sync.h"
 
+#ifndef PHG_GGET_SLEEP
+#define PHG_GGET_SLEEP 1   // granule poll interval, s_sleep units of 64 cycles (UC 64: 3 and 8 measured 1-3 % slower)
+#endif
+
 namespace phg {
 
 template <int NT>
@@ -562,7 +566,7 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
                 __hip_atomic_store(L.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(PHG_GGET_SLEEP);
         }
         return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
     };
