@@ -254,6 +254,25 @@ def test_uc_fullsize_stream_vs_oracle(S, layout):
     np.testing.assert_allclose(ph.engine.get(_lib.F_BOUND), o.outer, rtol=1e-5)
 
 
+def test_uc_fullsize_at_north_star_accuracy():
+    """The north star asks for bounds within 1e-6 relative: the full-size UC LP (2 scenarios,
+    bordered kernel) at pdhg_eps 1e-7 -- every Iter0 solve terminates inside the 2e5-iteration cap,
+    and its objective and its dual bound are within 1e-6 of HiGHS' optimum.  (Measured: 1.4e-7 and
+    6e-8; HiGHS' own feasibility tolerances are 1e-7, so the oracle is not exact below that.)"""
+    so = {"pdhg_eps": 1e-7}
+    S = 2
+    ph = PH(_opts(iter0_solver_options=so, iterk_solver_options=so), uc.scenario_names_creator(S),
+            uc.scenario_creator, scenario_creator_kwargs={"num_scens": S})
+    ph.PH_Prep()
+    assert ph.engine.layout == "border"
+    ph.Iter0()
+    o = oph.OraclePH(_opts(), om.uc_names(S), om.uc, {"num_scens": S})
+    o.Iter0()
+    assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all(), ph.engine.get_i32(_lib.I_ITERS)
+    np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6)
+    np.testing.assert_allclose(ph.engine.get(_lib.F_BOUND), o.outer, rtol=1e-6)
+
+
 def test_block_register_pieces_same_bits(monkeypatch):
     """sslp's pieces fit the registers (row pieces <= 8, columns in <= 2 rows), so the block layout
     runs the block kernel with the matrix held in registers for the whole solve; PHG_BLOCK_STREAM=1 forces
@@ -323,6 +342,35 @@ def test_uc_fullsize_lagrangian_lp_vs_oracle():
         assert bnd[k] <= ref + 1e-9 * abs(ref) and ref - bnd[k] <= 3e-5 * abs(ref), (k, bnd[k], ref)
         if st1[k] == 0:
             assert abs(dob[k] - ref) <= 4e-6 * abs(ref), (k, dob[k], ref)
+
+
+def test_uc_fullsize_lagrangian_lp_at_north_star_accuracy():
+    """The Lagrangian spoke's full-size UC subproblem (W on, prox off) at pdhg_eps 1e-7 on two
+    scenarios: objectives within 1e-6 of HiGHS' LP with the same W, and the safe_bound = 2
+    weak-duality certificate at or below the LP optimum (to HiGHS' own 1e-7 tolerances) and within
+    3e-6 of it -- the north star's 1e-6 on the outer bound's ingredients."""
+    S = 2
+    so = {"pdhg_eps": 1e-7}
+    ph = PH(_opts(iter0_solver_options=so, iterk_solver_options=so), uc.scenario_names_creator(S),
+            uc.scenario_creator, scenario_creator_kwargs={"num_scens": S})
+    ph.PH_Prep()
+    assert ph.engine.layout == "border"
+    ph.Iter0()
+    ph.Compute_Xbar()
+    ph.Update_W()
+    W = ph.engine.get(_lib.F_W).reshape(S, ph.engine.N)
+    ph.engine.solve(1, 0, eps=1e-7, max_iter=200000, warm_start=3, safe_bound=2)
+    ph.engine.sync()
+    obj, bnd, st = ph.engine.get(_lib.F_OBJ), ph.engine.get(_lib.F_BOUND), ph.engine.get_i32(_lib.I_STATUS)
+    o = oph.OraclePH(_opts(), om.uc_names(S), om.uc, {"num_scens": S})
+    o.W = W.copy()
+    o.W_on, o.prox_on = 1, 0
+    o.solve_loop()
+    for k in range(S):
+        ref = o.obj[k]
+        assert st[k] == 0, (k, st[k])
+        assert abs(obj[k] - ref) <= 1e-6 * abs(ref), (k, obj[k], ref)
+        assert bnd[k] <= ref + 2e-7 * abs(ref) and ref - bnd[k] <= 3e-6 * abs(ref), (k, bnd[k], ref)
 
 
 def test_wave_kernel_matches_block_kernel():
