@@ -678,6 +678,9 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     // heavy ones then run to the end one per slot.  Resuming restores the state and recomputes A x /
     // A^T y with the same gathers and sums: the same iterates, bits and iteration counts as an
     // uninterrupted solve.  Queue codes: s (fresh), S + s (resumed), 2 S (no work left).
+    // (only workgroup 0's lane 0 waits here; the slot's other workgroups wait in the mailbox barrier,
+    // whose bound (~2^23 polls) is far above any first-pass wait: a scenario suspends or finishes
+    // within one solve of at most max_iter iterations)
     auto requeued = [&](int j) -> int {   // the j-th suspended scenario, or 2 S once every scenario is done
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (true) {

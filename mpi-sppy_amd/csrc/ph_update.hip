@@ -802,12 +802,16 @@ hipError_t conv_gate_launch(const double* convpart, int P, double* gate, double*
     return hipGetLastError();
 }
 
-hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
-    // nontemporal loads of x (read once here) when x is far larger than the caches: S N = 1e8 (1e6 x
-    // 100), node sums 159.6 vs 177.2 us (4.5 -> 5.2 TB/s); farmer 10k (x just written by the solve,
-    // cache-resident) keeps plain loads.  PHG_NODESUM_NT=0 / 1 forces either
+// nontemporal loads of x in the node sums (x is read once there) when x is far larger than the
+// caches: S N = 1e8 (1e6 x 100), node sums 159.6 vs 177.2 us (4.5 -> 5.2 TB/s); farmer 10k (x just
+// written by the solve, cache-resident) keeps plain loads.  PHG_NODESUM_NT=0 / 1 forces either
+static bool node_sums_nontemporal(const PhArgs& a) {
     static const int ntenv = [] { const char* e = std::getenv("PHG_NODESUM_NT"); return e ? std::atoi(e) : -1; }();
-    const bool ntl = ntenv >= 0 ? ntenv == 1 : (long)a.S * a.N >= 10000000L;
+    return ntenv >= 0 ? ntenv == 1 : (long)a.S * a.N >= 10000000L;
+}
+
+hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
+    const bool ntl = node_sums_nontemporal(a);
     const dim3 grid(a.n_seg, (a.maxk + 255) / 256);
     if (ntl) hipLaunchKernelGGL((node_sums_kernel<true, false>), grid, dim3(256), 0, st, a, nodesum, 0.0, 0);
     else hipLaunchKernelGGL((node_sums_kernel<false, false>), grid, dim3(256), 0, st, a, nodesum, 0.0, 0);
@@ -817,8 +821,7 @@ hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
 // node sums + the x-bar head of the folded pipelined iteration in one launch (node_sums_kernel
 // HEADX; one GPU: packed is the handle's own buffer, nothing is exchanged between the two)
 hipError_t node_sums_head_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st) {
-    static const int ntenv = [] { const char* e = std::getenv("PHG_NODESUM_NT"); return e ? std::atoi(e) : -1; }();
-    const bool ntl = ntenv >= 0 ? ntenv == 1 : (long)a.S * a.N >= 10000000L;
+    const bool ntl = node_sums_nontemporal(a);
     const dim3 grid(a.n_seg, (a.maxk + 255) / 256);
     if (ntl) hipLaunchKernelGGL((node_sums_kernel<true, true>), grid, dim3(256), 0, st, a, packed, thr, first);
     else hipLaunchKernelGGL((node_sums_kernel<false, true>), grid, dim3(256), 0, st, a, packed, thr, first);
