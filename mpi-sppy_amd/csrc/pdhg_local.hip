@@ -760,36 +760,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         // second iterate only (the average of the even iterates: still an ergodic PDHG average, and
         // a restart candidate like any other point) -- 7 of ~72 fp64 instructions per PDHG
         // iteration on farmer saved in the other step
-        // sum_stride 3 (window): the running sums only in the check_every iterations before a check
-        // that evaluates the average (every avg_every-th): the average becomes that of the last
-        // check_every iterates, a restart candidate like any other point; the other blocks skip the
-        // 7 running-sum adds per PDHG iteration (farmer)
-        const bool win = a.sum_stride == 3;
-        const bool win_block = win && ((it / chk) + 1) % (a.avg_every > 1 ? a.avg_every : 1) == 0;
-        if (win_block) {
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) xsum[k] = 0.0;
-#pragma unroll
-            for (int r = 0; r < RPL; ++r) ysum[r] = 0.0;
-#pragma unroll
-            for (int d = 0; d < D; ++d) ydsum[d] = 0.0;
-            cnt = 0;
-        }
-        if (win) {
-            if (win_block) {
-#pragma unroll 1
-                for (int kk = 0; kk < chk; kk += 2) {
-                    step(std::true_type{});
-                    step(std::true_type{});
-                }
-            } else {
-#pragma unroll 1
-                for (int kk = 0; kk < chk; kk += 2) {
-                    step(std::false_type{});
-                    step(std::false_type{});
-                }
-            }
-        } else if (a.sum_stride == 2) {
+        if (a.sum_stride == 2) {
 #pragma unroll 1
             for (int kk = 0; kk < chk; kk += 2) {
                 step(std::false_type{});
@@ -804,7 +775,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         }
         it += chk;
         since += chk;
-        cnt += a.sum_stride == 2 ? chk / 2 : (win && !win_block ? 0 : chk);
+        cnt += a.sum_stride == 2 ? chk / 2 : chk;
         if (a.prof) {
             pf_t1 = clock64();
             pf_it += pf_t1 - pf_t0;

@@ -214,7 +214,7 @@ struct phg_handle {
     SafeBoundArgs sb{};
     // relative-gap test on the whole objective (PdhgArgs::gap_const); PHG_GAP_RAW=1 turns it off
     int gap_const = 1;
-    // PdhgArgs::sum_stride (PHG_SUM_STRIDE=1/2/3).  2 by default since round 4: the average iterate's
+    // PdhgArgs::sum_stride (PHG_SUM_STRIDE=1/2).  2 by default since round 4: the average iterate's
     // running sums take every second iterate -- farmer 10k: 0.268 vs 0.285 ms per PDHG launch (7 of
     // ~62 instructions per PDHG iteration saved in every other iteration), the same 286 PDHG
     // iterations per solve, time to conv 0.845 vs 0.852 s; round 3 measured it within noise
@@ -352,7 +352,7 @@ int phg_create(int device, phg_handle** out) {
     if (const char* ev = std::getenv("PHG_GAP_RAW")) h->gap_const = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_SUM_STRIDE")) {
         const int v = std::atoi(ev);
-        h->sum_stride = (v == 2 || v == 3) ? v : 1;   // 3: the windowed running sums (pdhg_local.hip)
+        h->sum_stride = v == 2 ? 2 : 1;   // (round 3's windowed sums, 3, are gone: opt-in, never kept)
     }
     if (const char* ev = std::getenv("PHG_FOLD")) h->fold = std::atoi(ev) != 0 ? 1 : 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
