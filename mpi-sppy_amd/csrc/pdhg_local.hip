@@ -49,12 +49,9 @@ constexpr size_t local_lds_bytes() {
     return (size_t)(CI::NL * 64 + (64 / LPS) * CI::NG) * sizeof(double);
 }
 
-// PERSIST: a persistent grid (as many waves as are resident) in which every lane group takes its
-// next scenario from a device work queue (a.queue, in launch order: heaviest first) as soon as its
-// current one has terminated -- so the two scenarios sharing a wave no longer run until the slower
-// of them finishes, and there is no tail of late-starting waves.  A group reloads at a check
-// boundary (the other group of its wave waits for that prologue: a few global loads).  !PERSIST:
-// one work item per group, grid = items / G (the round-1 kernel).
+// One work item per group, grid = items / G.  (Round 3's persistent work-queue grid was measured
+// slower and hung once; it is gone.)  PROF: the PHG_LOCAL_PROF diagnostic's clock reads and
+// per-wave stores, a separate instantiation so the default kernel carries none of them.
 //
 // MB / MC: the block slots (bit r*CPL + k) and coupling slots (bit d*CPL + k) that hold an entry in
 // at least one lane (computed on the host from the layout; all ones = the generic kernel).  A slot
@@ -80,7 +77,7 @@ __device__ __forceinline__ double x_minus_xbar(double xs, double dc, double xbar
     return x - xbar;
 }
 
-template <int LPS, int CPL, int RPL, int D, bool PERSIST, unsigned MB, unsigned MC, unsigned long long BI,
+template <int LPS, int CPL, int RPL, int D, bool PROF, unsigned MB, unsigned MC, unsigned long long BI,
           unsigned long long BF, unsigned QM>
 __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
@@ -659,18 +656,10 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         }
     };
 
-    // next work item of this group (group-uniform): the queue in PERSIST mode, else the group's
-    // one item of this workgroup (and nothing after it)
+    // next work item of this group (group-uniform): the group's one item of this workgroup (and
+    // nothing after it)
     int taken = 0;
-    auto fetch = [&]() -> int {
-        if constexpr (PERSIST) {
-            int w = 0;
-            if (gl == 0) w = (int)__hip_atomic_fetch_add(a.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return __shfl(w, grp * LPS, 64);
-        } else {
-            return taken++ ? a.S : (int)blockIdx.x * G + grp;
-        }
-    };
+    auto fetch = [&]() -> int { return taken++ ? a.S : (int)blockIdx.x * G + grp; };
 
     bool valid = true, live = false;   // valid: the group may still receive work
     const int chk = a.check_every;
@@ -678,10 +667,10 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     // restart block), in loads; checks (uniform per wave)
     unsigned long long pf_it = 0, pf_chk = 0, pf_load = 0, pf_n = 0, pf_t1 = 0, pf_kkt = 0, pf_rst = 0;
     // and the wave's start / end on the 100 MHz constant clock (s_memrealtime): the occupancy timeline
-    const unsigned long long pf_w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long pf_w0 = PROF ? __builtin_amdgcn_s_memrealtime() : 0ull;
     for (;;) {
         unsigned long long pf_t0 = 0;
-        if (a.prof) {
+        if constexpr (PROF) {
             pf_t0 = clock64();
             if (pf_t1) pf_chk += pf_t0 - pf_t1;
         }
@@ -698,7 +687,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                 }
             }
         }
-        if (a.prof) {
+        if constexpr (PROF) {
             const unsigned long long now = clock64();
             pf_load += now - pf_t0;
             pf_t0 = now;
@@ -776,7 +765,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         it += chk;
         since += chk;
         cnt += a.sum_stride == 2 ? chk / 2 : chk;
-        if (a.prof) {
+        if constexpr (PROF) {
             pf_t1 = clock64();
             pf_it += pf_t1 - pf_t0;
             ++pf_n;
@@ -791,7 +780,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         const bool avg = wave_any(live && (a.avg_every <= 1 || ((it / chk) % a.avg_every) == 0));
         if constexpr (FOLDT) mv_aty(y, yd, aty);   // not formed in the iterations
         kkt_both(avg, inv, oc, oa);
-        if (a.prof) pf_kkt += clock64() - pf_t1;
+        if constexpr (PROF) pf_kkt += clock64() - pf_t1;
         if (!avg)
 #pragma unroll
             for (int u = 0; u < 6; ++u) oa[u] = u == 4 ? INFINITY : (u == 5 ? -INFINITY : INFINITY);
@@ -816,7 +805,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                                       (cand <= a.beta_nec * a.beta_nec * krst && cand > GS(CI::SC + CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
         if (live) GS(CI::SC + CI::KPREV) = cand;
-        const unsigned long long pf_r0 = a.prof ? clock64() : 0ull;
+        const unsigned long long pf_r0 = PROF ? clock64() : 0ull;
         if (wave_any(restart)) {
             const bool ra = restart && use_avg;
             if (wave_any(ra)) {
@@ -861,24 +850,13 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
                 since = 0;
             }
         }
-        if (a.prof) pf_rst += clock64() - pf_r0;
+        if constexpr (PROF) pf_rst += clock64() - pf_r0;
     }
-    if (a.prof && lane < 8) {   // (lane-indexed: a vector store)
+    if (PROF && lane < 8) {   // (lane-indexed: a vector store)
         const unsigned long long pf_w1 = __builtin_amdgcn_s_memrealtime();
         const unsigned long long v = lane == 0 ? pf_it : lane == 1 ? pf_chk : lane == 2 ? pf_load : lane == 3 ? pf_kkt
                                    : lane == 4 ? pf_rst : lane == 5 ? pf_n : lane == 6 ? pf_w0 : pf_w1;
         a.prof[(size_t)blockIdx.x * 8 + lane] = v;
-    }
-    if constexpr (PERSIST) {
-        // the last wave out re-arms the queue for the next (stream-ordered) launch: every wave
-        // has stopped fetching by then (a fetch past the end only happens once the queue is dry)
-        if (lane == 0) {
-            const unsigned prev = __hip_atomic_fetch_add(a.queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (prev == gridDim.x - 1) {
-                __hip_atomic_store(a.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(a.queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
     }
 }
 
@@ -941,7 +919,7 @@ struct LocalVariant {
     unsigned QM;               // column slots that can hold a quadratic term (all ones: generic)
     size_t lds;                // dynamic LDS per wave (Cold layout)
     void (*fn)(PdhgArgs);
-    void (*fn_persist)(PdhgArgs);
+    void (*fn_prof)(PdhgArgs);   // PROF: PdhgArgs::prof set (PHG_LOCAL_PROF)
 };
 
 #define PHG_LM(a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_)                                         \
@@ -1024,28 +1002,12 @@ void pdhg_local_variant_shape(int v, int* out4) {
 
 size_t pdhg_local_lds_bytes(int v) { return kLocalVariants[v].lds; }
 
-// PERSIST (a.queue set): a grid of as many waves as fit on the device at once (occupancy x CUs,
-// queried once per variant); more would only find the queue dry, fewer would leave SIMDs idle
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream) {
     const LocalVariant& V = kLocalVariants[v];
     const int G = 64 / V.LPS;
     const size_t lds = pdhg_local_lds_bytes(v);
-    int grid = (a.S + G - 1) / G;
-    if (a.queue) {
-        static int resident[32] = {0};
-        if (!resident[v]) {
-            int dev = 0, cus = 0, per = 0;
-            hipError_t e = hipGetDevice(&dev);
-            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, V.fn_persist, 64, lds);
-            if (e != hipSuccess) return e;
-            resident[v] = std::max(1, per) * std::max(1, cus);
-        }
-        grid = std::min(grid, resident[v]);
-        hipLaunchKernelGGL(V.fn_persist, dim3(grid), dim3(64), lds, stream, a);
-    } else {
-        hipLaunchKernelGGL(V.fn, dim3(grid), dim3(64), lds, stream, a);
-    }
+    const int grid = (a.S + G - 1) / G;
+    hipLaunchKernelGGL(a.prof ? V.fn_prof : V.fn, dim3(grid), dim3(64), lds, stream, a);
     return hipGetLastError();
 }
 
