@@ -745,26 +745,19 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
             }
             if constexpr (!FOLDT) mv_aty(y, yd, aty);
         };
-        // sum_stride 2 (PdhgArgs::sum_stride): the running sums of the average iterate take every
-        // second iterate only (the average of the even iterates: still an ergodic PDHG average, and
-        // a restart candidate like any other point) -- 7 of ~72 fp64 instructions per PDHG
-        // iteration on farmer saved in the other step
-        if (a.sum_stride == 2) {
+        // the running sums of the average iterate take every second iterate only (the average of
+        // the even iterates: still an ergodic PDHG average, and a restart candidate like any other
+        // point) -- 7 of ~62 fp64 instructions per PDHG iteration on farmer saved in the other step.
+        // The only loop compiled: with the every-iterate and windowed loops beside it the scheduler
+        // did worse (end of round 4: 0.2623 vs 0.2666 ms per launch, the same iterations bit for bit)
 #pragma unroll 1
-            for (int kk = 0; kk < chk; kk += 2) {
-                step(std::false_type{});
-                step(std::true_type{});
-            }
-        } else {
-#pragma unroll 1
-            for (int kk = 0; kk < chk; kk += 2) {
-                step(std::true_type{});
-                step(std::true_type{});
-            }
+        for (int kk = 0; kk < chk; kk += 2) {
+            step(std::false_type{});
+            step(std::true_type{});
         }
         it += chk;
         since += chk;
-        cnt += a.sum_stride == 2 ? chk / 2 : chk;
+        cnt += chk / 2;
         if constexpr (PROF) {
             pf_t1 = clock64();
             pf_it += pf_t1 - pf_t0;

@@ -214,7 +214,8 @@ struct phg_handle {
     SafeBoundArgs sb{};
     // relative-gap test on the whole objective (PdhgArgs::gap_const); PHG_GAP_RAW=1 turns it off
     int gap_const = 1;
-    // PdhgArgs::sum_stride (PHG_SUM_STRIDE=1/2).  2 by default since round 4: the average iterate's
+    // PdhgArgs::sum_stride: 2, the only form the lane-local kernel compiles (end of round 4; the
+    // every-iterate and windowed loops and PHG_SUM_STRIDE are gone).  Since round 4 the average iterate's
     // running sums take every second iterate -- farmer 10k: 0.268 vs 0.285 ms per PDHG launch (7 of
     // ~62 instructions per PDHG iteration saved in every other iteration), the same 286 PDHG
     // iterations per solve, time to conv 0.845 vs 0.852 s; round 3 measured it within noise
@@ -350,10 +351,6 @@ int phg_create(int device, phg_handle** out) {
     if (const char* ev = std::getenv("PHG_AVG_EVERY")) h->avg_every = std::max(1, std::atoi(ev));
     if (const char* ev = std::getenv("PHG_FUSE")) h->no_fuse = std::atoi(ev) == 0;
     if (const char* ev = std::getenv("PHG_GAP_RAW")) h->gap_const = std::atoi(ev) == 0;
-    if (const char* ev = std::getenv("PHG_SUM_STRIDE")) {
-        const int v = std::atoi(ev);
-        h->sum_stride = v == 2 ? 2 : 1;   // (round 3's windowed sums, 3, are gone: opt-in, never kept)
-    }
     if (const char* ev = std::getenv("PHG_FOLD")) h->fold = std::atoi(ev) != 0 ? 1 : 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;

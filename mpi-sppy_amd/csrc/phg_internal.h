@@ -257,9 +257,8 @@ struct PdhgArgs {
     // term inflates to ~rho/2 ||xbar||^2 (hydro: 1e4 against objectives of order 1); 0: the
     // constant-free form (PHG_GAP_RAW=1, A/B runs)
     int gap_const;
-    // lane-local kernel: 1 = the average iterate's running sums take every PDHG iterate, 2 = every
-    // second one, 3 = only the check_every iterates before each check that evaluates the average
-    // (PHG_SUM_STRIDE)
+    // lane-local kernel: the average iterate's running sums take every sum_stride-th PDHG iterate
+    // (2, the only form compiled since the end of round 4; informational)
     int sum_stride;
     // folded PH update (phg_ph_head with the fold on, include/phg.h): the prologue first applies
     // Update_W of the x it warm-starts from -- W += rho (x - xbar), x = xs_in dc, the bits the last
