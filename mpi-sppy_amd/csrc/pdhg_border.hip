@@ -340,7 +340,9 @@ __global__ __launch_bounds__(NT) void pdhg_border_kernel(PdhgArgs a) {
 
         const double inv = 1.0 / (double)cnt;
         const double l_axs = exchange(ax_link(XS));   // A x of the linking rows at the average
-        if (t < NL) yl[t] = l_ys;
+        // the average's linking-row y sums beside the current y (kkt_part reads ylx for the
+        // average's A^T y; yl keeps the current y that the next iteration's A^T y reads)
+        if (t < NL) ylx[t] = l_ys;
         __syncthreads();
         double oc[6], oa[6];
         kkt_part(false, 0.0, 0.0, oc);
@@ -514,6 +516,10 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
         const int r = B.crl[G.cz0 + q];
         lri[q] = r >= 0 ? r : B.R_max - r - 1;
     }
+    // padding entries point at position 0 (value 0): zero every x / y slot once, so a slot this group
+    // never owns (Yl[0] of a group without local rows) is a finite 0 and fma(0, v, acc) = acc holds
+    // (each thread zeroes the positions t + e NT it owns later, so no barrier is needed before those)
+    for (int q = t; q < B.C_max + B.R_max; q += NT) Xl[q] = 0.0;
     // owned elements of this thread (fixed for the launch)
     int jc[E], ir[E];
     bool cv_[E], rv_[E];
@@ -681,18 +687,25 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
     // (only workgroup 0's lane 0 waits here; the slot's other workgroups wait in the mailbox barrier,
     // whose bound (~2^23 polls) is far above any first-pass wait: a scenario suspends or finishes
     // within one solve of at most max_iter iterations)
+    // (L.err is cleared with the queue words at every launch: pdhg_border_launch.)  A suspended
+    // scenario carries status 2 until a slot resumes and finishes it, so one this slot gives up on
+    // reports a failed solve.
     auto requeued = [&](int j) -> int {   // the j-th suspended scenario, or 2 S once every scenario is done
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        auto queued = [&]() -> int {
+            return j < a.S ? __hip_atomic_load(B.requeue + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        };
         while (true) {
-            if (j < a.S) {
-                const int v = __hip_atomic_load(B.requeue + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int v = queued();
+            if (v != 0) return a.S + v - 1;
+            const bool over =
+                __hip_atomic_load(L.ctrl + kCtrlDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)a.S ||
+                __hip_atomic_load(L.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            const bool late = __builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull;   // 30 s (100 MHz)
+            if (over || late) {
+                v = queued();   // published between the two reads: resume it
                 if (v != 0) return a.S + v - 1;
-            }
-            if (__hip_atomic_load(L.ctrl + kCtrlDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)a.S ||
-                __hip_atomic_load(L.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-                return 2 * a.S;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {   // 30 s (100 MHz): give up
-                __hip_atomic_store(L.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (late) __hip_atomic_store(L.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return 2 * a.S;
             }
             __builtin_amdgcn_s_sleep(8);
@@ -1111,6 +1124,11 @@ __global__ __launch_bounds__(NT) void pdhg_border_reg_kernel(PdhgArgs a) {
             SV[3] = (double)it;
             SV[4] = (double)since;
             SV[5] = (double)cnt;
+            // provisional outputs of a suspended solve: a failed solve (status 2, NaN KKT) unless the
+            // slot that resumes it overwrites them -- a scenario no slot resumes (its waiting slot gave
+            // up: requeued()) is then reported as failed, never with the previous launch's values
+            a.status[s] = 2;
+            a.kkt[s] = NAN;
             if constexpr (PROF) pf_scen[3] += 1;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1220,6 +1238,9 @@ int pdhg_border_max_per_thread() { return 2 * kBorderRegNT; }   // elements per 
 hipError_t pdhg_border_launch(const PdhgArgs& a, hipStream_t stream) {
     const StreamLayout& L = a.st;
     hipError_t e = hipMemsetAsync(L.ctrl, 0, (size_t)(kCtrlBar + 3 * L.slots) * sizeof(unsigned), stream);
+    if (e != hipSuccess) return e;
+    // the give-up flag too: a timeout in an earlier launch must not end this one's waits at once
+    e = hipMemsetAsync(L.err, 0, sizeof(int), stream);
     if (e != hipSuccess) return e;
     if (a.bd.reg && a.bd.slice > 0) {   // split solves: the re-queue starts empty
         e = hipMemsetAsync(a.bd.requeue, 0, (size_t)a.S * sizeof(int), stream);

@@ -408,6 +408,8 @@ hipError_t pdhg_stream_launch(const PdhgArgs& a, hipStream_t stream) {
     // queue head, barrier counters and mailboxes start from zero every launch
     hipError_t e = hipMemsetAsync(L.ctrl, 0, (size_t)(kCtrlBar + 3 * L.slots) * sizeof(unsigned), stream);
     if (e != hipSuccess) return e;
+    e = hipMemsetAsync(L.err, 0, sizeof(int), stream);   // the give-up flag too (per launch)
+    if (e != hipSuccess) return e;
     const dim3 grid((unsigned)L.slots * (unsigned)L.K), block(kStreamNT);
     const size_t lds = pdhg_stream_lds_bytes(L);
     const void* fn = L.res ? (const void*)pdhg_stream_kernel<kStreamNT, true> : (const void*)pdhg_stream_kernel<kStreamNT, false>;

@@ -2565,17 +2565,17 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.gap_const = h->gap_const;
     a.sum_stride = h->sum_stride;
     if (h->fold_w_pending) {
-        if (!fold_active(h) || h->xn_external) {   // the prologue's x = xs dc would not be the caller's xN
+        // the prologue's x = xs dc would not be the caller's xN (xn_external); or the caller did not
+        // gate this solve on conv although the head that left the update pending had a convthresh
+        // (a final / extension solve after PH converged).  Then the pending W update runs
+        // on its own, gated like that head (flush_fold: nothing moves when it found conv below its
+        // convthresh -- the reference's break before Update_W, phbase.py:1008-1010), and this solve
+        // runs ungated on whatever W that leaves: its outputs are always fresh
+        const bool ungated = !a.gate && h->fold_thr > -INFINITY;
+        if (!fold_active(h) || h->xn_external || ungated) {
             if (flush_fold(h)) return -1;
         } else {
-            a.fold_w = 1;
-            // the head's gate holds for the prologue's W update too: a solve the caller did not gate
-            // is skipped when that head found conv below its convthresh (nothing moves: the
-            // reference breaks before Update_W and solve_loop, phbase.py:1008-1010)
-            if (!a.gate && h->fold_thr > -INFINITY) {
-                a.gate = h->gate;
-                a.gate_below = h->fold_thr;
-            }
+            a.fold_w = 1;   // (gated by the caller, or the head had no convthresh)
             a.W_rw = h->W;
             a.conv_s = h->conv_s;
             a.fold_st = h->fold_st;

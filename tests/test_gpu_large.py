@@ -180,8 +180,12 @@ def test_border_split_solves_match_uninterrupted(monkeypatch, capfd):
         np.testing.assert_array_equal(a, b)
 
 
-def test_border_matches_block_kernel(monkeypatch):
-    """The bordered block-diagonal kernel (pdhg_border.hip: 16 workgroups per scenario, one block
+@pytest.mark.parametrize("reg", ["1", "0"])
+def test_border_matches_block_kernel(monkeypatch, reg):
+    """reg "0" (PHG_BORDER_REG=0): the memory-resident bordered variant the planner falls back to
+    when the register variant's LDS or per-thread budget is exceeded (its average
+    iterate's linking-row A^T y read a running-sum array nothing wrote).
+    The bordered block-diagonal kernel (pdhg_border.hip: 16 workgroups per scenario, one block
     per unit, the 24-nonzero demand / reserve rows as linking rows) runs the same arithmetic as the
     workgroup-per-scenario block kernel in a different order: on a 24-unit x 12-period UC LP and
     one prox-QP at the oracle's W / x-bar, both reach the same iteration counts and objectives (to
@@ -191,6 +195,7 @@ def test_border_matches_block_kernel(monkeypatch):
     would otherwise put the block kernel on the shared-scaling delta form)."""
     monkeypatch.setenv("PHG_DELTA", "0")
     monkeypatch.setenv("PHG_BLOCK_SEG", "0")   # (row segments sum the pieces in another order)
+    monkeypatch.setenv("PHG_BORDER_REG", reg)
     kw = {"num_gens": 24, "num_periods": 12, "num_scens": 3}
     o = oph.OraclePH(_opts(), om.uc_names(3), om.uc, kw)
     o.Iter0()
@@ -210,6 +215,7 @@ def test_border_matches_block_kernel(monkeypatch):
         res[layout] = (ob0, ph.engine.get(_lib.F_OBJ).copy(), ph.engine.get_i32(_lib.I_ITERS).copy(), ph.nonants())
         if layout == "border":
             assert ph.engine.workgroups_per_scenario > 1
+            assert bool(ph.engine.border_reg) == (reg == "1")
     (a0, a1, ai, ax), (b0, b1, bi, bx) = res["block"], res["border"]
     np.testing.assert_array_equal(ai, bi)
     np.testing.assert_allclose(b0, a0, rtol=1e-11)

@@ -36,3 +36,31 @@ def test_pipelined_exits_match_sequential(trip_at):
     np.testing.assert_array_equal(a.Ws(), b.Ws())
     np.testing.assert_array_equal(a.nonants(), b.nonants())
     np.testing.assert_array_equal(a.xbars(), b.xbars())
+
+
+def test_ungated_solve_after_converged_head_is_fresh():
+    """a head that found conv below its convthresh leaves the folded W update pending; a
+    later solve the caller does NOT gate (a final or extension solve after PH converged) must run --
+    W untouched (the reference breaks before Update_W, phbase.py:1008-1010) and every output fresh --
+    instead of inheriting the head's gate and silently keeping the previous launch's values."""
+    from mpisppy_amd import _lib
+    opts = {"solver_name": "phg", "PHIterLimit": 4, "defaultPHrho": 1.0, "convthresh": 1e-10,
+            "verbose": False, "display_progress": False}
+    ph = PH(opts, farmer.scenario_names_creator(30), farmer.scenario_creator,
+            scenario_creator_kwargs={"crops_multiplier": 10, "num_scens": 30})
+    ph.PH_Prep()
+    ph.Iter0()
+    ph.current_solver_options = ph.iterk_solver_options
+    for k in range(3):
+        ph.update_and_solve(first=k == 0)
+    eng = ph.engine
+    if not eng.set_fold(True):
+        pytest.skip("this batch's layout does not take the folded update")
+    W0 = eng.get(_lib.F_W)           # (nothing pending: the last gated solve applied its update)
+    eng.ph_step(1e30, False)        # conv < 1e30: the head keeps x-bar and leaves W alone
+    assert eng.conv_wait() < 1e30
+    eng.solve(1, 1, eps=1e-9, max_iter=32, check_every=32, warm_start=1, skip_below=0.0)
+    it = eng.get_i32(_lib.I_ITERS)
+    np.testing.assert_array_equal(eng.get(_lib.F_W), W0)     # the flushed update was gated: W unchanged
+    # this launch's counts (<= its cap of 32), not the last PH solve's (hundreds at eps 1e-9)
+    assert ((it > 0) & (it <= 32)).all(), it
