@@ -230,6 +230,11 @@ int  phg_mfma_info(phg_handle* h, int32_t* out4);
  * A x + A^T y, shared entries in one A x + A^T y} (workgroup layout; the other layouts
  * report {varying, 0, 0, 0})                                                                        */
 int  phg_values_info(phg_handle* h, int32_t* out4);
+/* lane-local layout: out4 = {variant, lanes per scenario, 1 if the next launch takes the lone-wave
+ * build (every wave alone on its SIMD: a grid of at most 4 x CUs waves, PHG_LOCAL_LONE), executed
+ * fp64 operations per PDHG iteration per lane of the variant's hot loop x 100 (pdhg_local.hip
+ * local_loop_ops; FMA counted as 2)}                                                                  */
+int  phg_local_info(phg_handle* h, int32_t* out4);
 int  phg_info(phg_handle* h, int32_t* out8);   /* S, n, m, nnz, N, N_tot, kernel variant
                                                   (>= 100: lane-local, >= 200: workgroup,
                                                   >= 300: shared-matrix MFMA, 400 + K:

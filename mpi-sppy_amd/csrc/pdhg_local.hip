@@ -15,6 +15,7 @@
 // So one PDHG iteration is ~100 fp64 VALU instructions and one short DPP chain per wave, with no
 // memory traffic at all between the prologue (load the scenario) and the epilogue (store x, y).
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "phg_internal.h"
@@ -63,11 +64,14 @@ constexpr size_t local_lds_bytes() {
 // coefficients re-derived after every check instead of held across it, 168 registers with a few
 // prologue spills -- but measured on MI355X that is 0.345-0.350 ms per farmer-10k launch against
 // 0.342 ms at two waves (the kernel is VALU-issue-bound, not latency-bound), so two it is.
+// WV = 1 (the "lone-wave" instantiation, small shards): when the grid has no more waves than the chip
+// has SIMDs, every wave runs alone on its SIMD whatever the register budget, so that build may take
+// the whole register file (__launch_bounds__(64, 1)): the check keeps its per-element loads
+// unserialised (no seq(): nothing else competes for the registers) and the scheduler interleaves
+// its elements.  The arithmetic is the same operation for operation (the same bits).
 #ifndef PHG_LOCAL_WAVES
 #define PHG_LOCAL_WAVES 2
 #endif
-template <int LPS, int CPL, int RPL, int D>
-constexpr int local_waves() { return PHG_LOCAL_WAVES; }
 
 // (xs dc) - xbar, each operation rounded on its own (the folded W update must see the bits of the
 // epilogue's xN = xs dc)
@@ -78,8 +82,8 @@ __device__ __forceinline__ double x_minus_xbar(double xs, double dc, double xbar
 }
 
 template <int LPS, int CPL, int RPL, int D, bool PROF, unsigned MB, unsigned MC, unsigned long long BI,
-          unsigned long long BF, unsigned QM>
-__global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_local_kernel(PdhgArgs a) {
+          unsigned long long BF, unsigned QM, int WV>
+__global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
     constexpr int G = 64 / LPS;                    // scenarios per wave
     constexpr int DD = D > 0 ? D : 1;
@@ -258,6 +262,10 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     // [2] ||pr||^2 unscaled, [3] ||dres||^2 unscaled, [4] primal objective, [5] dual objective.  The iterate is given element-wise (xf, atf: column k; yf, axf: local row r;
     // axdp: coupling row d's LOCAL partial of A x) so the average iterate is never materialised in
     // registers.  Padded column / row slots hold zeros everywhere, so no per-element branches.
+    // element-by-element order in the check (see kkt_part); dropped in the lone-wave build
+    auto sq = []() {
+        if constexpr (WV > 1) seq();
+    };
     constexpr int KT = 5 + DD;   // reduced values per iterate
     // slot of coupling row d's A x partial: 1 (free in the reduced vector), then 6, 7, ...
     auto cslot = [](int d) { return d == 0 ? 1 : 5 + d; };
@@ -269,7 +277,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         // products at once, which would hold them all in registers beside the hot state)
 #pragma unroll
         for (int r = 0; r < RPL; ++r) {
-            seq();
+            sq();
             const double axx = axf(r), yy = yf(r);
             const double bl = CS(CI::BLO + r), bu = CS(CI::BHI + r);
             // (one-sided rows: axx is the offset form A x - b)
@@ -282,7 +290,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
         }
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-            seq();
+            sq();
             const double xx = xf(k);
             const double qk = qon(k) ? CS(CI::Q + k) : 0.0;
             const double ck = FOLD ? CS(CI::C + k) : c[k];
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(64, (local_waves<LPS, CPL, RPL, D>())) void pdhg_lo
     auto kkt_coupling = [&](double* t, auto ydf, double scale) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            seq();
+            sq();
             const double axx = t[cslot(d)] * scale, yy = ydf(d);
             const double bl = GS(CI::DLO + d), bu = GS(CI::DHI + d);
             const double pr = axx - clampd(axx, bl, bu);
@@ -903,6 +911,57 @@ int pdhg_local_image_items(int v);
 
 hipError_t pdhg_local_image_launch(int v, const PdhgArgs& a, double* img, double* cimg, hipStream_t stream);
 
+// ----------------------------------------------------------------------------- executed work
+// fp64 operations ONE lane issues per PDHG iteration in the hot loop of a variant (x 100; an FMA
+// counts 2, an add / mul / max / min 1), restating the step's compile-time structure above:
+//   primal step per column slot: FOLDT fma(x, ip, -ctip) + one FMA per occupied block / coupling
+//     entry; FOLD two FMAs; else sub, FMA, mul -- then the clamps whose side is not infinite (BI);
+//   A x: per row slot its occupied entries (one-sided rows: all FMAs onto the offset; else a mul
+//     and FMAs), per coupling row a mul, FMAs and the log2(LPS) adds of the group sum;
+//   dual step: one-sided rows 2 FMAs + 1 clamp, else 2 FMAs + the finite-side clamps + 1 sub;
+//   A^T y (not FOLDT) per column a mul and FMAs; running sums (every second iterate) 1/2 per element.
+// tools/loop_ops.py checks it against the compiled inner loop (the compiler turns the first DPP
+// step's add into an FMA that re-forms the coupling product: +1 per coupling row in the ISA).
+constexpr int local_loop_ops(int LPS, int CPL, int RPL, int D, unsigned MB, unsigned MC, unsigned long long BI,
+                             unsigned long long BF) {
+    const bool FOLD = RPL * CPL + D * CPL <= 12;
+    const bool FOLDT = FOLD && (__builtin_popcount(MB) + __builtin_popcount(MC) <= 8);
+    auto bon = [&](int r, int k) { return ((MB >> (r * CPL + k)) & 1u) != 0u; };
+    auto con = [&](int d, int k) { return ((MC >> (d * CPL + k)) & 1u) != 0u; };
+    auto inf = [&](int bit) { return ((BI >> bit) & 1ull) != 0ull; };
+    auto finb = [&](int bit) { return ((BF >> bit) & 1ull) != 0ull; };
+    int ops = 0;   // x 2: half-ops of the stride-2 running sums
+    for (int k = 0; k < CPL; ++k) {
+        int e = 0;
+        for (int r = 0; r < RPL; ++r) e += bon(r, k);
+        for (int d = 0; d < D; ++d) e += con(d, k);
+        if (FOLDT) ops += 2 * (2 + 2 * e);
+        else if (FOLD) ops += 2 * 4;
+        else ops += 2 * 4;
+        ops += 2 * ((inf(k) ? 0 : 1) + (inf(16 + k) ? 0 : 1));
+        if (!FOLDT) ops += 2 * (e > 0 ? 2 * e - 1 : 0);   // A^T y
+        ops += 1;                                         // x running sum
+    }
+    for (int r = 0; r < RPL; ++r) {
+        int e = 0;
+        for (int k = 0; k < CPL; ++k) e += bon(r, k);
+        const bool one = (finb(32 + r) && inf(40 + r)) || (finb(40 + r) && inf(32 + r));
+        ops += 2 * (one ? 2 * e : (e > 0 ? 2 * e - 1 : 0));
+        ops += 2 * (one ? 5 : 4 + (inf(32 + r) ? 0 : 1) + (inf(40 + r) ? 0 : 1) + 1);
+        ops += 1;
+    }
+    int lg = 0;
+    for (int l = LPS; l > 1; l >>= 1) ++lg;
+    for (int d = 0; d < D; ++d) {
+        int e = 0;
+        for (int k = 0; k < CPL; ++k) e += con(d, k);
+        ops += 2 * ((e > 0 ? 2 * e - 1 : 0) + lg);
+        ops += 2 * (4 + (inf(48 + d) ? 0 : 1) + (inf(52 + d) ? 0 : 1) + 1);
+        ops += 1;
+    }
+    return ops * 50;
+}
+
 // ----------------------------------------------------------------------------- dispatch
 struct LocalVariant {
     int LPS, CPL, RPL, D;
@@ -913,12 +972,22 @@ struct LocalVariant {
     size_t lds;                // dynamic LDS per wave (Cold layout)
     void (*fn)(PdhgArgs);
     void (*fn_prof)(PdhgArgs);   // PROF: PdhgArgs::prof set (PHG_LOCAL_PROF)
+    void (*fn1)(PdhgArgs);       // the lone-wave build (WV = 1), or null
+    void (*fn1_prof)(PdhgArgs);
 };
 
-#define PHG_LM(a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_)                                         \
-    {a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_, local_lds_bytes<a_, b_, c_, d_>(),                   \
-     pdhg_local_kernel<a_, b_, c_, d_, false, mb_, mc_, bi_, bf_, qm_>,                            \
-     pdhg_local_kernel<a_, b_, c_, d_, true, mb_, mc_, bi_, bf_, qm_>}
+#define PHG_LK(a_, b_, c_, d_, p_, mb_, mc_, bi_, bf_, qm_, w_) \
+    pdhg_local_kernel<a_, b_, c_, d_, p_, mb_, mc_, bi_, bf_, qm_, w_>
+#define PHG_LM(a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_)                                                  \
+    {a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_, local_lds_bytes<a_, b_, c_, d_>(),                            \
+     PHG_LK(a_, b_, c_, d_, false, mb_, mc_, bi_, bf_, qm_, PHG_LOCAL_WAVES),                               \
+     PHG_LK(a_, b_, c_, d_, true, mb_, mc_, bi_, bf_, qm_, PHG_LOCAL_WAVES), nullptr, nullptr}
+// ... with a lone-wave build beside it
+#define PHG_LM1(a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_)                                                 \
+    {a_, b_, c_, d_, mb_, mc_, bi_, bf_, qm_, local_lds_bytes<a_, b_, c_, d_>(),                            \
+     PHG_LK(a_, b_, c_, d_, false, mb_, mc_, bi_, bf_, qm_, PHG_LOCAL_WAVES),                               \
+     PHG_LK(a_, b_, c_, d_, true, mb_, mc_, bi_, bf_, qm_, PHG_LOCAL_WAVES),                                \
+     PHG_LK(a_, b_, c_, d_, false, mb_, mc_, bi_, bf_, qm_, 1), PHG_LK(a_, b_, c_, d_, true, mb_, mc_, bi_, bf_, qm_, 1)}
 #define PHG_L(a_, b_, c_, d_) PHG_LM(a_, b_, c_, d_, (1u << (c_ * b_)) - 1u, (1u << ((d_ > 0 ? d_ : 1) * b_)) - 1u, 0ull, 0ull, (1u << b_) - 1u)
 // farmer's infinite sides: columns 2, 3 (QuantitySuperQuotaSold, QuantityPurchased) above; row 0
 // (cattle feed, >=) above, row 1 (limit sold, <= 0) below; the total-acreage row (<=) below
@@ -950,14 +1019,16 @@ static const LocalVariant kLocalVariants[] = {
     PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull, 0xFu),
     PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, 0ull, 0xFu),
     // ... its finite ones, and the nonant (DevotedAcreage) in column slot 0 only
-    PHG_LM(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
-    PHG_LM(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
-    PHG_LM(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
+    PHG_LM1(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
+    PHG_LM1(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
+    PHG_LM1(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
 };
 #undef PHG_FARMER_BI
 #undef PHG_FARMER_BF
 #undef PHG_L
 #undef PHG_LM
+#undef PHG_LM1
+#undef PHG_LK
 constexpr int kLocalShapes = 9;   // the generic entries; the planner walks these
 
 int pdhg_local_num_variants() { return kLocalShapes; }
@@ -995,12 +1066,41 @@ void pdhg_local_variant_shape(int v, int* out4) {
 
 size_t pdhg_local_lds_bytes(int v) { return kLocalVariants[v].lds; }
 
+int pdhg_local_loop_ops(int v) {
+    const LocalVariant& V = kLocalVariants[v];
+    return local_loop_ops(V.LPS, V.CPL, V.RPL, V.D, V.MB, V.MC, V.BI, V.BF);
+}
+
+// SIMDs of the current device (4 per CU): a grid of at most this many one-wave workgroups runs every
+// wave alone on its SIMD
+static int device_simds() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return 4 * cus;
+}
+
+// the lone-wave build is taken when the variant has one and the grid fits the chip's SIMDs one wave
+// each (small shards: farmer 10 000 over 4 or 8 GPUs); PHG_LOCAL_LONE=0 / 1 forces it off / on
+bool pdhg_local_lone(int v, int S) {
+    const LocalVariant& V = kLocalVariants[v];
+    if (!V.fn1) return false;
+    static const int force = [] { const char* e = std::getenv("PHG_LOCAL_LONE"); return e ? std::atoi(e) : -1; }();
+    if (force >= 0) return force > 0;
+    static int simds = -1;
+    if (simds < 0) simds = device_simds();
+    const int G = 64 / V.LPS;
+    return (S + G - 1) / G <= simds;
+}
+
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream) {
     const LocalVariant& V = kLocalVariants[v];
     const int G = 64 / V.LPS;
     const size_t lds = pdhg_local_lds_bytes(v);
     const int grid = (a.S + G - 1) / G;
-    hipLaunchKernelGGL(a.prof ? V.fn_prof : V.fn, dim3(grid), dim3(64), lds, stream, a);
+    const bool lone = pdhg_local_lone(v, a.S);
+    void (*fn)(PdhgArgs) = lone ? (a.prof ? V.fn1_prof : V.fn1) : (a.prof ? V.fn_prof : V.fn);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64), lds, stream, a);
     return hipGetLastError();
 }
 

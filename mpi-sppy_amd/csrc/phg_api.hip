@@ -35,6 +35,8 @@ int pdhg_local_image_items(int v);
 hipError_t pdhg_local_image_launch(int v, const PdhgArgs& a, double* img, double* cimg, hipStream_t stream);
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
+bool pdhg_local_lone(int v, int S);
+int pdhg_local_loop_ops(int v);
 int pdhg_block_num_variants();
 void pdhg_block_variant_shape(int v, int* out12);
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad, int nd, int ecodes);
@@ -2414,6 +2416,17 @@ int phg_mfma_info(phg_handle* h, int32_t* o) {
     o[1] = h->mshape[1];
     o[2] = __builtin_popcountll(h->mf.nz_ax);
     o[3] = __builtin_popcountll(h->mf.nz_aty);
+    return 0;
+}
+
+int phg_local_info(phg_handle* h, int32_t* o) {
+    if (!h || !h->loaded || !o) return fail("phg_local_info: no batch loaded");
+    if (h->local_variant < 0) return fail("phg_local_info: the batch does not use the lane-local layout");
+    CK(hipSetDevice(h->device));
+    o[0] = h->local_variant;
+    o[1] = h->lshape[0];
+    o[2] = pdhg_local_lone(h->local_variant, h->S) ? 1 : 0;
+    o[3] = pdhg_local_loop_ops(h->local_variant);
     return 0;
 }
 

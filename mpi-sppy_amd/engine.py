@@ -209,6 +209,15 @@ class Engine:
         return {"varying": int(out[0]), "delta": bool(out[1]), "unit": int(out[1]) == 2,
                 "per_scenario_vals": int(out[2]), "shared_vals": int(out[3])}
 
+    def local_info(self):
+        """Lane-local layout (phg_local_info): the variant, lanes per scenario, whether the next
+        launch takes the lone-wave build (small shards), and the fp64 operations one lane issues per
+        PDHG iteration in the variant's hot loop (FMA = 2; pdhg_local.hip local_loop_ops)."""
+        out = np.zeros(4, np.int32)
+        _lib.check(self.lib.phg_local_info(self.h, ptr(out)))
+        return {"variant": int(out[0]), "lanes": int(out[1]), "lone": bool(out[2]),
+                "loop_ops_per_lane": int(out[3]) / 100.0}
+
     def mfma_fragments(self):
         """MFMA instructions per PDHG iteration per 16 scenarios (nonzero 16x4 fragments of A x and
         A^T y) of the shared-matrix layout (phg_mfma_info)."""
