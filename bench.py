@@ -381,6 +381,21 @@ def main():
                    "flops_sparse_per_pdhg_iter_per_scen": f_it,
                    "sparse_tflops": round(achieved_tf, 4)}
 
+    # the lane-local kernel's EXECUTED work beside the fixed formula: the fp64 operations its hot loop
+    # issues per PDHG iteration (phg_local_info, pdhg_local.hip local_loop_ops: FMA = 2; the stride-2
+    # running sums, the -sigma-scaled bounds, the folded primal step and the compile-time-dropped
+    # clamps as compiled; every lane of the scenario's group, padding lanes included; the restart /
+    # termination check every check_every iterations is not counted), and whether the launch took the
+    # lone-wave build (small shards)
+    exe_rf = {}
+    if eng.layout == "local":
+        li = eng.local_info()
+        exe = li["loop_ops_per_lane"] * li["lanes"]
+        exe_tf = exe * pdhg_iters / args.steps / avg_launch_s / 1e12
+        exe_rf = {"executed_flops_per_pdhg_iter_per_scen": exe, "executed_tflops": round(exe_tf, 4),
+                  "frac_executed": round(exe_tf / FP64_PEAK_TFLOPS, 5), "lone_wave_build": li["lone"],
+                  "executed_basis": "hot-loop fp64 ops actually issued (FMA = 2) x lanes per scenario; "
+                                    "the check's work excluded"}
     out = {
         "metric": "scenario-QP solves/sec (PH iteration: batched prox-QP solve of every scenario + fused xbar/W/conv)",
         "value": round(value, 2),
@@ -443,6 +458,7 @@ def main():
                                            f"pdhg_border_kernel ({eng.workgroups_per_scenario} workgroups per scenario, "
                                            "bordered block-diagonal, slices in LDS, linking rows exchanged)")}[eng.layout],
                      "flops_per_pdhg_iter_per_scen": f_it,
+                     **exe_rf,
                      "pdhg_iters_per_scen_per_step": round(pdhg_iters / args.steps / S_loc, 2),
                      "max_pdhg_iters": max_iters,
                      "avg_launch_ms": round(avg_launch_s * 1e3, 4)},

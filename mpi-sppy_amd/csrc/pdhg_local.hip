@@ -853,11 +853,16 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         }
         if constexpr (PROF) pf_rst += clock64() - pf_r0;
     }
-    if (PROF && lane < 8) {   // (lane-indexed: a vector store)
+    if (PROF && lane < 10) {   // (lane-indexed: a vector store)
         const unsigned long long pf_w1 = __builtin_amdgcn_s_memrealtime();
+        // where the wave ran: HW_ID (SIMD [5:4], CU [11:8], SH [12], SE [15:13]) and the XCD
+        unsigned hwid = 0, xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         const unsigned long long v = lane == 0 ? pf_it : lane == 1 ? pf_chk : lane == 2 ? pf_load : lane == 3 ? pf_kkt
-                                   : lane == 4 ? pf_rst : lane == 5 ? pf_n : lane == 6 ? pf_w0 : pf_w1;
-        a.prof[(size_t)blockIdx.x * 8 + lane] = v;
+                                   : lane == 4 ? pf_rst : lane == 5 ? pf_n : lane == 6 ? pf_w0 : lane == 7 ? pf_w1
+                                   : lane == 8 ? (unsigned long long)hwid : (unsigned long long)xcc;
+        a.prof[(size_t)blockIdx.x * 10 + lane] = v;
     }
 }
 

@@ -17,6 +17,7 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <map>
 
 #include "../../include/phg.h"
 #include "phg_internal.h"
@@ -2671,10 +2672,11 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         static unsigned long long* pbuf = nullptr;
         static size_t pcap = 0;
         const size_t waves = (size_t)a.S;   // >= the grid (G scenarios per wave)
-        if (lprof && pcap < waves * 8) {
+        constexpr size_t PW = 10;            // items per wave (pdhg_local.hip, PROF)
+        if (lprof && pcap < waves * PW) {
             if (pbuf) CK(hipFree(pbuf));
-            CK(hipMalloc((void**)&pbuf, waves * 8 * sizeof(unsigned long long)));
-            pcap = waves * 8;
+            CK(hipMalloc((void**)&pbuf, waves * PW * sizeof(unsigned long long)));
+            pcap = waves * PW;
         }
         if (lprof) CK(hipMemsetAsync(pbuf, 0, pcap * sizeof(unsigned long long), h->stream));
         a.prof = lprof ? pbuf : nullptr;
@@ -2685,15 +2687,21 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             CK(hipStreamSynchronize(h->stream));
             double t[6] = {0, 0, 0, 0, 0, 0};
             for (size_t i = 0; i < pcap; ++i)
-                if (i % 8 < 6) t[i % 8] += (double)hb[i];
+                if (i % PW < 6) t[i % PW] += (double)hb[i];
+            // placement: waves per SIMD (XCD, SE, SH, CU, SIMD from HW_ID) over the launch
+            std::map<unsigned long long, int> per_simd;
+            for (size_t w = 0; w * PW + 9 < pcap; ++w)
+                if (hb[w * PW + 7] > 0) per_simd[(hb[w * PW + 9] << 16) | (hb[w * PW + 8] & 0xFF30ull)]++;
+            int simd_max = 0, simd_multi = 0;
+            for (auto& kv : per_simd) { simd_max = std::max(simd_max, kv.second); simd_multi += kv.second > 1; }
             // occupancy timeline from the waves' start / end stamps (100 MHz): the launch span, the mean
             // number of resident waves over it, and the span's last part with fewer than half the
             // peak resident (the tail)
             std::vector<std::pair<unsigned long long, int>> ev;
-            for (size_t w = 0; w * 8 + 7 < pcap; ++w)
-                if (hb[w * 8 + 7] > hb[w * 8 + 6] && hb[w * 8 + 6] > 0) {
-                    ev.push_back({hb[w * 8 + 6], +1});
-                    ev.push_back({hb[w * 8 + 7], -1});
+            for (size_t w = 0; w * PW + 7 < pcap; ++w)
+                if (hb[w * PW + 7] > hb[w * PW + 6] && hb[w * PW + 6] > 0) {
+                    ev.push_back({hb[w * PW + 6], +1});
+                    ev.push_back({hb[w * PW + 7], -1});
                 }
             std::sort(ev.begin(), ev.end());
             double span = 0, area = 0, tail = 0;
@@ -2716,8 +2724,10 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             }
             fprintf(stderr,
                     "PHG_LOCAL_PROF iter_cycles %.6e check_cycles %.6e load_cycles %.6e kkt_cycles %.6e restart_cycles %.6e "
-                    "checks %.0f span_us %.2f mean_resident %.1f peak_resident %d tail_below_half_us %.2f\n",
-                    t[0], t[1], t[2], t[3], t[4], t[5], span / 100.0, span > 0 ? area / span : 0.0, peak, tail / 100.0);
+                    "checks %.0f span_us %.2f mean_resident %.1f peak_resident %d tail_below_half_us %.2f "
+                    "simds_used %zu simds_with_2plus_waves %d max_waves_per_simd %d\n",
+                    t[0], t[1], t[2], t[3], t[4], t[5], span / 100.0, span > 0 ? area / span : 0.0, peak, tail / 100.0,
+                    per_simd.size(), simd_multi, simd_max);
         }
     }
     else if (h->block_variant >= 0) CK(pdhg_block_launch(h->block_variant, a, h->stream));
