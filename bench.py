@@ -567,7 +567,12 @@ def main():
                 if out["cpu_baseline"].get("value"):
                     proj["at_sample_rate_s"] = round(it_c * S_c / out["cpu_baseline"]["value"], 1)
                 if cc.get("solves_per_s"):
-                    proj["at_conv_run_rate_s"] = round(it_c * S_c / cc["solves_per_s"], 1)
+                    # the conv run's rate per process, scaled to the job's whole CPU share (the sample's
+                    # process count): HiGHS's QP solves are much slower over a PH run's later iterations
+                    # than at the sample's state
+                    rate = cc["solves_per_s"] / cc["processes"] * out["cpu_baseline"].get("cores", cc["processes"])
+                    proj["conv_run_rate_scaled_solves_per_s"] = round(rate, 1)
+                    proj["at_conv_run_rate_s"] = round(it_c * S_c / rate, 1)
                 out["cpu_baseline"]["projected_time_to_conv_s"] = proj.get("at_conv_run_rate_s") or proj.get("at_sample_rate_s")
                 out["cpu_baseline"]["projection"] = proj
     if rank == 0:
