@@ -278,6 +278,11 @@ def main():
     # the sequential statements) for its own roofline
     W_saved = eng.get(_lib.F_W)
     fold = eng.set_fold(os.environ.get("PHG_FOLD", "1") != "0")
+    # the timed steps ran the PH update in the solve's tail (ph_tail.h) where it applies: measure the
+    # update kernels here with separate launches (their own roofline), the tail off
+    tail_on = (ph.options.get("pdhg_tail") if ph.options.get("pdhg_tail") is not None else
+               os.environ.get("PHG_TAIL", "0") == "1") and eng.layout == "local" and fold
+    ph.options["pdhg_tail"] = False
     eng.timing_reset(solves=False, updates=True)
     for _ in range(args.steps):
         step()
@@ -478,7 +483,11 @@ def main():
                                "node_sums_avg_ms": round(ns_ms / max(1, n_ns), 4) if n_ns else None,
                                "head_avg_ms": round(hd_ms / max(1, n_hd), 4) if n_hd else None,
                                "survey_bytes_per_update": ph_bytes, "rho_streams": rho_streams,
-                               "timed": "HIP events on the library stream over extra pipelined iterations",
+                               "timed": "HIP events on the library stream over extra pipelined iterations "
+                                        "with separate launches",
+                               "in_solve_tail": bool(tail_on),
+                               "note": ("the timed steps ran this update at the end of each solve's launch "
+                                        "(ph_tail.h): its time is inside avg_launch_ms" if tail_on else None),
                                "standalone": {"kernels": "node_sums_kernel + w_update_kernel",
                                               "avg_ms": round(sa_ms / max(1, n_sa), 4),
                                               "node_sums_avg_ms": round(sa_ns_ms / max(1, n_sa_ns), 4),

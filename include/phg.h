@@ -307,6 +307,22 @@ int  phg_set_fold(phg_handle* h, int32_t on, int32_t* active);
 int  phg_exchange_layout(phg_handle* h, int32_t* out3);
 int  phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t first);
 int  phg_solve_undo(phg_handle* h);
+/* Fuse the NEXT iteration's PH update into the end of the NEXT phg_solve (one-shot request; the
+ * pipelined loop sets it before every solve): mode 1 (one GPU) -- node sums of the solve's x, the
+ * convergence metric of the folded W update its prologue applied, the gate and the next x-bar (the
+ * current one if conv < convthresh), all of which the following phg_ph_step then takes over instead
+ * of launching; mode 2 (exchange) -- node sums and partials into dev_packed, taken over by the
+ * following phg_node_sums(h, dev_packed); 0: off.  Only the lane-local layout with the folded
+ * update, on a gated solve; otherwise the request is dropped and the separate launches run.
+ * Replaces nothing in mpi-sppy by itself: it is the launch schedule of phbase.py:976-1030 on one
+ * device.  PHG_TAIL=0 disables it.                                                                     */
+int  phg_set_tail(phg_handle* h, int32_t mode, double convthresh, double* dev_packed);
+/* New column bounds of the loaded batch ([S*n] each, the caller's units; +-inf allowed) without a
+ * reload: intersected again with the rows the presolve folded into bounds, scaled on the device,
+ * the lane-local kernel re-picked for the new bound sides and its lane image rebuilt; the safe-bound
+ * pass's implied bounds are recomputed at the next safe-bound solve.  What the reference's
+ * _fix_nonants / _restore_nonants (spopt.py:590-640) change on a persistent solver (update_var). */
+int  phg_set_col_bounds(phg_handle* h, const double* col_lo, const double* col_hi);
 /* One GPU (nothing to exchange): phg_node_sums + phg_ph_head on the handle's own buffer.  With
  * PHG_FUSE=1 and a batch that allows it (two-stage tree, one virtual rank, no smoothing, no variable
  * probability) as ONE launch (the node-sum pass, then the W update by the last workgroups, x

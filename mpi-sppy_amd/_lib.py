@@ -88,6 +88,8 @@ SIGNATURES = {
     "phg_mfma_info": (C.c_int, [C.c_void_p, i32p]),
     "phg_values_info": (C.c_int, [C.c_void_p, i32p]),
     "phg_local_info": (C.c_int, [C.c_void_p, i32p]),
+    "phg_set_tail": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p]),
+    "phg_set_col_bounds": (C.c_int, [C.c_void_p, f64p, f64p]),
     "phg_group_unique_id": (C.c_int, [C.c_void_p]),
     "phg_create_group": (C.c_int, [C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
     "phg_group_size": (C.c_int, [C.c_void_p, i32p]),

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "ph_tail.h"
 #include "phg_internal.h"
 #include "wave_ops.h"
 
@@ -85,10 +86,10 @@ template <int LPS, int CPL, int RPL, int D, bool PROF, unsigned MB, unsigned MC,
           unsigned long long BF, unsigned QM, int WV>
 __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (see PdhgArgs::gate)
+    extern __shared__ double cold[];
     constexpr int G = 64 / LPS;                    // scenarios per wave
     constexpr int DD = D > 0 ? D : 1;
     using CI = Cold<CPL, RPL, D>;
-    extern __shared__ double cold[];
     const int lane = threadIdx.x;
     const int gl = lane % LPS;                     // lane inside the scenario's group
     const int grp = lane / LPS;
@@ -553,9 +554,9 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
 #pragma unroll
             for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
             gsum_many<LPS, 5>(rr);
-            if (fold && gl == 0) {
-                ka->conv_s[s] = rr[4];
-                ka->fold_st[s] = ka->status_in[s];
+            if (fold && gl == 0) {   // (write-through: the tail waves read them in this launch)
+                st_sc1(&ka->conv_s[s], rr[4]);
+                st_sc1(&ka->fold_st[s], ka->status_in[s]);
             }
             rr[3] += b2d;
             GS(CI::SC + CI::CNORM) = sqrt(rr[0]);
@@ -632,7 +633,7 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
                 xs_[b] = xv;
                 const double xu = xv * dcv[k];
                 if (xo) xo[b] = xu;
-                if (kq[k] >= 0) xN_[sN + kq[k]] = xu;
+                if (kq[k] >= 0) st_sc1(&xN_[sN + kq[k]], xu);   // (write-through: read by the tail)
             }
         }
 #pragma unroll
@@ -864,6 +865,8 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
                                    : lane == 8 ? (unsigned long long)hwid : (unsigned long long)xcc;
         a.prof[(size_t)blockIdx.x * 10 + lane] = v;
     }
+    // the pipelined iteration's PH update: the last waves to finish run it (ph_tail.h)
+    if (a.tl.mode) ph_tail_end(a.tl, cold);
 }
 
 // ----------------------------------------------------------------------------- lane image
@@ -1105,7 +1108,7 @@ hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream) {
     const int grid = (a.S + G - 1) / G;
     const bool lone = pdhg_local_lone(v, a.S);
     void (*fn)(PdhgArgs) = lone ? (a.prof ? V.fn1_prof : V.fn1) : (a.prof ? V.fn_prof : V.fn);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(64), lds, stream, a);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64), lds, stream, a);   // (TailArgs::W = grid)
     return hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ int pdhg_local_image_items(int v);
 hipError_t pdhg_local_image_launch(int v, const PdhgArgs& a, double* img, double* cimg, hipStream_t stream);
 void pdhg_local_variant_masks(int v, unsigned* out2);
 hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
+hipError_t scale_cols_launch(double* cl, double* cu, const double* dc, long cnt, hipStream_t stream);
 bool pdhg_local_lone(int v, int S);
 int pdhg_local_loop_ops(int v);
 int pdhg_block_num_variants();
@@ -114,6 +115,17 @@ struct phg_handle {
     double sense = 1.0;
     int variant = -1;          // gather kernel variant (pdhg.hip), or
     int local_variant = -1;    // lane-local kernel variant (pdhg_local.hip); preferred when >= 0
+    int local_shape_v = -1;    // its shape's generic entry (pdhg_local_pick_masked re-picks from it)
+    std::vector<int> lp_col_of, lp_row_of, lp_cpl_row;   // host copy of the lane plan (bound masks)
+    // host copy of the presolved batch: the safe-bound pass's implied bounds are computed from it at
+    // the first safe-bound solve (not at every load) and again after phg_set_col_bounds
+    struct {
+        std::vector<int> rowptr, colidx, nonant_col;
+        std::vector<double> vals, rl, ru, cl, cu;
+    } hb;
+    std::vector<int> fold_col;            // presolve-folded rows as column bounds (Presolved)
+    std::vector<double> fold_lo, fold_hi;
+    bool sb_stale = true;
     int block_variant = -1;    // workgroup-per-scenario kernel variant (pdhg_block.hip)
     int wave_variant = -1;     // one-wave-per-scenario shared-matrix kernel variant (pdhg_wave.hip)
     int wshape[6] = {0};
@@ -204,9 +216,27 @@ struct phg_handle {
     int m_orig = 0;
     // device-side convergence metric (phg_conv_start / phg_conv_wait, predicated solves)
     double* gate = nullptr;          // device {conv, not optimal, NaN}
-    double* gate_host = nullptr;     // fine-grained pinned host copy + sequence word [3]
+    double* gate_host = nullptr;     // fine-grained pinned host ring [2][4]: slot seq mod 2 = {values, seq}
     long long gate_seq = 0;          // sequence number of the last enqueued gate computation
+    long long wait_seq = 0;          // the one phg_conv_wait waits for (a tail's gate: not yet)
+    long long last_wait_seq = 0;     // the last one waited for, and its conv value
+    double last_conv = 0.0;
     bool gate_fused = false;         // the last phg_apply_xbar already computed the gate
+    // PH update fused into the end of the next solve (ph_tail.h; phg_set_tail): the request for the
+    // next phg_solve, and the last solve's tail whose results phg_ph_step / phg_node_sums take over
+    // when that solve ran (it was gated on the gate published as gated_seq: the host has waited for
+    // that value and it was not below gate_below)
+    int tail_req = 0;
+    double tail_req_thr = 0.0;
+    double* tail_req_out = nullptr;
+    struct {
+        int mode = 0;
+        double thr = 0.0, gate_below = 0.0;
+        long long gated_seq = 0, seq = 0;
+        double* out = nullptr;
+    } tp;
+    unsigned* tail_cnt = nullptr;    // [4] TailArgs::cnt
+    double* xbar_next = nullptr;     // [2 N_tot] staging x-bar of the one-GPU tail
     // the launch schedule is recomputed after every sched_every()-th solve (iteration counts move
     // slowly under warm starts; the sort is a latency-bound single-workgroup launch)
     int solves = 0;
@@ -298,6 +328,12 @@ static bool fold_active(const phg_handle* h) {
 // below its convthresh -- and its partials, written to the handle's own buffer, are carried into the
 // caller's exchange buffer by the next phg_node_sums / phg_fold_partials instead of being lost, which
 // would leave that buffer's already all-reduced partials to be summed a second time)
+// the last solve's fused tail ran (ph_tail.h): that solve was predicated on the gate the host has
+// since waited for, and the value was not below its threshold (a gated-off launch runs nothing)
+static bool tail_ran(const phg_handle* h) {
+    return h->tp.mode != 0 && h->last_wait_seq == h->tp.gated_seq && h->last_conv >= h->tp.gate_below;
+}
+
 static int flush_fold(phg_handle* h) {
     if (!h->fold_w_pending) return 0;
     PhArgs a = h->ph;
@@ -853,6 +889,10 @@ static int build_local_layout(phg_handle* h, const phg_batch* b) {
         const unsigned long long bf = local_fin_mask(b, plan, LPS, CPL, RPL, D);
         const unsigned qm = local_quad_mask(b, plan, LPS, CPL);
         h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc, bi, bf, qm);
+        h->local_shape_v = v;
+        h->lp_col_of = plan.col_of;
+        h->lp_row_of = plan.row_of;
+        h->lp_cpl_row = plan.cpl_row;
         h->local_masks[0] = mb;
         h->local_masks[1] = mc;
         std::memcpy(h->lshape, sh, sizeof sh);
@@ -1035,8 +1075,8 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
     h->nodesum = h->packed;
     h->convpart = h->packed + 2 * (size_t)b->N_tot;
     if (dalloc(h, &h->gate, 4)) return -1;
-    CK(hipHostMalloc((void**)&h->gate_host, 4 * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
-    for (int i = 0; i < 4; ++i) h->gate_host[i] = 0.0;
+    CK(hipHostMalloc((void**)&h->gate_host, 8 * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped));
+    for (int i = 0; i < 8; ++i) h->gate_host[i] = 0.0;
     return 0;
 }
 
@@ -1909,6 +1949,10 @@ struct Presolved {
     std::vector<double> vals, rl, ru, cl, cu;
     std::vector<int> row_map;
     int removed = 0;
+    // the folded rows as column bounds: fold_col[f], and per scenario [fold_lo, fold_hi][f * S + s]
+    // (phg_set_col_bounds intersects a caller's new column bounds with them again)
+    std::vector<int> fold_col;
+    std::vector<double> fold_lo, fold_hi;
 };
 
 static void presolve_singletons(const phg_batch* in, Presolved& P) {
@@ -1952,6 +1996,7 @@ static void presolve_singletons(const phg_batch* in, Presolved& P) {
             ok = std::max(P.cl[(size_t)s * n + j], lo) <= std::min(P.cu[(size_t)s * n + j], hi);
         }
         if (!ok) continue;
+        P.fold_col.push_back(j);
         for (int s = 0; s < S; ++s) {
             const double a = in->vals[(size_t)s * nnz + p];
             double lo = in->row_lo[(size_t)s * m + i] / a, hi = in->row_hi[(size_t)s * m + i] / a;
@@ -1960,6 +2005,8 @@ static void presolve_singletons(const phg_batch* in, Presolved& P) {
             double& U = P.cu[(size_t)s * n + j];
             L = std::max(L, lo);
             U = std::min(U, hi);
+            P.fold_lo.push_back(lo);
+            P.fold_hi.push_back(hi);
         }
         drop[i] = 1;
         ++P.removed;
@@ -2075,6 +2122,45 @@ static void implied_bounds(const phg_batch* b, std::vector<double>& L, std::vect
     free_cols.clear();
     for (int j = 0; j < n; ++j)
         if (free_any[j]) free_cols.push_back(j);
+}
+
+// the presolved batch as the handle keeps it on the host (phg_batch view: pattern, values, bounds)
+static phg_batch host_view(const phg_handle* h) {
+    phg_batch v{};
+    v.S = h->S; v.n = h->n; v.m = h->m; v.nnz = h->nnz; v.N = h->N;
+    v.rowptr = h->hb.rowptr.data();
+    v.colidx = h->hb.colidx.data();
+    v.nonant_col = h->hb.nonant_col.data();
+    v.vals = h->hb.vals.data();
+    v.row_lo = h->hb.rl.data();
+    v.row_hi = h->hb.ru.data();
+    v.col_lo = h->hb.cl.data();
+    v.col_hi = h->hb.cu.data();
+    return v;
+}
+
+// the safe-bound pass's implied column bounds and repair candidates, from the current bounds
+static int implied_bounds_upload(phg_handle* h) {
+    const phg_batch v = host_view(h);
+    std::vector<double> il, ih;
+    std::vector<int> fc;
+    implied_bounds(&v, il, ih, fc);
+    SafeBoundArgs& sb = h->sb;
+    if (!sb.ilo) {
+        double* dp;
+        int* ip;
+        if (dalloc(h, &dp, il.size())) return -1; sb.ilo = dp;
+        if (dalloc(h, &dp, ih.size())) return -1; sb.ihi = dp;
+        if (dalloc(h, &ip, std::max(1, h->n))) return -1; sb.free_col = ip;
+    }
+    CK(hipMemcpyAsync(const_cast<double*>(sb.ilo), il.data(), il.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    CK(hipMemcpyAsync(const_cast<double*>(sb.ihi), ih.data(), ih.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    sb.nf = (int)fc.size();
+    if (!fc.empty())
+        CK(hipMemcpyAsync(const_cast<int*>(sb.free_col), fc.data(), fc.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+    CK(hipStreamSynchronize(h->stream));   // (the host vectors go out of scope)
+    h->sb_stale = false;
+    return 0;
 }
 
 int phg_implied_bounds(const phg_batch* b_in, double* lo, double* hi, int32_t* n_free) {
@@ -2356,18 +2442,28 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
     pa.vals = h->vals; pa.dc = h->dc; pa.dr = h->dr; pa.cl = h->cl; pa.cu = h->cu; pa.rl = h->rl;
     pa.ru = h->ru; pa.eta = h->eta; pa.bnorm = h->bnorm; pa.scratch = scratch;
     CK(prep_launch(pa, h->stream));
-    {   // safe bounds (bound.hip): pattern in CSR / CSC, implied column bounds, repair candidates
-        std::vector<double> il, ih;
-        std::vector<int> fc;
-        implied_bounds(b, il, ih, fc);
+    {   // safe bounds (bound.hip): pattern in CSR / CSC now; the implied column bounds and repair
+        // candidates at the first safe-bound solve (implied_bounds_upload: a host pass over the
+        // batch that the plugin's one-scenario loads and PH runs without bound reads never need)
         SafeBoundArgs& sb = h->sb;
         sb.rowptr = pa.rowptr; sb.colidx = pa.colidx; sb.colptr = pa.colptr; sb.csc_p = pa.csc_p;
         if (dput(h, &ip, csc_row.data(), nnz)) return -1; sb.rowidx = ip;
-        double* dp;
-        if (dput(h, &dp, il.data(), il.size())) return -1; sb.ilo = dp;
-        if (dput(h, &dp, ih.data(), ih.size())) return -1; sb.ihi = dp;
-        sb.nf = (int)fc.size();
-        if (dput(h, &ip, fc.data(), std::max<size_t>(1, fc.size()))) return -1; sb.free_col = ip;
+        sb.ilo = sb.ihi = nullptr;
+        sb.free_col = nullptr;
+        sb.nf = 0;
+        h->sb_stale = true;
+        auto& hb = h->hb;
+        hb.rowptr.assign(b->rowptr, b->rowptr + m + 1);
+        hb.colidx.assign(b->colidx, b->colidx + nnz);
+        hb.nonant_col.assign(b->nonant_col, b->nonant_col + N);
+        hb.vals.assign(b->vals, b->vals + (size_t)S * nnz);
+        hb.rl.assign(b->row_lo, b->row_lo + (size_t)S * m);
+        hb.ru.assign(b->row_hi, b->row_hi + (size_t)S * m);
+        hb.cl.assign(b->col_lo, b->col_lo + (size_t)S * n);
+        hb.cu.assign(b->col_hi, b->col_hi + (size_t)S * n);
+        h->fold_col = P.fold_col;
+        h->fold_lo = P.fold_lo;
+        h->fold_hi = P.fold_hi;
     }
     if (h->local_variant >= 0) {   // the lane image of the scaled batch (LocalLayout::img)
         const int ni = pdhg_local_image_items(h->local_variant);
@@ -2469,6 +2565,7 @@ static double* field_ptr(phg_handle* h, int f, size_t* count) {
 
 int phg_set(phg_handle* h, int32_t f, const double* in) {
     if (!h || !h->loaded) return fail("phg_set: no batch loaded");
+    h->tp.mode = 0;   // a fused tail's results are for the state as the solve left it
     if ((f == PHG_F_W || f == PHG_F_XBAR || f == PHG_F_CONV_PART) && flush_fold(h)) return -1;
     size_t cnt = 0;
     double* p = field_ptr(h, f, &cnt);
@@ -2596,6 +2693,41 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             a.status_in = h->status;   // front: the solve whose x the update uses
             h->fold_w_pending = false;
             h->fold_conv_pending = true;
+        }
+    }
+    // the PH update of the pipelined iteration at the end of this launch (ph_tail.h): asked for by
+    // phg_set_tail, on a gated prox-QP solve of the lane-local layout that applies a folded update
+    // (its per-scenario partials are the convergence metric the tail reduces); PHG_TAIL=0: never
+    h->tp.mode = 0;
+    {
+        static const bool tail_off = [] { const char* e = std::getenv("PHG_TAIL"); return e && std::atoi(e) == 0; }();
+        const int mode = h->tail_req;
+        h->tail_req = 0;
+        if (mode && !tail_off && h->local_variant >= 0 && a.fold_w && a.gate && !o->fix_nonants && !a.prof) {
+            if (!h->tail_cnt && dalloc(h, &h->tail_cnt, 4)) return -1;
+            if (mode == 1 && !h->xbar_next && dalloc(h, &h->xbar_next, 2 * (size_t)std::max(1, h->N_tot))) return -1;
+            TailArgs& t = a.tl;
+            t.mode = mode;
+            t.W = (h->S + 64 / h->lshape[0] - 1) / (64 / h->lshape[0]);
+            t.T = std::min(t.W, std::min(256, std::max(1, std::max(h->ph.n_seg, h->ph.n_cseg))));
+            t.R = std::min(t.T, 8);
+            t.cnt = h->tail_cnt;
+            t.out = h->tail_req_out;
+            t.xbar_next = h->xbar_next;
+            t.xbar_cur = h->xbar;
+            t.thr = h->tail_req_thr;
+            t.gate = h->gate;
+            t.gate_host = h->gate_host;
+            t.ph = h->ph;
+            t.ph.xN = a.xN;                 // this solve's nonants (the back copy)
+            t.ph.conv_s = h->conv_s;        // ... and its prologue's W-update partials
+            t.ph.fold_st = h->fold_st;
+            h->tp.mode = mode;
+            h->tp.thr = t.thr;
+            h->tp.gate_below = a.gate_below;
+            h->tp.gated_seq = h->wait_seq;  // the gate this solve is predicated on
+            h->tp.out = t.out;
+            if (mode == 1) t.seq = (double)(h->tp.seq = ++h->gate_seq);
         }
     }
     if (h->border_layout) {
@@ -2740,6 +2872,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             if (dalloc(h, &h->sb.Y, (size_t)h->S * h->m)) return -1;
             if (dalloc(h, &h->sb.R, (size_t)h->S * h->n)) return -1;
         }
+        if (h->sb_stale && implied_bounds_upload(h)) return -1;
         SafeBoundArgs sb = h->sb;
         sb.all = o->safe_bound >= 2 ? 1 : 0;
         CK(safe_bound_launch(a, sb, h->stream));
@@ -2757,6 +2890,14 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
 int phg_node_sums(phg_handle* h, double* dev_nodesum) {
     if (!h || !h->loaded) return fail("phg_node_sums: no batch loaded");
     CK(hipSetDevice(h->device));
+    if (h->tp.mode == 2) {
+        const bool ran = tail_ran(h) && dev_nodesum == h->tp.out && !h->fold_w_pending;
+        h->tp.mode = 0;
+        if (ran) {   // the last solve's tail left the node sums and its partials in that buffer
+            h->fold_conv_pending = false;
+            return 0;
+        }
+    }
     if (h->fold_w_pending && flush_fold(h)) return -1;   // x changes only by a solve: keep W in step
     if (!h->t_open && timing_event(h, 1, 0)) return -1;
     h->t_open = (h->timing_mask & 2) != 0;
@@ -2782,7 +2923,7 @@ int phg_apply_xbar(phg_handle* h, const double* dev_nodesum, double* dev_convpar
     if (h->gate_fused) {
         a.gate = h->gate;
         a.gate_host = h->gate_host;
-        a.gate_seq = (double)(++h->gate_seq);
+        a.gate_seq = (double)(h->wait_seq = ++h->gate_seq);
     }
     if (!h->t_open && timing_event(h, 1, 0)) return -1;
     if (timing_event(h, 3, 0)) return -1;
@@ -2800,7 +2941,7 @@ int phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t fi
     PhArgs a = h->ph;
     a.gate = h->gate;
     a.gate_host = h->gate_host;
-    a.gate_seq = (double)(++h->gate_seq);
+    a.gate_seq = (double)(h->wait_seq = ++h->gate_seq);
     if (!h->t_open && timing_event(h, 1, 0)) return -1;
     if (timing_event(h, 3, 0)) return -1;
     if (fold_active(h)) {
@@ -2821,6 +2962,23 @@ int phg_ph_head(phg_handle* h, double* dev_packed, double convthresh, int32_t fi
 
 int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fused) {
     if (!h || !h->loaded) return fail("phg_ph_step: no batch loaded");
+    if (h->tp.mode == 1) {
+        const bool ran = tail_ran(h) && !first && convthresh == h->tp.thr && !h->fold_w_pending;
+        h->tp.mode = 0;
+        if (ran) {   // the last solve's tail did this step: commit its x-bar, take its gate
+            if (out_fused) *out_fused = 0;
+            std::swap(h->xbar, h->xbar_next);
+            h->xsqbar = h->xbar + std::max(1, h->N_tot);
+            h->ph.xbar = h->xbar;
+            h->ph.xsqbar = h->xsqbar;
+            h->fold_conv_pending = false;   // (reduced by the tail into the packed buffer)
+            h->fold_w_pending = true;
+            h->fold_thr = convthresh;
+            h->wait_seq = h->tp.seq;
+            h->gate_fused = false;
+            return 0;
+        }
+    }
     const PhArgs& p = h->ph;
     const bool fusable = p.root_only && p.P == 1 && !p.smooth_on && !p.pcv && !h->no_fuse && !fold_active(h);
     if (out_fused) *out_fused = fusable ? 1 : 0;
@@ -2839,7 +2997,7 @@ int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fu
         a.fold_st = h->fold_st;
         a.gate = h->gate;
         a.gate_host = h->gate_host;
-        a.gate_seq = (double)(++h->gate_seq);
+        a.gate_seq = (double)(h->wait_seq = ++h->gate_seq);
         CK(node_sums_head_launch(a, h->packed, convthresh, first, h->stream));
         h->fold_conv_pending = false;
         if (carry_flushed_partials(h, nullptr)) return -1;
@@ -2859,12 +3017,78 @@ int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fu
     PhArgs a = h->ph;
     a.gate = h->gate;
     a.gate_host = h->gate_host;
-    a.gate_seq = (double)(++h->gate_seq);
+    a.gate_seq = (double)(h->wait_seq = ++h->gate_seq);
     if (!h->t_open && timing_event(h, 1, 0)) return -1;
     CK(ph_step_launch(a, h->packed, convthresh, first, h->stream));
     if (timing_event(h, 1, 1)) return -1;
     h->t_open = false;
     h->gate_fused = false;
+    return 0;
+}
+
+int phg_set_col_bounds(phg_handle* h, const double* col_lo, const double* col_hi) {
+    if (!h || !h->loaded || !col_lo || !col_hi) return fail("phg_set_col_bounds: no batch loaded / null argument");
+    CK(hipSetDevice(h->device));
+    const int S = h->S, n = h->n;
+    const size_t Sn = (size_t)S * n;
+    std::vector<double> L(col_lo, col_lo + Sn), U(col_hi, col_hi + Sn);
+    for (size_t f = 0; f < h->fold_col.size(); ++f) {   // rows the presolve folded into these columns
+        const int j = h->fold_col[f];
+        for (int s = 0; s < S; ++s) {
+            L[(size_t)s * n + j] = std::max(L[(size_t)s * n + j], h->fold_lo[f * S + s]);
+            U[(size_t)s * n + j] = std::min(U[(size_t)s * n + j], h->fold_hi[f * S + s]);
+        }
+    }
+    for (size_t e = 0; e < Sn; ++e)
+        if (!(L[e] <= U[e])) return fail("phg_set_col_bounds: lower bound above upper bound (or NaN)");
+    h->tp.mode = 0;
+    h->hb.cl = L;
+    h->hb.cu = U;
+    h->sb_stale = true;
+    CK(hipMemcpyAsync(h->cl, L.data(), Sn * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    CK(hipMemcpyAsync(h->cu, U.data(), Sn * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    CK(scale_cols_launch(h->cl, h->cu, h->dc, (long)Sn, h->stream));   // x = dc xhat: bounds / dc (prep.hip)
+    if (h->local_variant >= 0) {
+        // the compile-time bound sides of the specialised kernel (BI / BF) must still hold: re-pick
+        // the variant of the same shape for the new bounds, then rebuild the lane image (it holds the
+        // scaled bounds)
+        const phg_batch v = host_view(h);
+        LocalPlan plan;
+        plan.col_of = h->lp_col_of;
+        plan.row_of = h->lp_row_of;
+        plan.cpl_row = h->lp_cpl_row;
+        const int* sh = h->lshape;
+        const unsigned long long bi = local_inf_mask(&v, plan, sh[0], sh[1], sh[2], sh[3]);
+        const unsigned long long bf = local_fin_mask(&v, plan, sh[0], sh[1], sh[2], sh[3]);
+        const unsigned qm = local_quad_mask(&v, plan, sh[0], sh[1]);
+        const char* gen = std::getenv("PHG_LOCAL_GENERIC");
+        const int v2 = (gen && std::atoi(gen)) ? h->local_shape_v
+                       : pdhg_local_pick_masked(h->local_shape_v, h->local_masks[0], h->local_masks[1], bi, bf, qm);
+        const int ni = pdhg_local_image_items(v2);
+        if (ni > h->loc.ni) {
+            double* img;
+            if (dalloc(h, &img, (size_t)S * ni * sh[0])) return -1;
+            h->loc.img = img;
+        }
+        h->local_variant = v2;
+        h->loc.ni = ni;
+        PdhgArgs ia{};
+        ia.S = S; ia.n = n; ia.m = h->m; ia.nnz = h->nnz;
+        ia.loc = h->loc;
+        ia.dc = h->dc; ia.c = h->c; ia.cl = h->cl; ia.cu = h->cu; ia.dr = h->dr; ia.rl = h->rl; ia.ru = h->ru;
+        ia.vals = h->vals;
+        CK(pdhg_local_image_launch(v2, ia, const_cast<double*>(h->loc.img), const_cast<double*>(h->loc.cimg), h->stream));
+    }
+    return 0;
+}
+
+int phg_set_tail(phg_handle* h, int32_t mode, double convthresh, double* dev_packed) {
+    if (!h || !h->loaded) return fail("phg_set_tail: no batch loaded");
+    if (mode < 0 || mode > 2) return fail("phg_set_tail: mode must be 0, 1 or 2");
+    if (mode == 2 && !dev_packed) return fail("phg_set_tail: mode 2 needs the exchange buffer");
+    h->tail_req = mode;
+    h->tail_req_thr = convthresh;
+    h->tail_req_out = mode == 1 ? h->packed : dev_packed;
     return 0;
 }
 
@@ -2875,6 +3099,7 @@ int phg_solve_undo(phg_handle* h) {
     CK(hipStreamSynchronize(h->stream));   // nothing queued may still write the copy being restored
     swap_state(h);
     --h->swaps;
+    h->tp.mode = 0;
     return 0;
 }
 
@@ -2896,17 +3121,17 @@ int phg_conv_start(phg_handle* h, const double* dev_convpart) {
     }
     if (!(h->gate_fused && dev_convpart == nullptr))   // after an all-reduce: a small kernel
         CK(conv_gate_launch(dev_convpart ? dev_convpart : h->convpart, h->P, h->gate, h->gate_host,
-                            (double)(++h->gate_seq), h->stream));
+                            (double)(h->wait_seq = ++h->gate_seq), h->stream));
     h->gate_fused = false;
     return 0;
 }
 
 int phg_conv_wait(phg_handle* h, double* host_conv) {
-    if (!h || !h->loaded || h->gate_seq == 0) return fail("phg_conv_wait: no phg_conv_start pending");
-    // poll the sequence word the kernel stores last; every 2^16 polls make sure the stream has not
-    // failed (an error would otherwise leave us spinning)
-    volatile double* g = h->gate_host;
-    const double want = (double)h->gate_seq;
+    if (!h || !h->loaded || h->wait_seq == 0) return fail("phg_conv_wait: no phg_conv_start pending");
+    // poll the sequence word the kernel stores last (ring slot wait_seq mod 2); every 2^16 polls make
+    // sure the stream has not failed (an error would otherwise leave us spinning)
+    volatile double* g = h->gate_host + 4 * (h->wait_seq & 1);
+    const double want = (double)h->wait_seq;
     for (unsigned long spin = 1; g[3] != want; ++spin) {
         if ((spin & 0xFFFF) == 0) {
             const hipError_t e = hipStreamQuery(h->stream);
@@ -2918,6 +3143,8 @@ int phg_conv_wait(phg_handle* h, double* host_conv) {
     *host_conv = g[0];
     h->summary[0] = (int)g[1];
     h->summary[1] = (int)g[2];
+    h->last_wait_seq = h->wait_seq;
+    h->last_conv = g[0];
     return 0;
 }
 

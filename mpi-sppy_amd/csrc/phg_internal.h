@@ -177,6 +177,86 @@ constexpr int kCtrlTail = 1;     //   re-queued (suspended) scenarios so far (bo
 constexpr int kCtrlDone = 2;     //   scenarios finished (bordered split solves)
 constexpr int kCtrlBar = 16;     //   then 2 words per slot (barrier counter), then 1 per slot (mailbox)
 
+struct NodeSeg {           // a contiguous scenario range inside one node (one level)
+    int level, node, s0, s1, kofs, klen, seg_first_of_node;
+};
+
+struct PhArgs {
+    int S, N, N_tot, n_seg, n_cseg, P;
+    const double* xN;       // [S*N]
+    double* W;              // [S*N]
+    const double* rho;      // [S*N]
+    const double* rho_k;    // [N] when rho[s*N + k] == rho_k[k] for every scenario (set by phg_set on the
+                            // host check; the usual case: defaultPHrho / a per-variable rho_setter), else
+                            // null -- the W update then reads N doubles instead of streaming S*N
+    const int* xidx;        // [S*N]
+    int root_only;          // xidx[s*N + k] == k for all s (two-stage trees): xidx is not read
+    const double* pc;       // [S*L]
+    const double* pcv;      // [S*N] per-nonant prob coefficients (variable probability) or null
+    int L;
+    const int* nonant_level;// [N]
+    const NodeSeg* seg;     // [n_seg]
+    double* segpart;        // [n_seg * 2 * maxk]
+    int maxk;
+    const int* node_first_seg; // [n_nodes+1] segments of node g: [first[g], first[g+1])
+    const int* node_off;    // [n_nodes]
+    const int* node_level;  // [n_nodes]
+    const int* level_len;   // [L]
+    const int* level_kofs;  // [L]
+    int n_nodes;
+    double* nodesum;        // [2*N_tot]
+    double* xbar;           // [N_tot]
+    double* xsqbar;         // [N_tot]
+    const int* cseg_v;      // [n_cseg] virtual rank of conv segment
+    const int* cseg_s0;     // [n_cseg]
+    const int* cseg_s1;
+    double* csegpart;       // [n_cseg]
+    int* csegbad;           // [2*n_cseg] scenarios not optimal / NaN in the last solve
+    const int* vr_first;    // [P+1] conv segments of vrank v
+    const int* status;      // [S] status of the last solve (may be null)
+    double* Z;              // [S*N] smoothing centre (Update_z, phbase.py:329-346), when smooth_on
+    const double* beta;     // [S*N]
+    int smooth_on;
+    unsigned* ticket;       // [3] last-workgroup counters of the two kernels + node_sums' done count
+    unsigned* fticket;      // [4] counters of the fused single-GPU step (ph_step_kernel)
+    int n_final;            // workgroups sharing node_sums' final reduction (last_k_workgroups)
+    // single-GPU PH update: the last w_update workgroup also computes conv into gate (device, read
+    // by predicated solves) and gate_host (pinned host memory, read after the handle's event)
+    double* gate;
+    double* gate_host;
+    double gate_seq;
+    // folded PH update (PdhgArgs::fold_w): per-scenario sums |x - xbar| and statuses left by the solve
+    // prologue; fold_conv: node_sums_kernel also reduces them into the conv partials of the packed
+    // exchange buffer (nodesum + 2 N_tot)
+    const double* conv_s;
+    const int* fold_st;
+    int fold_conv;
+    // a folded update applied on its own (flush_fold): the head's published conv (gate[0]) and its
+    // convthresh -- below it the head left xbar unchanged and W must not move either (the
+    // reference's break before Update_W, phbase.py:1008-1010); null: no gate
+    const double* skip_gate;
+    double skip_below;
+};
+
+// The PH update fused into the end of a lane-local solve (ph_tail.h): mode 0 off; 1 one GPU (node
+// sums into `out`, convergence partials, gate, next x-bar into xbar_next); 2 multi-GPU (node sums and
+// the folded update's convergence partials into the caller's exchange buffer `out`)
+struct TailArgs {
+    int mode;
+    int W;                   // waves of the solve's grid
+    int T;                   // the last T of them to finish run the update (<= W)
+    int R;                   // ranks of the final phase (<= T)
+    unsigned* cnt;           // [4] waves done, tail ranks arrived, final ranks done, give-up flag
+    double* out;             // [2 N_tot node sums | 2P+2 partials | flag]
+    double* xbar_next;       // mode 1: [2 N_tot] the next x-bar / x-sq-bar (the current ones if conv < thr)
+    const double* xbar_cur;  // mode 1: [2 N_tot]
+    double thr;              // mode 1: convthresh
+    double seq;              // mode 1: gate sequence number (gate_host slot seq mod 2)
+    double* gate;            // mode 1: [3] device gate
+    double* gate_host;       // mode 1: [2][4] pinned host ring
+    PhArgs ph;               // node segments, conv segments, probabilities, xN / conv_s / fold_st of this solve
+};
+
 struct PdhgArgs {
     int S, n, m, nnz, N, n_pad;
     Layout lay;
@@ -269,6 +349,8 @@ struct PdhgArgs {
     double* conv_s;         // [S]
     int* fold_st;           // [S]
     const int* status_in;   // [S] statuses of the solve being warm-started from (front copy)
+    // the PH update of the pipelined iteration at the end of the launch (lane-local layout; ph_tail.h)
+    TailArgs tl;
 };
 
 // The kernel argument block in the kernarg segment (constant address space: scalar loads).  Cold code
@@ -319,66 +401,6 @@ struct PrepArgs {
     double* scratch;        // [S*(2n+2m)]
 };
 
-struct NodeSeg {           // a contiguous scenario range inside one node (one level)
-    int level, node, s0, s1, kofs, klen, seg_first_of_node;
-};
-
-struct PhArgs {
-    int S, N, N_tot, n_seg, n_cseg, P;
-    const double* xN;       // [S*N]
-    double* W;              // [S*N]
-    const double* rho;      // [S*N]
-    const double* rho_k;    // [N] when rho[s*N + k] == rho_k[k] for every scenario (set by phg_set on the
-                            // host check; the usual case: defaultPHrho / a per-variable rho_setter), else
-                            // null -- the W update then reads N doubles instead of streaming S*N
-    const int* xidx;        // [S*N]
-    int root_only;          // xidx[s*N + k] == k for all s (two-stage trees): xidx is not read
-    const double* pc;       // [S*L]
-    const double* pcv;      // [S*N] per-nonant prob coefficients (variable probability) or null
-    int L;
-    const int* nonant_level;// [N]
-    const NodeSeg* seg;     // [n_seg]
-    double* segpart;        // [n_seg * 2 * maxk]
-    int maxk;
-    const int* node_first_seg; // [n_nodes+1] segments of node g: [first[g], first[g+1])
-    const int* node_off;    // [n_nodes]
-    const int* node_level;  // [n_nodes]
-    const int* level_len;   // [L]
-    const int* level_kofs;  // [L]
-    int n_nodes;
-    double* nodesum;        // [2*N_tot]
-    double* xbar;           // [N_tot]
-    double* xsqbar;         // [N_tot]
-    const int* cseg_v;      // [n_cseg] virtual rank of conv segment
-    const int* cseg_s0;     // [n_cseg]
-    const int* cseg_s1;
-    double* csegpart;       // [n_cseg]
-    int* csegbad;           // [2*n_cseg] scenarios not optimal / NaN in the last solve
-    const int* vr_first;    // [P+1] conv segments of vrank v
-    const int* status;      // [S] status of the last solve (may be null)
-    double* Z;              // [S*N] smoothing centre (Update_z, phbase.py:329-346), when smooth_on
-    const double* beta;     // [S*N]
-    int smooth_on;
-    unsigned* ticket;       // [3] last-workgroup counters of the two kernels + node_sums' done count
-    unsigned* fticket;      // [4] counters of the fused single-GPU step (ph_step_kernel)
-    int n_final;            // workgroups sharing node_sums' final reduction (last_k_workgroups)
-    // single-GPU PH update: the last w_update workgroup also computes conv into gate (device, read
-    // by predicated solves) and gate_host (pinned host memory, read after the handle's event)
-    double* gate;
-    double* gate_host;
-    double gate_seq;
-    // folded PH update (PdhgArgs::fold_w): per-scenario sums |x - xbar| and statuses left by the solve
-    // prologue; fold_conv: node_sums_kernel also reduces them into the conv partials of the packed
-    // exchange buffer (nodesum + 2 N_tot)
-    const double* conv_s;
-    const int* fold_st;
-    int fold_conv;
-    // a folded update applied on its own (flush_fold): the head's published conv (gate[0]) and its
-    // convthresh -- below it the head left xbar unchanged and W must not move either (the
-    // reference's break before Update_W, phbase.py:1008-1010); null: no gate
-    const double* skip_gate;
-    double skip_below;
-};
 
 
 // PH terms of nonant t = s*N + k in the min-form subproblem objective (phbase.py:670-760):

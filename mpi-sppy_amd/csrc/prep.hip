@@ -1,3 +1,4 @@
+#include <algorithm>
 // prep.hip -- one-time per-batch preconditioning of the scenario LPs (runs at phg_load_batch).
 //
 // For every scenario (one 256-thread workgroup each): Ruiz equilibration (inf-norm, 10 passes),
@@ -105,6 +106,20 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
         a.eta[s] = 0.99 / fmax(anorm, 1e-12);
         a.bnorm[s] = bn;
     }
+}
+
+// new column bounds of a loaded batch (phg_set_col_bounds): scaled as prep_kernel scales them
+__global__ void scale_cols_kernel(double* cl, double* cu, const double* dc, long cnt) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < cnt; e += (long)gridDim.x * blockDim.x) {
+        cl[e] = cl[e] / dc[e];
+        cu[e] = cu[e] / dc[e];
+    }
+}
+
+hipError_t scale_cols_launch(double* cl, double* cu, const double* dc, long cnt, hipStream_t stream) {
+    const int grid = (int)std::min<long>(1024, (cnt + 255) / 256);
+    hipLaunchKernelGGL(scale_cols_kernel, dim3(std::max(1, grid)), dim3(256), 0, stream, cl, cu, dc, cnt);
+    return hipGetLastError();
 }
 
 hipError_t prep_launch(const PrepArgs& a, hipStream_t stream) {

@@ -313,6 +313,21 @@ class Engine:
         _lib.check(self.lib.phg_ph_step(self.h, float(convthresh), int(bool(first)), ptr(fused)))
         return bool(fused[0])
 
+    def set_col_bounds(self, lo, hi):
+        """New column bounds ([S, n], the models' units) without reloading (phg_set_col_bounds)."""
+        lo = as_f64(np.asarray(lo, np.float64).reshape(-1))
+        hi = as_f64(np.asarray(hi, np.float64).reshape(-1))
+        if lo.size != self.S * self.batch.n or hi.size != lo.size:
+            raise ValueError("set_col_bounds: need S * n lower and upper bounds")
+        _lib.check(self.lib.phg_set_col_bounds(self.h, ptr(lo), ptr(hi)))
+
+    def set_tail(self, convthresh):
+        """Run the next iteration's PH update at the end of the next solve (phg_set_tail): one GPU,
+        node sums + gate + next x-bar, which the following ph_step takes over; with an exchange
+        buffer, node sums + partials into it, which the following node_sums takes over."""
+        mode = 2 if self.exchange is not None else 1
+        _lib.check(self.lib.phg_set_tail(self.h, mode, float(convthresh), self._ns_ptr()))
+
     def set_fold(self, on):
         """Folded PH update on / off (phg_set_fold); returns whether this batch's solves take it."""
         out = np.zeros(1, np.int32)

@@ -150,6 +150,7 @@ class PHGSolver(_PersistentBase):
         self._pending_obj = None
         self._X = None
         self.rebuilds = 0     # engine loads (matrix + bounds); a PH run on one model needs one
+        self.bound_updates = 0   # column-bound changes applied to the loaded engine (no reload)
         self.solves = 0
 
     # ------------------------------------------------------------------ plugin surface
@@ -258,10 +259,14 @@ class PHGSolver(_PersistentBase):
         for (c, q, c0, sense, lo, hi) in cur:
             if (sense * q < 0).any():
                 raise ValueError("PHGSolver: the quadratic objective is not convex (min-form diagonal < 0)")
-        if self._engine is None or any(
-                b[2] != k[3] or not np.array_equal(b[3], k[4]) or not np.array_equal(b[4], k[5])
-                for b, k in zip(self._base, cur)):
+        if self._engine is None or any(b[2] != k[3] for b, k in zip(self._base, cur)):
             self._build(cur)
+        elif any(not np.array_equal(b[3], k[4]) or not np.array_equal(b[4], k[5]) for b, k in zip(self._base, cur)):
+            # fixed / freed variables (spopt.py:590-640): the bounds change on the device (phg_set_col_bounds),
+            # the engine -- matrix, scaling, layout, warm start -- stays
+            self._engine.set_col_bounds(np.stack([k[4] for k in cur]), np.stack([k[5] for k in cur]))
+            self._base = [(b[0], b[1], b[2], k[4].copy(), k[5].copy()) for b, k in zip(self._base, cur)]
+            self.bound_updates += 1
         eng = self._engine
         # the objective now, as PH terms on the loaded base cost (min form): W = c - c0, rho = q
         eng.set(_lib.F_W, np.concatenate([sense * (c - b[0]) for (c, q, c0, sense, lo, hi), b in zip(cur, self._base)]))

@@ -19,6 +19,7 @@ raises (the kernels solve the exact prox QP).  ``variable_probability`` (``prob_
 ``prob0_mask``) and smoothed PH are supported.
 """
 import math
+import os
 import time
 
 import numpy as np
@@ -327,6 +328,13 @@ class PHBase(SPBase):
             eng.ph_head(thr, first)
         else:   # one GPU: node sums and the gated W update in one launch (phg_ph_step)
             eng.ph_step(thr, first)
+        # the next iteration's node sums (+ head on one GPU) at the end of this solve's launch
+        # (include/phg.h phg_set_tail; taken over by the next ph_step / node_sums when the solve ran)
+        tail = self.options.get("pdhg_tail")
+        if tail is None:   # (off by default until it measures faster: DESIGN.md (d) round 5; PHG_TAIL=1 on)
+            tail = os.environ.get("PHG_TAIL", "0") == "1"
+        if thr > 0 and tail and hasattr(eng, "set_tail"):
+            eng.set_tail(thr)
         self.solve_loop(solver_options=self.current_solver_options, gripe=verbose, verbose=verbose,
                         skip_below=thr if thr > 0 else 0.0, safe_bound=False)
         self._spec_pending = True

@@ -259,7 +259,8 @@ def test_reference_solve_one_on_mutated_models_reproduces_w_file(persistent):
 def test_plugin_rereads_fixed_bounds():
     """``_fix_nonants`` fixes variables in place (``spopt.py:590-620``; a persistent plugin also gets
     ``update_var``): the next solve honours the fixed values, the one after unfixing frees them
-    again (a bound change reloads the engine; the objective-only changes above do not)."""
+    again -- each bound change applied to the loaded engine (phg_set_col_bounds: one engine load
+    for the whole sequence, two bound updates)."""
     m = farmer.scenario_creator("scen1", num_scens=3)
     s = PHModel(m, 1.0)
     opt = SolverFactory("phg")
@@ -283,8 +284,47 @@ def test_plugin_rereads_fixed_bounds():
         s.vars[j].fixed = False
     r2 = opt.solve(s, load_solutions=True)
     assert r2.Problem[0].Upper_bound == pytest.approx(free_obj, rel=1e-7)
-    assert opt.rebuilds == 3
+    assert opt.rebuilds == 1 and opt.bound_updates == 2
     opt.close()
+
+
+@pytest.mark.parametrize("layout", ["auto", "gather", "block"])
+def test_set_col_bounds_equals_fresh_load(layout):
+    """phg_set_col_bounds on a loaded farmer batch (every nonant fixed to a point, then a mix of
+    tightened and freed bounds) solves to the same bits as a fresh load of the same bounds, cold
+    started: the bounds are scaled as the load scales them, the lane-local variant is re-picked for
+    the new bound sides (its compile-time infinite / finite sides, BI / BF) and its lane image
+    rebuilt; the safe bounds use implied bounds recomputed from the new ones."""
+    from mpisppy_amd import _lib
+    from mpisppy_amd.engine import BatchArrays, Engine
+    names = farmer.scenario_names_creator(6)
+    models = [farmer.scenario_creator(nm, crops_multiplier=2, num_scens=6) for nm in names]
+    batch = BatchArrays(models, ["ROOT"], [1.0 / 6] * 6, 0, 6, 1)
+    lo, hi = batch.cl.copy(), batch.cu.copy()
+    lo2, hi2 = lo.copy(), hi.copy()
+    cols = batch.nonant_col
+    lo2[:, cols[::2]] = hi2[:, cols[::2]] = 100.0          # every other acreage fixed
+    hi2[:, cols[1::2]] = np.inf                             # the others' finite upper sides freed:
+    lo2[:, cols[1::2]] = 10.0                               # (a compile-time-finite side -> re-pick)
+    outs = []
+    for mode in ("update", "fresh"):
+        b = BatchArrays(models, ["ROOT"], [1.0 / 6] * 6, 0, 6, 1)
+        if mode == "fresh":
+            b.cl, b.cu = lo2.copy(), hi2.copy()
+        eng = Engine(b, layout=layout)
+        eng.set(_lib.F_XBAR, np.zeros(b.N))
+        if mode == "update":
+            eng.solve(0, 0, eps=1e-9, warm_start=0)
+            eng.set_col_bounds(lo2, hi2)
+        eng.solve(0, 0, eps=1e-9, warm_start=0, safe_bound=2)
+        outs.append([eng.get(_lib.F_OBJ), eng.get(_lib.F_BOUND), eng.get_i32(_lib.I_ITERS), eng.get(_lib.F_X)])
+        eng.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+    x = outs[0][3].reshape(6, -1)
+    assert (x >= lo2 - 1e-6).all() and (x <= hi2 + 1e-6).all()
+    assert (x[:, cols[1::2]] >= 10.0 - 1e-6).all()
+    np.testing.assert_allclose(x[:, cols[::2]], 100.0, rtol=1e-7)
 
 
 def _ph(names, creator, kw, **extra):

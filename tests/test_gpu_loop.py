@@ -15,10 +15,12 @@ from mpisppy_amd.examples import farmer  # noqa: E402
 from mpisppy_amd.ph import PH  # noqa: E402
 
 
-def _run(pipeline, trip_at=None, limit=12):
+def _run(pipeline, trip_at=None, limit=12, tail=False):
+    # (tail=False: the separate-launch pipeline, bit-identical to the sequential loop; the solve's
+    # fused tail sums in another order: test_gpu_parity.test_solve_tail_matches_separate_launches)
     opts = {"solver_name": "phg", "PHIterLimit": limit, "defaultPHrho": 1.0, "convthresh": 1e-10,
             "verbose": False, "display_progress": False, "pdhg_pipeline": pipeline,
-            "time_limit": 1e9 if trip_at else None}
+            "time_limit": 1e9 if trip_at else None, "pdhg_tail": tail}
     ph = PH(opts, farmer.scenario_names_creator(30), farmer.scenario_creator,
             scenario_creator_kwargs={"crops_multiplier": 10, "num_scens": 30})
     if trip_at:
@@ -36,6 +38,19 @@ def test_pipelined_exits_match_sequential(trip_at):
     np.testing.assert_array_equal(a.Ws(), b.Ws())
     np.testing.assert_array_equal(a.nonants(), b.nonants())
     np.testing.assert_array_equal(a.xbars(), b.xbars())
+
+
+@pytest.mark.parametrize("trip_at", [None, 2, 5])
+def test_tail_pipeline_exits_match_sequential(trip_at):
+    """The same exits with the PH update fused into the solve's tail (ph_tail.h): the drain after the
+    time limit / PHIterLimit must discard the last tail's staged x-bar and recompute conv from the
+    partials -- the state equals the sequential loop's to rounding."""
+    a, b = _run(True, trip_at, tail=True), _run(False, trip_at)
+    assert a._PHIter == b._PHIter
+    assert len(a.conv_history) == len(b.conv_history) == a._PHIter
+    np.testing.assert_allclose(a.conv_history, b.conv_history, rtol=1e-10)
+    for u, v in ((a.Ws(), b.Ws()), (a.nonants(), b.nonants()), (a.xbars(), b.xbars())):
+        np.testing.assert_allclose(u, v, rtol=1e-9, atol=1e-9 * max(1.0, float(np.abs(v).max())))
 
 
 def test_ungated_solve_after_converged_head_is_fresh():

@@ -360,7 +360,8 @@ def test_pipelined_iteration_matches_sequential(fuse, fold, monkeypatch):
     monkeypatch.setenv("PHG_FOLD", fold)
     out = []
     for pipe in (True, False):
-        ph = _farmer_ph(4, cm=1, PHIterLimit=200, convthresh=1e-3, pdhg_pipeline=pipe)
+        # (the separate-launch pipeline: the fused solve tail sums in another order, tested below)
+        ph = _farmer_ph(4, cm=1, PHIterLimit=200, convthresh=1e-3, pdhg_pipeline=pipe, pdhg_tail=False)
         conv, eobj, tb = ph.ph_main()
         out.append((ph._PHIter, conv, eobj, ph.conv_history, ph.Ws().copy(), ph.xbars().copy(),
                     ph.nonants().copy(), ph.solve_count))
@@ -383,7 +384,7 @@ def test_folded_update_at_full_size_matches_unfolded(monkeypatch):
     res = []
     for fold, exch in (("1", False), ("0", False), ("1", True)):
         monkeypatch.setenv("PHG_FOLD", fold)
-        opts = dict(PHIterLimit=30, convthresh=1e-10)
+        opts = dict(PHIterLimit=30, convthresh=1e-10, pdhg_tail=False)
         if exch:
             opts["pdhg_exchange"] = True
         ph = _farmer_ph(10000, cm=10, **opts)
@@ -404,7 +405,7 @@ def test_field_read_between_head_and_solve_keeps_fold_trajectory(monkeypatch, th
     monkeypatch.setenv("PHG_FOLD", "1")
     res = []
     for peek in (False, True):
-        ph = _farmer_ph(1000, cm=10, PHIterLimit=25, convthresh=thr, pdhg_exchange=True)
+        ph = _farmer_ph(1000, cm=10, PHIterLimit=25, convthresh=thr, pdhg_exchange=True, pdhg_tail=False)
         if peek:
             from mpisppy_amd.engine import Engine
             head = Engine.ph_head
@@ -421,6 +422,40 @@ def test_field_read_between_head_and_solve_keeps_fold_trajectory(monkeypatch, th
         assert len(res[0][0]) < 25 and res[0][0][-1] < thr       # stopped on convthresh
     for a, b in zip(res[0][1:], res[1][1:]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("S,exch,thr", [(10000, False, 1e-10), (10000, True, 1e-10), (1000, False, 5.0),
+                                        (1000, True, 5.0), (30, False, 1e-4)])
+def test_solve_tail_matches_separate_launches(S, exch, thr):
+    """The PH update fused into the end of the solve (ph_tail.h, phg_set_tail): one GPU (mode 1:
+    node sums, conv, gate and the staged next x-bar) and the exchange form (mode 2: node sums and
+    partials into the packed buffer, then the all-reduce and the head) against the same pipelined
+    iterations with separate launches.  The tail's sums are fixed-order but associated differently
+    (node segments summed by 64-lane waves), so the trajectories agree to rounding: the same PH
+    iteration count and break (thr 5 stops on convthresh; S = 30 runs to conv < 1e-4), conv history
+    to 1e-10 relative, W / x-bar / x to 1e-9."""
+    res = []
+    for tail in (True, False):
+        opts = dict(PHIterLimit=30 if S > 30 else 20000, convthresh=thr, pdhg_tail=tail)
+        if exch:
+            opts["pdhg_exchange"] = True
+        ph = _farmer_ph(S, cm=10, **opts)
+        ph.ph_main(finalize=False)
+        res.append((list(ph.conv_history), ph.Ws().copy(), ph.xbars().copy(), ph.nonants().copy(), ph._PHIter))
+    (h1, W1, xb1, x1, it1), (h0, W0, xb0, x0, it0) = res
+    assert it1 == it0 and len(h1) == len(h0), (it1, it0)
+    # over 30 PH iterations the rounding stays at 1e-10; over the ~9 500 of the S = 30 run to
+    # convergence it grows (each prox-QP is solved to a 1e-9 KKT error) -- there the north star's
+    # tolerances: x-bar 1e-6 relative, W 1e-5
+    long_run = len(h0) > 100
+    tol = 1e-6 if long_run else 1e-9
+    np.testing.assert_allclose(h1, h0, rtol=1e-5 if long_run else 1e-10)
+    if thr > 1e-9:
+        assert h1[-1] < thr
+    sc = max(1.0, float(np.abs(x0).max()))
+    np.testing.assert_allclose(xb1, xb0, rtol=tol, atol=tol * sc)
+    np.testing.assert_allclose(x1, x0, rtol=tol, atol=tol * sc)
+    np.testing.assert_allclose(W1, W0, rtol=tol, atol=1e-5 if long_run else 1e-9 * max(1.0, float(np.abs(W0).max())))
 
 
 # ----------------------------------------------------------------------------- non-uniform trees (M3)
