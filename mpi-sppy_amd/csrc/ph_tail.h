@@ -79,14 +79,37 @@ __device__ __forceinline__ void ph_tail_end(const TailArgs& tl, double* lds) {
     unsigned* cnt = tl.cnt;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are out
     int t = -1;
+    // PHG_TAIL_PROF stamps (100 MHz): [0] the last wave's arrival, [1] rank 0 past the wait,
+    // [2] rank 0 done with its partials, [3] final rank 0 past the second wait, [4] its stores done
+    auto stamp = [&](int i) {
+        if (tl.prof && lane == 0) tl.prof[i] = __builtin_amdgcn_s_memrealtime();
+    };
     if (lane == 0) {
         const unsigned prev = __hip_atomic_fetch_add(cnt + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         t = (int)prev - (tl.W - tl.T);
+        if (tl.prof && prev == (unsigned)tl.W - 1) tl.prof[0] = __builtin_amdgcn_s_memrealtime();
     }
     t = __shfl(t, 0, 64);
     if (t < 0) return;
     if (!tail_wait(cnt + 0, (unsigned)tl.W, cnt + 3)) return;
+    if (t == 0) stamp(1);
     // ---------------------------------------------------------------- 1. partials
+    // this rank's conv segment (one per rank when n_cseg <= T and a segment has <= 128 scenarios:
+    // its loads issued now, with the node segment's, and reduced after -- one round trip for both)
+    const bool cpre = p.n_cseg <= tl.T && (t >= p.n_cseg || p.cseg_s1[t] - p.cseg_s0[t] <= 128);
+    double cv[2] = {0.0, 0.0};
+    int cst[2] = {0, 0};
+    if (cpre && t < p.n_cseg) {
+        const int s0 = p.cseg_s0[t], s1 = p.cseg_s1[t];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int s = s0 + lane + 64 * h;
+            const int sc = s < s1 ? s : s0;
+            cv[h] = p.conv_s[sc];
+            cst[h] = p.fold_st[sc];
+            if (!(s < s1)) { cv[h] = 0.0; cst[h] = 0; }
+        }
+    }
     for (int g = t; g < p.n_seg; g += tl.T) {
         const NodeSeg sg = p.seg[g];
         double* out = p.segpart + (long)g * 2 * p.maxk;
@@ -137,7 +160,17 @@ __device__ __forceinline__ void ph_tail_end(const TailArgs& tl, double* lds) {
         }
     }
     // the folded update's conv segments: sum |x - xbar| and the status counts of its solve
-    for (int b = t; b < p.n_cseg; b += tl.T) {
+    if (cpre && t < p.n_cseg) {   // (the order of the loop below: lane-strided, then the butterfly)
+        const double acc = wave_sum(cv[0] + cv[1]);
+        const int nb = wave_sum((int)(cst[0] != 0) + (int)(cst[1] != 0));
+        const int nn = wave_sum((int)(cst[0] == 2) + (int)(cst[1] == 2));
+        if (lane == 0) {
+            st_sc1(&p.csegpart[t], acc);
+            st_sc1(&p.csegbad[2 * t], nb);
+            st_sc1(&p.csegbad[2 * t + 1], nn);
+        }
+    }
+    for (int b = t; !cpre && b < p.n_cseg; b += tl.T) {
         const int s0 = p.cseg_s0[b], s1 = p.cseg_s1[b];
         double acc = 0.0;
         int nb = 0, nn = 0;
@@ -158,6 +191,7 @@ __device__ __forceinline__ void ph_tail_end(const TailArgs& tl, double* lds) {
     }
     // ---------------------------------------------------------------- arrival, ranks
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t == 0) stamp(2);
     int rank = -1;
     if (lane == 0) {
         const unsigned prev = __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -166,46 +200,19 @@ __device__ __forceinline__ void ph_tail_end(const TailArgs& tl, double* lds) {
     rank = __shfl(rank, 0, 64);
     if (rank < 0) return;
     if (!tail_wait(cnt + 1, (unsigned)tl.T, cnt + 3)) return;
-    // ---------------------------------------------------------------- 2. convergence partials
-    // per virtual rank v: (sum |x - xbar|, count) in fixed order; the status counts; the flag
+    if (rank == 0) stamp(3);
+    // ---------------------------------------------------------------- 2. final (rank of R)
     double* cp = tl.out + 2 * (long)p.N_tot;
-    double conv = 0.0;
-    int tb = 0, tn = 0;
-    for (int v = 0; v < p.P; ++v) {
-        const int g0 = p.vr_first[v], g1 = p.vr_first[v + 1];
-        double s = 0.0;
-        for (int g = g0 + lane; g < g1; g += 64) s += p.csegpart[g];
-        s = wave_sum(s);
-        const double c = g1 > g0 ? (double)(p.cseg_s1[g1 - 1] - p.cseg_s0[g0]) * (double)p.N : 0.0;
-        if (c > 0.0) conv += s / c;
-        if (rank == 0 && lane == 0) {
-            cp[2 * v] = s;
-            cp[2 * v + 1] = c;
-        }
-    }
-    for (int g = lane; g < p.n_cseg; g += 64) {
-        tb += p.csegbad[2 * g];
-        tn += p.csegbad[2 * g + 1];
-    }
-    tb = wave_sum(tb);
-    tn = wave_sum(tn);
-    conv /= (double)p.P;
-    if (rank == 0 && lane == 0) {
-        cp[2 * p.P] = (double)tb;
-        cp[2 * p.P + 1] = (double)tn;
-        cp[2 * p.P + 2] = 1.0;   // the partials are a W update's
-    }
-    const bool keep = tl.mode == 1 && !(conv >= tl.thr);   // below convthresh: x-bar stays
-    // ---------------------------------------------------------------- final node sums, slice `rank`
+    // this rank's slice of the node sums: TL lanes per element, each adding every TL-th segment of
+    // the element's node, then a fixed butterfly
     const int e_lo = (int)((long)p.N_tot * rank / tl.R), e_hi = (int)((long)p.N_tot * (rank + 1) / tl.R);
     const int ne = e_hi - e_lo;
-    int TL = 1;   // lanes per element: each adds every TL-th segment, then a fixed butterfly
+    int TL = 1;
     while (TL < 64 && TL * 2 * ne <= 64) TL *= 2;
     const int E = 64 / TL;
     const int sub = lane % TL;
-    for (int e0 = e_lo; e0 < e_hi; e0 += E) {
-        const int e = e0 + lane / TL;
-        double a1 = 0.0, a2 = 0.0;
+    auto node_sum = [&](int e, double& a1, double& a2) {
+        a1 = a2 = 0.0;
         if (e < e_hi) {
             int lo = 0, hi = p.n_nodes - 1;   // node g with node_off[g] <= e
             while (lo < hi) {
@@ -223,6 +230,63 @@ __device__ __forceinline__ void ph_tail_end(const TailArgs& tl, double* lds) {
             a1 += __shfl_xor(a1, o, 64);
             a2 += __shfl_xor(a2, o, 64);
         }
+    };
+    // one virtual rank and <= 128 conv segments (the usual case): their partials loaded first, then
+    // this rank's node sums (one pass when its slice fits), both in flight together
+    const bool fastc = p.P == 1 && p.n_cseg <= 128;
+    const bool one_pass = ne <= E;
+    double cA[2] = {0.0, 0.0};
+    int bA[4] = {0, 0, 0, 0};
+    if (fastc) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int g = lane + 64 * h;
+            const int gc = g < p.n_cseg ? g : 0;
+            cA[h] = p.csegpart[gc];
+            bA[2 * h] = p.csegbad[2 * gc];
+            bA[2 * h + 1] = p.csegbad[2 * gc + 1];
+            if (!(g < p.n_cseg)) { cA[h] = 0.0; bA[2 * h] = bA[2 * h + 1] = 0; }
+        }
+    }
+    double f1 = 0.0, f2 = 0.0;
+    if (one_pass) node_sum(e_lo + lane / TL, f1, f2);
+    // convergence partials: per virtual rank v (sum |x - xbar|, count) in fixed order; the status
+    // counts; the flag -- the same sums in every rank
+    double conv = 0.0;
+    int tb = 0, tn = 0;
+    for (int v = 0; v < p.P; ++v) {
+        const int g0 = p.vr_first[v], g1 = p.vr_first[v + 1];
+        double sv = 0.0;
+        if (fastc) sv = cA[0] + cA[1];
+        else
+            for (int g = g0 + lane; g < g1; g += 64) sv += p.csegpart[g];
+        sv = wave_sum(sv);
+        const double c = g1 > g0 ? (double)(p.cseg_s1[g1 - 1] - p.cseg_s0[g0]) * (double)p.N : 0.0;
+        if (c > 0.0) conv += sv / c;
+        if (rank == 0 && lane == 0) {
+            cp[2 * v] = sv;
+            cp[2 * v + 1] = c;
+        }
+    }
+    if (fastc) {
+        tb = bA[0] + bA[2];
+        tn = bA[1] + bA[3];
+    } else {
+        for (int g = lane; g < p.n_cseg; g += 64) {
+            tb += p.csegbad[2 * g];
+            tn += p.csegbad[2 * g + 1];
+        }
+    }
+    tb = wave_sum(tb);
+    tn = wave_sum(tn);
+    conv /= (double)p.P;
+    if (rank == 0 && lane == 0) {
+        cp[2 * p.P] = (double)tb;
+        cp[2 * p.P + 1] = (double)tn;
+        cp[2 * p.P + 2] = 1.0;   // the partials are a W update's
+    }
+    const bool keep = tl.mode == 1 && !(conv >= tl.thr);   // below convthresh: x-bar stays
+    auto put = [&](int e, double a1, double a2) {
         if (e < e_hi && sub == 0) {
             tl.out[e] = a1;
             tl.out[p.N_tot + e] = a2;
@@ -231,6 +295,18 @@ __device__ __forceinline__ void ph_tail_end(const TailArgs& tl, double* lds) {
                 tl.xbar_next[p.N_tot + e] = keep ? tl.xbar_cur[p.N_tot + e] : a2;
             }
         }
+    };
+    if (one_pass) {
+        put(e_lo + lane / TL, f1, f2);
+    } else {
+        for (int e0 = e_lo; e0 < e_hi; e0 += E) {
+            node_sum(e0 + lane / TL, f1, f2);
+            put(e0 + lane / TL, f1, f2);
+        }
+    }
+    if (tl.prof && rank == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(4);
     }
     // ---------------------------------------------------------------- gate (one GPU), re-arm
     if (tl.mode == 1 && rank == 0 && lane == 0) {

@@ -2711,6 +2711,14 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
             t.W = (h->S + 64 / h->lshape[0] - 1) / (64 / h->lshape[0]);
             t.T = std::min(t.W, std::min(256, std::max(1, std::max(h->ph.n_seg, h->ph.n_cseg))));
             t.R = std::min(t.T, 8);
+            // PHG_TAIL_PROF=1 (diagnostic): the tail's phase stamps, printed after the launch (syncs)
+            static unsigned long long* tprof = nullptr;
+            t.prof = nullptr;
+            if (const char* e = std::getenv("PHG_TAIL_PROF"); e && std::atoi(e)) {
+                if (!tprof) CK(hipMalloc((void**)&tprof, 8 * sizeof(unsigned long long)));
+                CK(hipMemsetAsync(tprof, 0, 8 * sizeof(unsigned long long), h->stream));
+                t.prof = tprof;
+            }
             t.cnt = h->tail_cnt;
             t.out = h->tail_req_out;
             t.xbar_next = h->xbar_next;
@@ -2866,6 +2874,15 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     else if (h->wave_variant >= 0) CK(pdhg_wave_launch(h->wave_variant, a, h->stream));
     else CK(pdhg_launch(h->variant, a, h->stream));
     if (timing_event(h, 0, 1)) return -1;
+    if (a.tl.mode && a.tl.prof) {
+        unsigned long long st[8];
+        CK(hipMemcpyAsync(st, a.tl.prof, sizeof st, hipMemcpyDeviceToHost, h->stream));
+        CK(hipStreamSynchronize(h->stream));
+        auto us = [&](int i, int j) { return st[i] && st[j] ? ((double)st[j] - (double)st[i]) / 100.0 : -1.0; };
+        fprintf(stderr, "PHG_TAIL_PROF T %d R %d waves %d: last wave -> rank0 past wait %.2f us, partials %.2f us, "
+                "-> final past wait %.2f us, final %.2f us, total %.2f us\n", a.tl.T, a.tl.R, a.tl.W, us(0, 1),
+                us(1, 2), us(2, 3), us(3, 4), us(0, 4));
+    }
     h->xn_external = false;
     if (o->safe_bound && !o->fix_nonants) {   // bound.hip: certificates whatever the statuses
         if (!h->sb.Y) {

@@ -247,6 +247,7 @@ struct TailArgs {
     int T;                   // the last T of them to finish run the update (<= W)
     int R;                   // ranks of the final phase (<= T)
     unsigned* cnt;           // [4] waves done, tail ranks arrived, final ranks done, give-up flag
+    unsigned long long* prof;   // diagnostic (PHG_TAIL_PROF): [8] s_memrealtime stamps of the tail, or null
     double* out;             // [2 N_tot node sums | 2P+2 partials | flag]
     double* xbar_next;       // mode 1: [2 N_tot] the next x-bar / x-sq-bar (the current ones if conv < thr)
     const double* xbar_cur;  // mode 1: [2 N_tot]

@@ -290,41 +290,44 @@ def test_plugin_rereads_fixed_bounds():
 
 @pytest.mark.parametrize("layout", ["auto", "gather", "block"])
 def test_set_col_bounds_equals_fresh_load(layout):
-    """phg_set_col_bounds on a loaded farmer batch (every nonant fixed to a point, then a mix of
-    tightened and freed bounds) solves to the same bits as a fresh load of the same bounds, cold
-    started: the bounds are scaled as the load scales them, the lane-local variant is re-picked for
-    the new bound sides (its compile-time infinite / finite sides, BI / BF) and its lane image
-    rebuilt; the safe bounds use implied bounds recomputed from the new ones."""
+    """phg_set_col_bounds on a loaded farmer batch (half the nonants fixed to a point, the others'
+    finite upper side freed and their lower side raised) solves to the same bits as a fresh load of
+    the same bounds, cold started: the bounds are scaled as the load scales them, the lane-local
+    variant is re-picked for the new bound sides (its compile-time finite sides, BF) and its lane
+    image rebuilt; the safe bounds use implied bounds recomputed from the new ones."""
     from mpisppy_amd import _lib
-    from mpisppy_amd.engine import BatchArrays, Engine
-    names = farmer.scenario_names_creator(6)
-    models = [farmer.scenario_creator(nm, crops_multiplier=2, num_scens=6) for nm in names]
-    batch = BatchArrays(models, ["ROOT"], [1.0 / 6] * 6, 0, 6, 1)
-    lo, hi = batch.cl.copy(), batch.cu.copy()
-    lo2, hi2 = lo.copy(), hi.copy()
-    cols = batch.nonant_col
-    lo2[:, cols[::2]] = hi2[:, cols[::2]] = 100.0          # every other acreage fixed
-    hi2[:, cols[1::2]] = np.inf                             # the others' finite upper sides freed:
-    lo2[:, cols[1::2]] = 10.0                               # (a compile-time-finite side -> re-pick)
+    S, kw = 6, {"crops_multiplier": 2, "num_scens": 6}
+    m0 = farmer.scenario_creator("scen0", **kw)
+    cols = [v.col for nd in m0._mpisppy_node_list for v in nd.nonant_vardata_list]
+    lo2, hi2 = np.array(m0._lo, float), np.array(m0._hi, float)
+    lo2[cols[::2]] = hi2[cols[::2]] = 100.0          # every other acreage fixed
+    hi2[cols[1::2]] = np.inf                          # the others' finite upper side freed
+    lo2[cols[1::2]] = 10.0
+
+    def bounded(nm, **k):
+        m = farmer.scenario_creator(nm, **k)
+        m._lo, m._hi = list(lo2), list(hi2)
+        return m
     outs = []
     for mode in ("update", "fresh"):
-        b = BatchArrays(models, ["ROOT"], [1.0 / 6] * 6, 0, 6, 1)
-        if mode == "fresh":
-            b.cl, b.cu = lo2.copy(), hi2.copy()
-        eng = Engine(b, layout=layout)
-        eng.set(_lib.F_XBAR, np.zeros(b.N))
+        ph = PH({"solver_name": "phg", "PHIterLimit": 1, "defaultPHrho": 1.0, "convthresh": 1e-10,
+                 "verbose": False, "display_progress": False, "pdhg_layout": layout},
+                farmer.scenario_names_creator(S), farmer.scenario_creator if mode == "update" else bounded,
+                scenario_creator_kwargs=kw)
+        ph.PH_Prep()
+        eng = ph.engine
         if mode == "update":
             eng.solve(0, 0, eps=1e-9, warm_start=0)
-            eng.set_col_bounds(lo2, hi2)
+            eng.set_col_bounds(np.tile(lo2, (S, 1)), np.tile(hi2, (S, 1)))
         eng.solve(0, 0, eps=1e-9, warm_start=0, safe_bound=2)
         outs.append([eng.get(_lib.F_OBJ), eng.get(_lib.F_BOUND), eng.get_i32(_lib.I_ITERS), eng.get(_lib.F_X)])
         eng.close()
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
-    x = outs[0][3].reshape(6, -1)
+    x = outs[0][3].reshape(S, -1)
     assert (x >= lo2 - 1e-6).all() and (x <= hi2 + 1e-6).all()
-    assert (x[:, cols[1::2]] >= 10.0 - 1e-6).all()
     np.testing.assert_allclose(x[:, cols[::2]], 100.0, rtol=1e-7)
+    assert (x[:, cols[1::2]] >= 10.0 - 1e-6).all()
 
 
 def _ph(names, creator, kw, **extra):
