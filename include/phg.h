@@ -217,9 +217,16 @@ int  phg_set_presolve(phg_handle* h, int32_t on);
 int  phg_implied_bounds(const phg_batch* b, double* lo, double* hi, int32_t* n_free);
 int  phg_presolve_info(phg_handle* h, int32_t* out2);
 int  phg_load_batch(phg_handle* h, const phg_batch* b);
+/* phg_set returns once host_in is copied (to page-locked staging); the device copy is ordered on the
+ * handle's stream before everything enqueued after it.  phg_get / phg_get_i32 synchronise.        */
 int  phg_set(phg_handle* h, int32_t field, const double* host_in);
 int  phg_get(phg_handle* h, int32_t field, double* host_out);
 int  phg_get_i32(phg_handle* h, int32_t field, int32_t* host_out);
+/* the last solve's per-scenario results in ONE synchronisation (replaces phg_sync + phg_get_i32
+ * STATUS / ITERS + phg_get KKT / OBJ / BOUND / X after a solve: what a solver plugin returns per
+ * solve, spopt.py:184-231); any pointer may be NULL.  status, iters, kkt, obj, bound: [S]; x: [S*n]  */
+int  phg_solve_results(phg_handle* h, int32_t* status, int32_t* iters, double* kkt, double* obj,
+                       double* bound, double* x);
 /* shared-matrix MFMA layout: out4 = {row tiles, column tiles, 16x4 fragments with a nonzero in
  * A x, in A^T y} (each is one v_mfma_f64_16x16x4_f64 per PDHG iteration per 16 scenarios)       */
 int  phg_mfma_info(phg_handle* h, int32_t* out4);

@@ -64,6 +64,7 @@ SIGNATURES = {
     "phg_set": (C.c_int, [C.c_void_p, C.c_int32, f64p]),
     "phg_get": (C.c_int, [C.c_void_p, C.c_int32, f64p]),
     "phg_get_i32": (C.c_int, [C.c_void_p, C.c_int32, i32p]),
+    "phg_solve_results": (C.c_int, [C.c_void_p, i32p, i32p, f64p, f64p, f64p, f64p]),
     "phg_info": (C.c_int, [C.c_void_p, i32p]),
     "phg_solve": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(PhgOpts)]),
     "phg_node_sums": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -190,6 +190,12 @@ struct phg_handle {
     bool no_fuse = true;
     bool have_order = false;
     double* pinned = nullptr;  // page-locked readback buffer (convergence partials)
+    // page-locked staging of phg_set's uploads (a ring: each slot reused once its copy has run, so
+    // phg_set returns without a stream synchronisation) and of phg_solve_results' one readback
+    struct Stage { void* p = nullptr; size_t cap = 0; hipEvent_t ev = nullptr; };
+    Stage up[4];
+    int up_next = 0;
+    Stage down;
     int summary[2] = {0, 0};   // scenarios not optimal / NaN, as of the last phg_conv_finish
     int* nonant_col_d = nullptr;
     unsigned char* row_fixed = nullptr;   // [m] every column of the (kept) row is a nonant
@@ -407,6 +413,11 @@ void phg_destroy(phg_handle* h) {
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->pinned) (void)hipHostFree(h->pinned);
     if (h->gate_host) (void)hipHostFree(h->gate_host);
+    for (auto& st : h->up) {
+        if (st.p) (void)hipHostFree(st.p);
+        if (st.ev) (void)hipEventDestroy(st.ev);
+    }
+    if (h->down.p) (void)hipHostFree(h->down.p);
     for (auto& v : h->tev)
         for (auto& e : v) (void)hipEventDestroy(e);
     if (h->own_stream) (void)hipStreamDestroy(h->stream);
@@ -2563,6 +2574,32 @@ static double* field_ptr(phg_handle* h, int f, size_t* count) {
     }
 }
 
+// a page-locked copy of `bytes` of host data, valid until the copies enqueued from it have run
+// (stage_done records that point): pageable uploads are staged and synchronised by the runtime, ~25 us
+// each; from pinned memory they are plain stream-ordered DMA
+static int stage_upload(phg_handle* h, const void* in, size_t bytes, const void** out) {
+    auto& st = h->up[h->up_next];
+    if (st.ev) CK(hipEventSynchronize(st.ev));          // the slot's previous copies have run
+    else CK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
+    if (st.cap < bytes) {
+        if (st.p) CK(hipHostFree(st.p));
+        st.p = nullptr;
+        st.cap = 0;
+        const size_t cap = std::max(bytes, (size_t)4096);
+        CK(hipHostMalloc(&st.p, cap, hipHostMallocDefault));
+        st.cap = cap;
+    }
+    std::memcpy(st.p, in, bytes);
+    *out = st.p;
+    return 0;
+}
+
+static int stage_done(phg_handle* h) {
+    CK(hipEventRecord(h->up[h->up_next].ev, h->stream));
+    h->up_next = (h->up_next + 1) % 4;
+    return 0;
+}
+
 int phg_set(phg_handle* h, int32_t f, const double* in) {
     if (!h || !h->loaded) return fail("phg_set: no batch loaded");
     h->tp.mode = 0;   // a fused tail's results are for the state as the solve left it
@@ -2571,9 +2608,7 @@ int phg_set(phg_handle* h, int32_t f, const double* in) {
     double* p = field_ptr(h, f, &cnt);
     if (!p) return fail("phg_set: unknown field");
     if ((f == PHG_F_X || f == PHG_F_Y) && materialize_outputs(h)) return -1;
-    if (f == PHG_F_XBAR) {   // also keep the node-sum buffer consistent
-        CK(hipMemcpyAsync(h->nodesum, in, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
-    }
+    CK(hipSetDevice(h->device));
     std::vector<double> packed;
     if (f == PHG_F_Y && h->m != h->m_orig) {   // caller's rows -> kept rows
         packed.resize(cnt);
@@ -2583,7 +2618,11 @@ int phg_set(phg_handle* h, int32_t f, const double* in) {
                     packed[(size_t)s2 * h->m + h->row_map[i]] = in[(size_t)s2 * h->m_orig + i];
         in = packed.data();
     }
-    CK(hipMemcpyAsync(p, in, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    const void* staged = nullptr;
+    if (stage_upload(h, in, cnt * sizeof(double), &staged)) return -1;
+    if (f == PHG_F_XBAR)   // also keep the node-sum buffer consistent
+        CK(hipMemcpyAsync(h->nodesum, staged, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    CK(hipMemcpyAsync(p, staged, cnt * sizeof(double), hipMemcpyHostToDevice, h->stream));
     if (f == PHG_F_XN) h->xn_external = true;
     if (f == PHG_F_RHO) {   // rho the same in every scenario? then the W update reads its [N] copy
         bool shared = true;
@@ -2593,11 +2632,10 @@ int phg_set(phg_handle* h, int32_t f, const double* in) {
             if (dalloc(h, &q, (size_t)std::max(1, h->N))) return -1;
             h->rho_k = q;
         }
-        if (shared) CK(hipMemcpyAsync(h->rho_k, in, (size_t)h->N * sizeof(double), hipMemcpyHostToDevice, h->stream));
+        if (shared) CK(hipMemcpyAsync(h->rho_k, staged, (size_t)h->N * sizeof(double), hipMemcpyHostToDevice, h->stream));
         h->ph.rho_k = shared ? h->rho_k : nullptr;
     }
-    CK(hipStreamSynchronize(h->stream));
-    return 0;
+    return stage_done(h);
 }
 
 int phg_get(phg_handle* h, int32_t f, double* out) {
@@ -2628,6 +2666,40 @@ int phg_get_i32(phg_handle* h, int32_t f, int32_t* out) {
     if (!p) return fail("phg_get_i32: unknown field");
     CK(hipMemcpyAsync(out, p, (size_t)h->S * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     CK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int phg_solve_results(phg_handle* h, int32_t* status, int32_t* iters, double* kkt, double* obj,
+                      double* bound, double* x) {
+    if (!h || !h->loaded) return fail("phg_solve_results: no batch loaded");
+    CK(hipSetDevice(h->device));
+    if (x && materialize_outputs(h)) return -1;
+    const size_t S = (size_t)h->S, nx = (size_t)h->S * h->n;
+    const size_t bytes = 2 * S * sizeof(int) + 3 * S * sizeof(double) + (x ? nx * sizeof(double) : 0) + 64;
+    auto& st = h->down;
+    if (st.cap < bytes) {
+        if (st.p) CK(hipHostFree(st.p));
+        st.p = nullptr;
+        st.cap = 0;
+        CK(hipHostMalloc(&st.p, bytes, hipHostMallocDefault));
+        st.cap = bytes;
+    }
+    // doubles first (8-byte aligned), then the two int arrays
+    double* d = (double*)st.p;
+    int* iv = (int*)(d + 3 * S + (x ? nx : 0));
+    CK(hipMemcpyAsync(d, h->kkt, S * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    CK(hipMemcpyAsync(d + S, h->obj, S * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    CK(hipMemcpyAsync(d + 2 * S, h->bound, S * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (x) CK(hipMemcpyAsync(d + 3 * S, h->x_out, nx * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    CK(hipMemcpyAsync(iv, h->status, S * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    CK(hipMemcpyAsync(iv + S, h->iters, S * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    if (kkt) std::memcpy(kkt, d, S * sizeof(double));
+    if (obj) std::memcpy(obj, d + S, S * sizeof(double));
+    if (bound) std::memcpy(bound, d + 2 * S, S * sizeof(double));
+    if (x) std::memcpy(x, d + 3 * S, nx * sizeof(double));
+    if (status) std::memcpy(status, iv, S * sizeof(int));
+    if (iters) std::memcpy(iters, iv + S, S * sizeof(int));
     return 0;
 }
 

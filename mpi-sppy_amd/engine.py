@@ -255,6 +255,17 @@ class Engine:
         a = as_f64(np.broadcast_to(np.asarray(values, np.float64), (self._count(field),)).copy())
         _lib.check(self.lib.phg_set(self.h, field, ptr(a)))
 
+    def results(self, x=True):
+        """(status, iters, kkt, obj, bound, x or None) of the last solve in one synchronisation
+        (``phg_solve_results``); x is [S, n]."""
+        S = self.S
+        st, it = np.empty(S, np.int32), np.empty(S, np.int32)
+        kkt, obj, bnd = np.empty(S), np.empty(S), np.empty(S)
+        X = np.empty((S, self.batch.n)) if x else None
+        _lib.check(self.lib.phg_solve_results(self.h, ptr(st), ptr(it), ptr(kkt), ptr(obj), ptr(bnd),
+                                              ptr(X) if x else None))
+        return st, it, kkt, obj, bnd, X
+
     def get_i32(self, field):
         out = np.empty(self.S, np.int32)
         _lib.check(self.lib.phg_get_i32(self.h, field, ptr(out)))

@@ -39,6 +39,8 @@ of the solve's dual iterate for every solve (``phg_opts.safe_bound`` = 2): never
 of the optimum, also at ``maxIterations`` (a converged solve's own dual objective can sit
 eps (1 + |p| + |d|) above it).
 """
+import os
+
 import numpy as np
 
 from ..engine import BatchArrays, Engine
@@ -152,6 +154,7 @@ class PHGSolver(_PersistentBase):
         self.rebuilds = 0     # engine loads (matrix + bounds); a PH run on one model needs one
         self.bound_updates = 0   # column-bound changes applied to the loaded engine (no reload)
         self.solves = 0
+        self.pdhg_iterations = 0   # PDHG iterations over all solves (diagnostic)
 
     # ------------------------------------------------------------------ plugin surface
     def available(self, exception_flag=False):
@@ -250,6 +253,7 @@ class PHGSolver(_PersistentBase):
         self._engine.set(_lib.F_XBAR, np.zeros(self._lms[0].n))
         self._base = [(c.copy(), c0, sense, lo.copy(), hi.copy()) for c, q, c0, sense, lo, hi in cur]
         self._warm = False
+        self._sent_w = self._sent_rho = None
         self.rebuilds += 1
 
     def _solve(self, tee, load_solutions):
@@ -269,21 +273,25 @@ class PHGSolver(_PersistentBase):
             self.bound_updates += 1
         eng = self._engine
         # the objective now, as PH terms on the loaded base cost (min form): W = c - c0, rho = q
-        eng.set(_lib.F_W, np.concatenate([sense * (c - b[0]) for (c, q, c0, sense, lo, hi), b in zip(cur, self._base)]))
-        eng.set(_lib.F_RHO, np.concatenate([sense * q for (c, q, c0, sense, lo, hi) in cur]))
-        warm = 1 if (self._warm and self.options.get("pdhg_warm_start", True)) else 0
+        # (each upload only when it changed: PH's rho is fixed, W moves every iteration)
+        w = np.concatenate([sense * (c - b[0]) for (c, q, c0, sense, lo, hi), b in zip(cur, self._base)])
+        r = np.concatenate([sense * q for (c, q, c0, sense, lo, hi) in cur])
+        if self._sent_w is None or not np.array_equal(w, self._sent_w):
+            eng.set(_lib.F_W, w)
+            self._sent_w = w
+        if self._sent_rho is None or not np.array_equal(r, self._sent_rho):
+            eng.set(_lib.F_RHO, r)
+            self._sent_rho = r
+        # warm start from the previous solution (bit 0) and its primal weight (bit 1, as the batched PH)
+        ws = self.options.get("pdhg_warm_start", True)
+        warm = (int(os.environ.get("PHG_PLUGIN_WARM", "3")) if ws is True else int(ws)) if self._warm else 0
         eng.solve(1, 1, eps=float(self.options.get("pdhg_eps", 1e-9)),
                   max_iter=int(self.options.get("pdhg_max_iter", 200000)),
                   check_every=int(self.options.get("pdhg_check_every", 32)), warm_start=warm, safe_bound=2)
-        eng.sync()
+        st, it, kkt, obj, bnd, X = eng.results()     # one synchronisation (phg_solve_results)
         self._warm = True
         self.solves += 1
-        st = eng.get_i32(_lib.I_STATUS)
-        it = eng.get_i32(_lib.I_ITERS)
-        kkt = eng.get(_lib.F_KKT)
-        obj = eng.get(_lib.F_OBJ)
-        bnd = eng.get(_lib.F_BOUND)
-        X = eng.get(_lib.F_X).reshape(eng.S, -1)
+        self.pdhg_iterations += int(it.sum())
         self._X = X
         out = []
         for s, ((c, q, c0, sense, lo, hi), b) in enumerate(zip(cur, self._base)):
