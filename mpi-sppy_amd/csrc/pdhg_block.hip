@@ -385,7 +385,8 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
             if (ri[r] >= 0) {
                 const double pr = axx[r] - clampd(axx[r], rlo[r], rhi[r]);
                 v[0] += pr * pr;
-                const double pu = pr / a.dr[sm_ + ri[r]];
+                // (VS: the scaling is already in a register -- no per-check load or address to keep)
+                const double pu = pr / (VS ? drs[r] : a.dr[sm_ + ri[r]]);
                 v[2] += pu * pu;
                 if (fin(rlo[r])) v[5] += rlo[r] * fmax(yy[r], 0.0);
                 if (fin(rhi[r])) v[5] += rhi[r] * fmin(yy[r], 0.0);
@@ -400,7 +401,7 @@ __global__ __launch_bounds__(NT) void pdhg_block_kernel(PdhgArgs a) {
                 if (!fin(lo[k]) && rc_ > 0.0) dres += rc_;
                 if (!fin(hi[k]) && rc_ < 0.0) dres += rc_;
                 v[1] += dres * dres;
-                const double du = dres / a.dc[sn_ + cj[k]];
+                const double du = dres / (VS ? dcs[k] : a.dc[sn_ + cj[k]]);
                 v[3] += du * du;
                 v[4] += c[k] * xx[k] + 0.5 * q[k] * xx[k] * xx[k];
                 if (fin(lo[k])) v[5] += lo[k] * fmax(rc_, 0.0);
