@@ -52,8 +52,8 @@ def parse():
                          "unit's cost at mid output, as uc_cylinders.py passes it): PH converges ~17x further in "
                          "60 s, each early PH iteration's solves ~15x heavier (DESIGN.md (d))")
     ap.add_argument("--eps", type=float, default=None,
-                    help="PDHG relative KKT tolerance (default 1e-9; uc 1e-6: at n ~ 2e4 PDHG needs > 2e5 "
-                         "iterations per solve for 1e-9)")
+                    help="PDHG relative KKT tolerance (default 1e-9; uc 1e-7, where its bounds are within the "
+                         "north star's 1e-6 -- at n ~ 2e4 PDHG needs > 2e5 iterations per solve for 1e-9)")
     ap.add_argument("--conv-iters", type=int, default=20000, help="PH iteration cap for time-to-conv (0: skip)")
     ap.add_argument("--conv-time", type=float, default=120.0,
                     help="wall cap (s) for time-to-conv (PHBase time_limit; not set for farmer, whose "
@@ -218,7 +218,8 @@ def main():
     if args.scen is None:
         args.scen = default_scen
     if args.eps is None:
-        args.eps = 1e-6 if args.case == "uc" else 1e-9
+        # uc: 1e-7, the tolerance at which its bounds meet the north star's 1e-6 (test_uc_fullsize_at_north_star_accuracy)
+        args.eps = 1e-7 if args.case == "uc" else 1e-9
     if args.rho is None:
         args.rho = 10000.0 if args.case == "netdes" else 1.0
     S = args.scen * world
@@ -258,7 +259,8 @@ def main():
         step()
     # timed region: per-launch HIP events and iteration counts are accumulated on the device and
     # read once afterwards (no per-step host synchronisation beyond PH's own conv readback)
-    eng.timing_reset(solves=True)
+    ev_inline = os.environ.get("PHG_BENCH_EVENTS", "1") != "0"
+    eng.timing_reset(solves=ev_inline)
     if comm is not None:
         comm.barrier()
     torch.cuda.synchronize()
@@ -269,6 +271,11 @@ def main():
     if comm is not None:
         comm.barrier()
     el = time.perf_counter() - t0
+    if not ev_inline:   # (A/B of the events' own cost) the solve launches timed over as many further steps
+        eng.timing_reset(solves=True)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
     pdhg_ms, n_solves, pdhg_iters = eng.timing(0)
     assert n_solves == args.steps, n_solves
     # the PH update timed separately (HIP events only on it) over extra pipelined iterations, as the
