@@ -131,6 +131,7 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
     }
     double omega = 1.0, tau = 0.0, sig = 0.0;
     int it = 0, since = 0, cnt = 0;
+    int chk_mod = 0;   // the group's checks so far, modulo avg_every (avg: chk_mod == 0 at a check)
 
     // ------------------------------------------------------------------ products
     // (loops fully unrolled: the mask tests fold to constants)
@@ -596,6 +597,7 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         it = 0;
         since = 0;
         cnt = 0;
+        chk_mod = 0;
     };
 
     // epilogue of a group that has terminated (st 0 optimal, 1 iteration limit, 2 NaN)
@@ -779,7 +781,10 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         // the average iterate's KKT (products of the running sums: ~half the check) every
         // avg_every-th check of the group -- uniform over the wave, the check's reductions are
         // group-local but the products are wave-wide
-        const bool avg = wave_any(live && (a.avg_every <= 1 || ((it / chk) % a.avg_every) == 0));
+        // ((it / chk) % avg_every == 0, counted instead of divided: a runtime integer division and
+        // modulo on the VALU were ~40 instructions per check)
+        chk_mod = chk_mod + 1 >= a.avg_every ? 0 : chk_mod + 1;
+        const bool avg = wave_any(live && chk_mod == 0);
         if constexpr (FOLDT) mv_aty(y, yd, aty);   // not formed in the iterations
         kkt_both(avg, inv, oc, oa);
         if constexpr (PROF) pf_kkt += clock64() - pf_t1;
