@@ -556,8 +556,14 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
             for (int k = 0; k < CPL; ++k) rr[2] += c[k] * c[k];
             gsum_many<LPS, 5>(rr);
             if (fold && gl == 0) {   // (write-through: the tail waves read them in this launch)
-                st_sc1(&ka->conv_s[s], rr[4]);
-                st_sc1(&ka->fold_st[s], ka->status_in[s]);
+                if (ka->tl.mode) {
+                    st_sc1(&ka->conv_s[s], rr[4]);
+                    st_sc1(&ka->fold_st[s], ka->status_in[s]);
+                } else {   // (plain stores without the tail: write-through stores cost ~0.3 ms per
+                           // launch at 1e6 scenarios, the PH-update sweep)
+                    ka->conv_s[s] = rr[4];
+                    ka->fold_st[s] = ka->status_in[s];
+                }
             }
             rr[3] += b2d;
             GS(CI::SC + CI::CNORM) = sqrt(rr[0]);
@@ -626,6 +632,7 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         const double sg = ka->sense;
         double* xs_ = ka->xs;
         double* xN_ = ka->xN;
+        const bool tl_on = ka->tl.mode != 0;
         double* ys_ = ka->ys;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
@@ -635,7 +642,10 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
                 xs_[b] = xv;
                 const double xu = xv * dcv[k];
                 if (xo) xo[b] = xu;
-                if (kq[k] >= 0) st_sc1(&xN_[sN + kq[k]], xu);   // (write-through: read by the tail)
+                if (kq[k] >= 0) {   // (write-through only when the tail reads them in this launch)
+                    if (tl_on) st_sc1(&xN_[sN + kq[k]], xu);
+                    else xN_[sN + kq[k]] = xu;
+                }
             }
         }
 #pragma unroll
