@@ -2753,8 +2753,10 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         // (a final / extension solve after PH converged).  Then the pending W update runs
         // on its own, gated like that head (flush_fold: nothing moves when it found conv below its
         // convthresh -- the reference's break before Update_W, phbase.py:1008-1010), and this solve
-        // runs ungated on whatever W that leaves: its outputs are always fresh
-        const bool ungated = !a.gate && h->fold_thr > -INFINITY;
+        // runs ungated on whatever W that leaves: its outputs are always fresh.  (A head whose
+        // convthresh is <= 0 can never have found conv below it -- conv >= 0 -- so its update is
+        // unconditional and stays folded into this solve.)
+        const bool ungated = !a.gate && h->fold_thr > 0.0;
         if (!fold_active(h) || h->xn_external || ungated) {
             if (flush_fold(h)) return -1;
         } else {
