@@ -55,6 +55,14 @@ def check_every_default(layout):
     return 64 if layout in ("gather", "block") else 32
 
 
+def beta_artificial_default(layout):
+    """PDHG artificial-restart fraction by kernel layout (0: the library's 0.25).  The multi-workgroup
+    bordered / range-split layouts (UC) take PDLP's 0.36: UC 64 at eps 1e-7, 477 vs 581 ms per PH
+    iteration, the slowest solve 62 880 vs 75 264 PDHG iterations (0.5: 478, 0.6: 507, 0.8: 536 ms;
+    DESIGN.md (d) round 5); the lane-local / gather / block kernels keep 0.25."""
+    return 0.36 if layout in ("border", "stream") else 0.0
+
+
 class PHBase(SPBase):
     def __init__(self, options, all_scenario_names, scenario_creator, scenario_denouement=None,
                  all_nodenames=None, mpicomm=None, scenario_creator_kwargs=None, extensions=None,
@@ -152,6 +160,8 @@ class PHBase(SPBase):
                 o[k] = self.current_solver_options[k]
         if o["pdhg_check_every"] is None:
             o["pdhg_check_every"] = check_every_default(getattr(self.engine, "layout", "auto"))
+        if not o["pdhg_beta_artificial"]:
+            o["pdhg_beta_artificial"] = beta_artificial_default(getattr(self.engine, "layout", "auto"))
         return o
 
     # ------------------------------------------------------------------------------- W / prox

@@ -203,8 +203,10 @@ def test_border_matches_block_kernel(monkeypatch, reg):
     o.Update_W()
     res = {}
     for layout in ("block", "border"):
-        # the same check interval on both (the default is by layout: phbase.check_every_default)
-        ph = PH(_opts(pdhg_layout=layout, pdhg_check_every=32), uc.scenario_names_creator(3), uc.scenario_creator, scenario_creator_kwargs=kw)
+        # the same check interval and artificial-restart fraction on both (the defaults are by
+        # layout: phbase.check_every_default, beta_artificial_default)
+        ph = PH(_opts(pdhg_layout=layout, pdhg_check_every=32, pdhg_beta_artificial=0.25), uc.scenario_names_creator(3),
+                uc.scenario_creator, scenario_creator_kwargs=kw)
         ph.PH_Prep()
         assert ph.engine.layout == layout
         ph.Iter0()
