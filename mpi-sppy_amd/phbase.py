@@ -56,11 +56,18 @@ def check_every_default(layout):
 
 
 def beta_artificial_default(layout):
-    """PDHG artificial-restart fraction by kernel layout (0: the library's 0.25).  The multi-workgroup
-    bordered / range-split layouts (UC) take PDLP's 0.36: UC 64 at eps 1e-7, 477 vs 581 ms per PH
-    iteration, the slowest solve 62 880 vs 75 264 PDHG iterations (0.5: 478, 0.6: 507, 0.8: 536 ms;
-    DESIGN.md (d) round 5); the lane-local / gather / block kernels keep 0.25."""
-    return 0.36 if layout in ("border", "stream") else 0.0
+    """PDHG artificial-restart fraction by kernel layout (0: the library's 0.25), from round 5's
+    sweeps on MI355X (`profiles/r05/betaart/`, `profiles/r05/uc/sweep/`):
+    * bordered / range-split (UC 64, eps 1e-7): PDLP's 0.36 -- 477 vs 581 ms per PH iteration
+      (0.5: 478, 0.6: 507, 0.8: 536);
+    * workgroup block (sslp 4 096): 0.15 -- 5.24-5.26 vs 5.46-5.47 ms per PH iteration, 1 096 vs
+      1 145 PDHG iterations per solve (0.1: 5.44, 0.2: 5.26, 0.36: 6.10); netdes within noise;
+    * wave gather (hydro 2 000): 0.15 -- 0.318 vs 0.325 ms (0.1: 0.315, 0.36: 0.353);
+    * lane-local (farmer 10k): the library's 0.25 (0.15: 0.2924, 0.2: 0.2897, 0.36: 0.3009 vs
+      0.2885 ms).
+    (The one-wave-per-scenario shared-matrix kernel, on request for block-kernel problems, follows
+    the block kernel.)"""
+    return {"border": 0.36, "stream": 0.36, "block": 0.15, "wave": 0.15, "gather": 0.15}.get(layout, 0.0)
 
 
 class PHBase(SPBase):
