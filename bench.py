@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--check-every", type=int, default=None,
                     help="PDHG restart/termination check interval (default: by layout, phbase.check_every_default)")
     ap.add_argument("--beta-art", type=float, default=0.0, help="artificial restart fraction (0: default)")
+    ap.add_argument("--beta-suf", type=float, default=0.0, help="sufficient-decay restart factor (0: default 0.2)")
+    ap.add_argument("--beta-nec", type=float, default=0.0, help="necessary-decay restart factor (0: default 0.8)")
     ap.add_argument("--theta", type=float, default=0.0, help="primal weight smoothing (0: default)")
     ap.add_argument("--keep-omega", default="blend", choices=["fresh", "carry", "blend"],
                     help="PDHG primal weight at each solve: fresh estimate, the previous solve's, or "
@@ -227,7 +229,8 @@ def main():
     opts = {"solver_name": "phg", "PHIterLimit": args.warmup + args.steps, "defaultPHrho": args.rho,
             "convthresh": 1e-4, "verbose": False, "display_progress": False, "pdhg_layout": args.layout,
             "pdhg_schedule": not args.no_schedule, "pdhg_check_every": args.check_every,
-            "pdhg_beta_artificial": args.beta_art, "pdhg_primal_weight_theta": args.theta, "pdhg_presolve": not args.no_presolve,
+            "pdhg_beta_artificial": args.beta_art, "pdhg_beta_sufficient": args.beta_suf,
+            "pdhg_beta_necessary": args.beta_nec, "pdhg_primal_weight_theta": args.theta, "pdhg_presolve": not args.no_presolve,
             "pdhg_keep_omega": {"fresh": False, "carry": True, "blend": "blend"}[args.keep_omega],
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps},
             "pdhg_exchange": force_dist}
