@@ -76,9 +76,9 @@ def parse():
     ap.add_argument("--beta-suf", type=float, default=0.0, help="sufficient-decay restart factor (0: default 0.2)")
     ap.add_argument("--beta-nec", type=float, default=0.0, help="necessary-decay restart factor (0: default 0.8)")
     ap.add_argument("--theta", type=float, default=0.0, help="primal weight smoothing (0: default)")
-    ap.add_argument("--keep-omega", default="blend", choices=["fresh", "carry", "blend"],
+    ap.add_argument("--keep-omega", default=None, choices=["fresh", "carry", "blend"],
                     help="PDHG primal weight at each solve: fresh estimate, the previous solve's, or "
-                         "their geometric mean (default)")
+                         "their geometric mean (default: by layout, phbase.keep_omega_default)")
     ap.add_argument("--no-presolve", action="store_true", help="keep singleton rows as rows")
     ap.add_argument("--traffic-json", default=DEFAULT_TRAFFIC)
     return ap.parse_args()
@@ -231,7 +231,7 @@ def main():
             "pdhg_schedule": not args.no_schedule, "pdhg_check_every": args.check_every,
             "pdhg_beta_artificial": args.beta_art, "pdhg_beta_sufficient": args.beta_suf,
             "pdhg_beta_necessary": args.beta_nec, "pdhg_primal_weight_theta": args.theta, "pdhg_presolve": not args.no_presolve,
-            "pdhg_keep_omega": {"fresh": False, "carry": True, "blend": "blend"}[args.keep_omega],
+            "pdhg_keep_omega": {None: None, "fresh": False, "carry": True, "blend": "blend"}[args.keep_omega],
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps},
             "pdhg_exchange": force_dist}
     args.creator_kwargs = ckw

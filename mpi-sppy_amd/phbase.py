@@ -40,7 +40,7 @@ def _omega_bits(keep):
 
 
 # pdhg_check_every None: by layout (check_every_default)
-_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": None, "pdhg_keep_omega": "blend",
+_SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every": None, "pdhg_keep_omega": None,
                     "pdhg_schedule": True, "pdhg_beta_sufficient": 0.0, "pdhg_beta_necessary": 0.0,
                     "pdhg_beta_artificial": 0.0, "pdhg_primal_weight_theta": 0.0}
 
@@ -50,9 +50,18 @@ def check_every_default(layout):
     one-wave-per-scenario gather kernel (tiny subproblems: hydro 2 000, 6.2 vs 5.3 M solves/s, the
     slowest scenario 704 vs 1 024 PDHG iterations, time to PH conv 0.029 vs 0.34 s over the same
     ~104 PH iterations) and the workgroup-block kernel (netdes 1 024: 19.9 vs 22.0 ms per PH
-    iteration, sslp 4 096: 5.50 vs 5.65 ms), 32 elsewhere (farmer: 40 / 48 / 64 cost time to conv;
-    the MFMA kernel at 64 missed a hydro parity objective in round 2)."""
-    return 64 if layout in ("gather", "block") else 32
+    iteration, sslp 4 096: 5.50 vs 5.65 ms) and the shared-matrix MFMA kernel (hydro 20 000, round
+    5: 0.565 vs 0.688 ms per PH iteration; 96 / 128: 0.80 / 0.77 ms; its round-2 parity miss at 64
+    predates the gap test on the whole objective), 32 elsewhere (farmer: 40 / 48 / 64 cost time to
+    conv)."""
+    return 64 if layout in ("gather", "block", "mfma") else 32
+
+
+def keep_omega_default(layout):
+    """pdhg_keep_omega by layout: the primal weight re-estimated at every solve on the shared-matrix
+    MFMA kernel (hydro 20 000 at check interval 64: 0.537 vs 0.565 ms per PH iteration with the
+    blend, 1.60 ms carried -- round 5), the blend elsewhere (farmer: DESIGN.md (d) round 2)."""
+    return False if layout == "mfma" else "blend"
 
 
 def beta_artificial_default(layout):
@@ -167,6 +176,8 @@ class PHBase(SPBase):
                 o[k] = self.current_solver_options[k]
         if o["pdhg_check_every"] is None:
             o["pdhg_check_every"] = check_every_default(getattr(self.engine, "layout", "auto"))
+        if o["pdhg_keep_omega"] is None:
+            o["pdhg_keep_omega"] = keep_omega_default(getattr(self.engine, "layout", "auto"))
         if not o["pdhg_beta_artificial"]:
             o["pdhg_beta_artificial"] = beta_artificial_default(getattr(self.engine, "layout", "auto"))
         return o
