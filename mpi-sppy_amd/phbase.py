@@ -45,7 +45,7 @@ _SOLVER_DEFAULTS = {"pdhg_eps": 1e-9, "pdhg_max_iter": 200000, "pdhg_check_every
                     "pdhg_beta_artificial": 0.0, "pdhg_primal_weight_theta": 0.0}
 
 
-def check_every_default(layout):
+def check_every_default(layout, threads=0):
     """PDHG restart / termination check interval by kernel layout (measured on MI355X): 64 for the
     one-wave-per-scenario gather kernel (tiny subproblems: hydro 2 000, 6.2 vs 5.3 M solves/s, the
     slowest scenario 704 vs 1 024 PDHG iterations, time to PH conv 0.029 vs 0.34 s over the same
@@ -54,6 +54,11 @@ def check_every_default(layout):
     5: 0.565 vs 0.688 ms per PH iteration; 96 / 128: 0.80 / 0.77 ms; its round-2 parity miss at 64
     predates the gap test on the whole objective), 32 elsewhere (farmer: 40 / 48 / 64 cost time to
     conv)."""
+    if layout == "block" and 0 < threads <= 256:
+        # 256-thread workgroups (sslp's register-resident pieces): 96 with the block kernel's
+        # artificial-restart fraction 0.15 -- 5.14 vs 5.25-5.27 ms per PH iteration at 4 096 (128:
+        # 5.43); netdes' 1 024-thread kernel stays at 64 (96: 8.56 vs 8.04 ms) -- round 5
+        return 96
     return 64 if layout in ("gather", "block", "mfma") else 32
 
 
@@ -175,7 +180,8 @@ class PHBase(SPBase):
             if self.current_solver_options and k in self.current_solver_options:
                 o[k] = self.current_solver_options[k]
         if o["pdhg_check_every"] is None:
-            o["pdhg_check_every"] = check_every_default(getattr(self.engine, "layout", "auto"))
+            o["pdhg_check_every"] = check_every_default(getattr(self.engine, "layout", "auto"),
+                                                        getattr(self.engine, "lanes_per_scenario", 0))
         if o["pdhg_keep_omega"] is None:
             o["pdhg_keep_omega"] = keep_omega_default(getattr(self.engine, "layout", "auto"))
         if not o["pdhg_beta_artificial"]:
