@@ -1,5 +1,5 @@
 """Parity at the bench's full sizes (BASELINE.json configs): farmer cm=10 x 10 000 scenarios
-(local kernel), sslp_15_45_10 x 2 048 and netdes x 1 024 (block kernel), hydro 3-stage tree x 20 000
+(local kernel) and its 1 250-scenario shard (the lone-wave build), sslp_15_45_10 x 2 048 and netdes x 1 024 (block kernel), hydro 3-stage tree x 20 000
 (shared-matrix MFMA kernel).
 
 The whole batch is too large for the oracle, so the checks are
@@ -31,6 +31,10 @@ CASES = {
     "farmer": (10000, lambda S: farmer.scenario_names_creator(S), farmer.scenario_creator,
                lambda S: {"crops_multiplier": 10, "num_scens": S},
                lambda nm, S: om.farmer(nm, crops_multiplier=10, num_scens=S), 8, "local"),
+    # the 10k instance's shard on one of 8 GPUs: 625 pair-waves on the SIMDs, the lone-wave build
+    "farmer1250": (1250, lambda S: farmer.scenario_names_creator(S), farmer.scenario_creator,
+                   lambda S: {"crops_multiplier": 10, "num_scens": S},
+                   lambda nm, S: om.farmer(nm, crops_multiplier=10, num_scens=S), 6, "local"),
     "sslp": (2048, lambda S: sslp.scenario_names_creator(S), sslp.scenario_creator, lambda S: {},
              lambda nm, S: om.sslp(nm), 3, "block"),
     "netdes": (1024, lambda S: netdes.scenario_names_creator(S), netdes.scenario_creator,
@@ -54,13 +58,15 @@ def _certificates(ph):
     assert gap.max() <= 1e-6, gap.max()
 
 
-@pytest.mark.parametrize("case", ["farmer", "sslp", "netdes"])
+@pytest.mark.parametrize("case", ["farmer", "farmer1250", "sslp", "netdes"])
 def test_full_size_properties_and_sampled_parity(case):
     S, pn, pc, pkw, ob, nsamp, layout = CASES[case]
     names = pn(S)
     ph = PH(_opts(), names, pc, scenario_creator_kwargs=pkw(S))
     ph.PH_Prep()
     assert ph.engine.layout == layout
+    if case == "farmer1250":
+        assert ph.engine.local_info()["lone"]   # one wave per SIMD (pdhg_local_lone)
     ph.Iter0()
     _certificates(ph)
     p = ph.engine.batch.prob
