@@ -2577,7 +2577,15 @@ static double* field_ptr(phg_handle* h, int f, size_t* count) {
 // a page-locked copy of `bytes` of host data, valid until the copies enqueued from it have run
 // (stage_done records that point): pageable uploads are staged and synchronised by the runtime, ~25 us
 // each; from pinned memory they are plain stream-ordered DMA
+// uploads above this size are not staged (no page-locked copy held per slot): they take the
+// synchronous pageable path, whose fixed cost is small beside the copy itself
+static constexpr size_t kStageMax = (size_t)16 << 20;
+
 static int stage_upload(phg_handle* h, const void* in, size_t bytes, const void** out) {
+    if (bytes > kStageMax) {
+        *out = in;
+        return 0;
+    }
     auto& st = h->up[h->up_next];
     if (st.ev) CK(hipEventSynchronize(st.ev));          // the slot's previous copies have run
     else CK(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
@@ -2594,7 +2602,11 @@ static int stage_upload(phg_handle* h, const void* in, size_t bytes, const void*
     return 0;
 }
 
-static int stage_done(phg_handle* h) {
+static int stage_done(phg_handle* h, size_t bytes) {
+    if (bytes > kStageMax) {   // the copies read the caller's memory: done before returning
+        CK(hipStreamSynchronize(h->stream));
+        return 0;
+    }
     CK(hipEventRecord(h->up[h->up_next].ev, h->stream));
     h->up_next = (h->up_next + 1) % 4;
     return 0;
@@ -2635,7 +2647,7 @@ int phg_set(phg_handle* h, int32_t f, const double* in) {
         if (shared) CK(hipMemcpyAsync(h->rho_k, staged, (size_t)h->N * sizeof(double), hipMemcpyHostToDevice, h->stream));
         h->ph.rho_k = shared ? h->rho_k : nullptr;
     }
-    return stage_done(h);
+    return stage_done(h, cnt * sizeof(double));
 }
 
 int phg_get(phg_handle* h, int32_t f, double* out) {
@@ -2676,6 +2688,16 @@ int phg_solve_results(phg_handle* h, int32_t* status, int32_t* iters, double* kk
     if (x && materialize_outputs(h)) return -1;
     const size_t S = (size_t)h->S, nx = (size_t)h->S * h->n;
     const size_t bytes = 2 * S * sizeof(int) + 3 * S * sizeof(double) + (x ? nx * sizeof(double) : 0) + 64;
+    if (bytes > kStageMax) {   // large batches: straight into the caller's arrays (no page-locked copy kept)
+        if (kkt) CK(hipMemcpyAsync(kkt, h->kkt, S * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        if (obj) CK(hipMemcpyAsync(obj, h->obj, S * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        if (bound) CK(hipMemcpyAsync(bound, h->bound, S * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        if (x) CK(hipMemcpyAsync(x, h->x_out, nx * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        if (status) CK(hipMemcpyAsync(status, h->status, S * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+        if (iters) CK(hipMemcpyAsync(iters, h->iters, S * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+        CK(hipStreamSynchronize(h->stream));
+        return 0;
+    }
     auto& st = h->down;
     if (st.cap < bytes) {
         if (st.p) CK(hipHostFree(st.p));
