@@ -359,6 +359,15 @@ def main():
                 traffic = tj.get("pdhg_bytes_per_launch")
         except Exception:
             traffic = None
+    valu_pmc = None
+    vpath = os.path.join(ROOT, "profiles", "r05", "pmc_valu_r05.json")
+    if args.case == "farmer" and eng.layout == "local" and S_loc == 10000 and os.path.exists(vpath):
+        try:
+            vj = json.load(open(vpath))
+            valu_pmc = {"valu_issue_utilisation": vj["valu_issue_utilisation"],
+                        "fp64_fma_share_of_valu": vj["fp64_fma_share_of_valu"], "file": "profiles/r05/pmc_valu_r05.json"}
+        except Exception:
+            valu_pmc = None
     # PH update, algorithmic bytes:
     #   8 S N (1 x read + 1 W read + 1 W write + [rho per scenario ? 1 : 0]) + 8 S + 16 N_tot
     # rho is read from an [N] copy when it is the same in every scenario (PhArgs::rho_k), as here
@@ -451,6 +460,9 @@ def main():
                       "nnz_distinct": nnz_distinct, "tflops_fp64": round(achieved_tf, 4),
                       "valu_frac_fp64": round(achieved_tf / FP64_PEAK_TFLOPS, 5)}) | {
                      "traffic": traffic,
+                     # VALU issue measured by PMC on the headline kernel (profiles/r05/pmc_valu_r05.json:
+                     # VALU instructions x 4 cycles / all SIMDs' cycles over the launch), when this is it
+                     "valu_issue_pmc": valu_pmc,
                      # measured HBM rate of the same kernel: PMC bytes per launch / launch duration
                      "hbm_measured_GBs": round(traffic / avg_launch_s / 1e9, 2) if traffic else None,
                      "hbm_measured_frac": round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5) if traffic else None,
