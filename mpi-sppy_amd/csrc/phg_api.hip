@@ -180,9 +180,11 @@ struct phg_handle {
     // check only (restarts / termination on the current iterate otherwise).  Farmer 10k A/B on the
     // box: 1 -> 26.7 M solves/s (272.7 PDHG iterations per solve), 3 -> 27.4 M, 6 -> 27.9 M
     // (283.6), never -> 28.1 M (283.2): the average's products are ~half of a check's work, and on
-    // these warm-started prox-QPs the current iterate restarts about as well.  6 keeps the average
-    // in reach of long (cold, LP) solves.
-    int avg_every = 6;
+    // these warm-started prox-QPs the current iterate restarts about as well.  Round 5 (farmer 10k,
+    // 4 A/B pairs): 12 -> 0.2834-0.2896 vs 0.2863-0.2939 ms per PH iteration at 6, time to conv
+    // 0.801-0.805 vs 0.821-0.829 s, the same 5 185 PH iterations and EF gaps (24: within noise of
+    // 6).  12 (every 384th PDHG iteration) keeps the average in reach of long (cold, LP) solves.
+    int avg_every = 12;
     // PHG_FUSE=1: phg_ph_step runs node sums + W update as ONE launch (ph_step_kernel) where the batch
     // allows.  Off by default: on farmer 10k the fused launch took 23.7 us against 18.4 us for the two
     // launches back to back (its last-K hand-offs cost more than the launch and the x re-read save),
