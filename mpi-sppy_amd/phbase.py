@@ -69,19 +69,25 @@ def keep_omega_default(layout):
     return False if layout == "mfma" else "blend"
 
 
-def beta_artificial_default(layout):
+def beta_artificial_default(layout, threads=0):
     """PDHG artificial-restart fraction by kernel layout (0: the library's 0.25), from round 5's
     sweeps on MI355X (`profiles/r05/betaart/`, `profiles/r05/uc/sweep/`):
     * bordered / range-split (UC 64, eps 1e-7): PDLP's 0.36 -- 477 vs 581 ms per PH iteration
       (0.5: 478, 0.6: 507, 0.8: 536);
     * workgroup block (sslp 4 096): 0.15 -- 5.24-5.26 vs 5.46-5.47 ms per PH iteration, 1 096 vs
       1 145 PDHG iterations per solve (0.1: 5.44, 0.2: 5.26, 0.36: 6.10); netdes within noise;
-    * wave gather (hydro 2 000): 0.15 -- 0.318 vs 0.325 ms (0.1: 0.315, 0.36: 0.353);
+    * wave gather (hydro 2 000): per iteration 0.15 -- 0.318 vs 0.325 ms (0.1: 0.315, 0.36: 0.353),
+      but see below;
     * lane-local (farmer 10k): the library's 0.25 (0.15: 0.2924, 0.2: 0.2897, 0.36: 0.3009 vs
       0.2885 ms).
     (The one-wave-per-scenario shared-matrix kernel, on request for block-kernel problems, follows
-    the block kernel.)"""
-    return {"border": 0.36, "stream": 0.36, "block": 0.15, "wave": 0.15, "gather": 0.15}.get(layout, 0.0)
+    the block kernel.)
+    Time to PH conv decides where the per-iteration gain does not carry over: the gather kernel's
+    0.15 made hydro 2 000's conv leg 0.141 vs 0.030 s over the same 105 PH iterations, and netdes'
+    1 024-thread block kernel converged in 37.3 vs 32.8 s -- both keep the library's 0.25."""
+    if layout == "block":
+        return 0.15 if 0 < threads <= 256 else 0.0
+    return {"border": 0.36, "stream": 0.36, "wave": 0.15}.get(layout, 0.0)
 
 
 class PHBase(SPBase):
@@ -185,7 +191,8 @@ class PHBase(SPBase):
         if o["pdhg_keep_omega"] is None:
             o["pdhg_keep_omega"] = keep_omega_default(getattr(self.engine, "layout", "auto"))
         if not o["pdhg_beta_artificial"]:
-            o["pdhg_beta_artificial"] = beta_artificial_default(getattr(self.engine, "layout", "auto"))
+            o["pdhg_beta_artificial"] = beta_artificial_default(getattr(self.engine, "layout", "auto"),
+                                                                getattr(self.engine, "lanes_per_scenario", 0))
         return o
 
     # ------------------------------------------------------------------------------- W / prox

@@ -14,11 +14,11 @@ def test_check_every_by_layout(layout, threads, want):
     assert check_every_default(layout, threads) == want
 
 
-@pytest.mark.parametrize("layout, want", [
-    ("local", 0.0), ("gather", 0.15), ("block", 0.15), ("wave", 0.15), ("border", 0.36), ("stream", 0.36),
-    ("mfma", 0.0)])
-def test_beta_artificial_by_layout(layout, want):
-    assert beta_artificial_default(layout) == want
+@pytest.mark.parametrize("layout, threads, want", [
+    ("local", 32, 0.0), ("gather", 64, 0.0), ("block", 256, 0.15), ("block", 1024, 0.0), ("wave", 64, 0.15),
+    ("border", 512, 0.36), ("stream", 1024, 0.36), ("mfma", 4, 0.0)])
+def test_beta_artificial_by_layout(layout, threads, want):
+    assert beta_artificial_default(layout, threads) == want
 
 
 @pytest.mark.parametrize("layout, want", [("mfma", False), ("local", "blend"), ("block", "blend"), ("border", "blend")])
