@@ -522,6 +522,24 @@ def main():
         "iter0_s": round(t_iter0, 4),
         "conv_at_end": conv,
     }
+    # who carried the exchange: the path, the collective's own rank count (RCCL's
+    # ncclCommCount for the library group), every rank's device / PCI bus id, and the per-iteration
+    # all-reduce of the packed buffer timed on the device (HIP events on the stream it runs on)
+    from mpisppy_amd.comm import SingleComm, rank_report
+    out["ranks"] = rank_report(comm if comm is not None else SingleComm(), device)
+    if comm is not None and eng.exchange is not None:
+        buf = torch.zeros_like(eng.exchange)
+        for _ in range(3):
+            comm.allreduce_sum_(buf)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n_ar = 50
+        e0.record()
+        for _ in range(n_ar):
+            comm.allreduce_sum_(buf)
+        e1.record()
+        torch.cuda.synchronize()
+        out["ranks"]["allreduce_us_device"] = round(e0.elapsed_time(e1) / n_ar * 1e3, 2)
+        out["ranks"]["allreduce_doubles"] = int(buf.numel())
     if rank == 0:
         print("[bench] timed region done", file=sys.stderr, flush=True)
     cpu_in = None

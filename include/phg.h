@@ -377,7 +377,7 @@ int  phg_exchange_buffers(phg_handle* h, double** dev_nodesum, double** dev_conv
  *     phg_node_sums(h, NULL); phg_ph_exchange(h, g); phg_ph_head(h, NULL, thr, first); phg_solve(...)
  *   phg_group_allreduce : in-place SUM of count doubles at dev_buf, on h's stream (h on g's device)
  *   phg_ph_exchange     : phg_group_allreduce of h's own packed exchange buffer
- *   phg_group_size      : out2 = {nranks, rank}                                                  */
+ *   phg_group_size      : out2 = {ncclCommCount, ncclCommUserRank} of the communicator          */
 typedef struct phg_group phg_group;
 int  phg_group_unique_id(uint8_t* out128);
 int  phg_create_group(int32_t nranks, int32_t rank, const uint8_t* id128, int32_t device, phg_group** out);

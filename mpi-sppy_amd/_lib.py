@@ -171,6 +171,13 @@ class PhgGroup:
         """In-place SUM of ``count`` doubles at device address ``dev_ptr``, on ``handle``'s stream."""
         check(self.lib.phg_group_allreduce(self.g, handle, C.c_void_p(int(dev_ptr)), C.c_int64(int(count))))
 
+    def size(self):
+        """(ranks, this rank) of the communicator as RCCL reports them (``phg_group_size``:
+        ``ncclCommCount``, ``ncclCommUserRank``)."""
+        n = np.zeros(2, np.int32)
+        check(self.lib.phg_group_size(self.g, ptr(n)))
+        return int(n[0]), int(n[1])
+
     def ph_exchange(self, handle):
         """All-reduce the handle's own packed exchange buffer (``phg_ph_exchange``)."""
         check(self.lib.phg_ph_exchange(handle, self.g))

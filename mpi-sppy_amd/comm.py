@@ -42,6 +42,10 @@ class SingleComm:
     def allgather_object(self, obj):
         return [obj]
 
+    def exchange_path(self):
+        """(what carries the per-iteration device exchange, ranks the collective library counts)"""
+        return "none (one rank: nothing to exchange)", None
+
 
 class TorchComm:
     """SUM all-reduces over an initialised ``torch.distributed`` process group."""
@@ -102,6 +106,13 @@ class TorchComm:
         out = [None] * self.size
         self.dist.all_gather_object(out, obj, group=self.group)
         return out
+
+    def exchange_path(self):
+        """(path, ranks): under nccl the device all-reduce is RCCL's, over the process group's ranks;
+        gloo stages through host memory (tests put several ranks on one device with it)."""
+        if self.backend == "nccl":
+            return "torch.distributed nccl (RCCL)", self.dist.get_world_size(self.group)
+        return f"torch.distributed {self.backend} (host-staged)", None
 
 
 def _device_count():
@@ -171,6 +182,14 @@ class PhgGroupComm:
     def close(self):
         self.group.close()
 
+    def exchange_path(self):
+        """(path, ranks): the ranks are RCCL's own count of the communicator (ncclCommCount through
+        phg_group_size), not the arguments it was created with."""
+        n, r = self.group.size()
+        if r != self.rank:
+            raise RuntimeError(f"libphg RCCL group: RCCL places this process at rank {r}, the host at {self.rank}")
+        return "libphg RCCL group (phg_group_allreduce)", n
+
     def __getattr__(self, name):   # host-side collectives (arrays, scalars, objects, barrier)
         return getattr(self.host, name)
 
@@ -196,3 +215,29 @@ def group_or_host(host, device, log=None):
         log(f"libphg RCCL group not created on {host.Get_size() - int(n_ok)} rank(s)"
             + (f" ({err})" if err is not None else "") + "; exchange through torch.distributed")
     return host
+
+
+def rank_report(comm, device=None):
+    """Evidence of who carried the multi-GPU exchange, for the bench line: the
+    exchange path and its collective's own rank count, and every rank's device and PCI bus id
+    (gathered through ``comm``; reference: the Allreduces of ``phbase.py:88-92, 369`` and their
+    communicator, ``spbase.py``'s ``mpicomm``)."""
+    me = {"rank": comm.Get_rank(), "device": device, "pci_bus_id": None, "device_name": None}
+    if device is not None:
+        try:
+            import torch
+            pr = torch.cuda.get_device_properties(device)
+            me["pci_bus_id"] = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+            me["device_name"] = pr.name
+        except Exception:
+            pass
+    try:
+        import socket
+        me["host"] = socket.gethostname()
+    except Exception:
+        me["host"] = None
+    ranks = comm.allgather_object(me) if comm.Get_size() > 1 else [me]
+    path, n = comm.exchange_path()
+    return {"world_size": comm.Get_size(), "exchange_path": path, "collective_ranks": n,
+            "distinct_devices": len({(r["host"], r["pci_bus_id"] or r["device"]) for r in ranks}),
+            "ranks": ranks}

@@ -3383,8 +3383,13 @@ int phg_create_group(int32_t nranks, int32_t rank, const uint8_t* id128, int32_t
 
 int phg_group_size(phg_group* g, int32_t* out2) {
     if (!g || !out2) return fail("phg_group_size: null argument");
-    out2[0] = g->nranks;
-    out2[1] = g->rank;
+    // RCCL's own view of the communicator (not the caller's arguments): a bench line that reports
+    // these proves the exchange ran over that many ranks
+    int cnt = 0, urank = -1;
+    NCK(ncclCommCount(g->comm, &cnt));
+    NCK(ncclCommUserRank(g->comm, &urank));
+    out2[0] = cnt;
+    out2[1] = urank;
     return 0;
 }
 
