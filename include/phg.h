@@ -322,8 +322,14 @@ int  phg_solve_undo(phg_handle* h);
  * following phg_node_sums(h, dev_packed); 0: off.  Only the lane-local layout with the folded
  * update, on a gated solve; otherwise the request is dropped and the separate launches run.
  * Replaces nothing in mpi-sppy by itself: it is the launch schedule of phbase.py:976-1030 on one
- * device.  PHG_TAIL=0 disables it.                                                                     */
+ * device.  The tail's sums are the separate launches' bit for bit (ph_tail.h: each node / conv
+ * segment reduced by the wave that completes it, the final reduction by the wave that completes the
+ * last segment; no wave waits on another).  PHG_TAIL=0 disables it.                                */
 int  phg_set_tail(phg_handle* h, int32_t mode, double convthresh, double* dev_packed);
+/* Diagnostic (synchronises): out4 = {tail units (node + conv segments), final-reduction slots,
+ * unit / done counters not at zero (0 between launches: each is re-armed by the wave that
+ * completes it), the mode of the last solve's tail (0: none)}                                    */
+int  phg_tail_info(phg_handle* h, int32_t* out4);
 /* New column bounds of the loaded batch ([S*n] each, the caller's units; +-inf allowed) without a
  * reload: intersected again with the rows the presolve folded into bounds, scaled on the device,
  * the lane-local kernel re-picked for the new bound sides and its lane image rebuilt; the safe-bound

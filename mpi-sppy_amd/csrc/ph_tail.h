@@ -4,28 +4,32 @@
 // the node sums of its x (_Compute_Xbar, mpisppy/phbase.py:32-112) and, on one GPU, by the x-bar
 // head (the convergence metric of update k from the folded W update's per-scenario partials,
 // phbase.py:349-371, the gate of solve k+1 and x-bar of iteration k+1).  Launched as a kernel of its
-// own that work costs a dependent-kernel boundary and a launch ramp (~25 us between two solves on
-// farmer 10k, ~16 us of it the node-sum kernel).  Here it runs at the END of the solve's own launch:
-// each wave, once it has no work left, drains its stores and adds to a counter; the LAST T waves to
-// arrive (tail ranks, as node_sums_kernel's last-K workgroups: every other wave has finished, so the
-// few still running are all resident) wait for the count to reach the grid, then
-//   1. node-sum partials of the node segments and the folded update's conv-segment partials
-//      (tail rank t takes segments t, t + T, ...), published write-through;
-//   2. the last R of them to arrive wait for all T, then each forms the
-//      convergence partials (the same fixed-order sums in every rank), adds its slice of the
-//      node sums in segment order into the packed buffer, and -- one GPU -- writes the next x-bar
-//      into a staging buffer (the current x-bar where conv < convthresh: the reference's break
-//      before Update_W, phbase.py:1008-1010) that phg_ph_step commits; rank 0 publishes the gate.
-// Hand-offs as in node_sums_kernel (MI355X_MICROARCH.md, inter-workgroup visibility): every
-// handed-off store is an sc1 (write-through) store drained by s_waitcnt vmcnt(0) before the counter
-// add; the consumer polls the counter, takes ONE agent-scope acquire, then reads with plain loads
-// (batched: a first version read with sc1 atomic loads, which the compiler issued one at a time --
-// +54 us per launch on farmer 10k).  All spins are bounded (a give-up sets an error word and the
-// wave leaves; the grid always drains).  The sums are deterministic
-// (fixed orders); their association differs from node_sums_kernel's, so a pipelined trajectory
-// with the tail agrees with the statement-by-statement one to rounding, not bit for bit.
+// own that work costs a dependent-kernel boundary and a launch ramp.  Here it runs at the end of the
+// solve's own launch, as a chain of "last arrival does the work" hand-offs -- no wave ever waits for
+// another:
+//   1. every wave, after its epilogue (its x stores write-through, drained), counts its scenarios
+//      into their node segments (one counter per segment and tree level, PhArgs::seg) and their
+//      convergence segments (PhArgs::cseg_*);
+//   2. the wave that completes a segment computes the segment's partial sums -- exactly what
+//      node_sums_kernel's 256-thread workgroup computes for it (the same per-thread sums of
+//      ph_sums.h, the four 64-lane quarters of that workgroup run by one wave) -- or the conv
+//      segment's sum |x - x-bar| and status counts (fold_conv_segment's), publishes them
+//      write-through and counts one finished unit;
+//   3. the wave that finishes the last unit runs the final reduction: every node sum in
+//      node_sum_final's order (a host-built slot plan, TailArgs::fin, puts each element's T
+//      strided partial sums in T aligned lanes), the convergence partials (conv_partials_final's
+//      order) and -- one GPU -- the convergence metric (conv_value_block's tree), the gate and the
+//      next x-bar into a staging buffer (the current x-bar where conv < convthresh: the reference's
+//      break before Update_W, phbase.py:1008-1010), which phg_ph_step commits.
+// Every sum is associated as in the separate launches, so the results are the separate launches'
+// bit for bit.  Hand-offs as in node_sums_kernel (MI355X_MICROARCH.md, inter-workgroup
+// visibility): handed-off stores are sc1 (write-through), drained by s_waitcnt vmcnt(0) before the
+// counter add; the consumer takes ONE agent-scope acquire, then plain loads.  Each counter is
+// re-zeroed by the wave that completes it (every add of this launch has happened by then), so the
+// next stream-ordered launch starts from zero; no wave spins, so no wave can give up.
 #pragma once
 #include "phg_internal.h"
+#include "ph_sums.h"
 #include "wave_ops.h"
 
 namespace phg {
@@ -37,7 +41,8 @@ __device__ __forceinline__ void st_sc1(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one wave's butterfly sum (every lane the same bits)
+// one wave's butterfly sum, xor 32 ... 1 (the per-wave step of the 256-thread reductions; every
+// lane the same bits)
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -49,267 +54,246 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// lane 0 waits until *cnt >= target (bounded: ~2^22 polls of ~64 cycles each, seconds); false on
-// a give-up, which also sets the error word
-__device__ __forceinline__ bool tail_wait(unsigned* cnt, unsigned target, unsigned* err) {
-    int ok = 1;
-    if (threadIdx.x == 0) {
-        unsigned spins = 0;
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (++spins > (1u << 22)) {
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (ok) {   // agent-scope acquire: this CU's L1 holds no stale copy of the handed-off bytes
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    return __shfl(ok, 0, 64) != 0;
+__device__ __forceinline__ void tail_acquire() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// the whole tail, run at the end of every wave of the grid (one 64-lane wave per workgroup) after
-// its last epilogue; lds: >= 128 doubles of the wave's dynamic LDS (its cold state is dead by now)
-__device__ __forceinline__ void ph_tail_end(const TailArgs& tl, double* lds) {
+// ---------------------------------------------------------------------------- 2. node segment
+// node_sum_partials (ph_update.hip) of segment g by one wave: virtual thread tid = lane + 64 p of
+// the workgroup in quarter p.  RMAX: rows per virtual thread up to which every load of the four
+// quarters is issued at once (farmer: a 64-scenario segment is <= 4 rows per thread); beyond it the
+// quarters run one after another through the workgroup's own loops.
+template <int RMAX>
+__device__ void tail_seg_partial(const PhArgs& a, int g, double* sh, bool generic) {
     const int lane = threadIdx.x;
-    const PhArgs& p = tl.ph;
-    unsigned* cnt = tl.cnt;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are out
-    int t = -1;
-    // PHG_TAIL_PROF stamps (100 MHz): [0] the last wave's arrival, [1] rank 0 past the wait,
-    // [2] rank 0 done with its partials, [3] final rank 0 past the second wait, [4] its stores done
-    auto stamp = [&](int i) {
-        if (tl.prof && lane == 0) tl.prof[i] = __builtin_amdgcn_s_memrealtime();
-    };
-    if (lane == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(cnt + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        t = (int)prev - (tl.W - tl.T);
-        if (tl.prof && prev == (unsigned)tl.W - 1) tl.prof[0] = __builtin_amdgcn_s_memrealtime();
-    }
-    t = __shfl(t, 0, 64);
-    if (t < 0) return;
-    if (!tail_wait(cnt + 0, (unsigned)tl.W, cnt + 3)) return;
-    if (t == 0) stamp(1);
-    // ---------------------------------------------------------------- 1. partials
-    // this rank's conv segment (one per rank when n_cseg <= T and a segment has <= 128 scenarios:
-    // its loads issued now, with the node segment's, and reduced after -- one round trip for both)
-    const bool cpre = p.n_cseg <= tl.T && (t >= p.n_cseg || p.cseg_s1[t] - p.cseg_s0[t] <= 128);
-    double cv[2] = {0.0, 0.0};
-    int cst[2] = {0, 0};
-    if (cpre && t < p.n_cseg) {
-        const int s0 = p.cseg_s0[t], s1 = p.cseg_s1[t];
+    const NodeSeg sg = a.seg[g];
+    double* out = a.segpart + (long)g * 2 * a.maxk;
+    const bool pairs = nsum_pairs(a, sg);
+    const int len = sg.s1 - sg.s0;
+    for (int k0 = 0; k0 < sg.klen; k0 += 256) {
+        NsumThread th[4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int s = s0 + lane + 64 * h;
-            const int sc = s < s1 ? s : s0;
-            cv[h] = p.conv_s[sc];
-            cst[h] = p.fold_st[sc];
-            if (!(s < s1)) { cv[h] = 0.0; cst[h] = 0; }
-        }
-    }
-    for (int g = t; g < p.n_seg; g += tl.T) {
-        const NodeSeg sg = p.seg[g];
-        double* out = p.segpart + (long)g * 2 * p.maxk;
-        for (int k0 = 0; k0 < sg.klen; k0 += 64) {
-            const int kl = min(64, sg.klen - k0);
-            const int q = 64 / kl;                 // lanes per element
-            const int k = lane % kl, so = lane / kl;
-            double s1 = 0.0, s2 = 0.0;
-            if (so < q) {
-                const long kg = sg.kofs + k0 + k;
-                // 32 rows per lane in flight (a farmer segment, 64 scenarios x 2 lanes per element,
-                // in ONE round trip), accumulated into 8 sums by row mod 8 (fixed pairing)
-                constexpr int RB = 32, R = 8;
-                double t1[R], t2[R];
+        for (int p = 0; p < 4; ++p) th[p] = nsum_thread(pairs, sg.klen, k0, len, lane + 64 * p);
+        const int kl = th[0].kl, q = th[0].q;
+        if (!generic && len <= RMAX * q && pairs) {
+            double2 xv[4][RMAX];
+            double pr[4][RMAX];
 #pragma unroll
-                for (int u = 0; u < R; ++u) t1[u] = t2[u] = 0.0;
-                int s = sg.s0 + so;
-                for (; s < sg.s1; s += RB * q) {
-                    double xv[RB], pr[RB];
+            for (int p = 0; p < 4; ++p)
 #pragma unroll
-                    for (int u = 0; u < RB; ++u) {   // (rows past the segment: a valid row, weight 0)
-                        const int su = s + u * q;
-                        const int sc = su < sg.s1 ? su : sg.s0;
-                        xv[u] = p.xN[(long)sc * p.N + kg];
-                        pr[u] = p.pcv ? p.pcv[(long)sc * p.N + kg] : p.pc[(long)sc * p.L + sg.level];
-                        pr[u] = su < sg.s1 ? pr[u] : 0.0;
-                    }
+                for (int i = 0; i < RMAX; ++i) {
+                    const int s = sg.s0 + th[p].so + i * q;
+                    const int sc = i < th[p].nr ? s : sg.s0;   // (rows past the thread's: a valid row, unused)
+                    xv[p][i] = *reinterpret_cast<const double2*>(a.xN + (long)sc * a.N + sg.kofs + k0 + 2 * th[p].kk);
+                    pr[p][i] = a.pc[(long)sc * a.L + sg.level];
+                }
 #pragma unroll
-                    for (int u = 0; u < RB; ++u) {
-                        const double px = pr[u] * xv[u];
-                        t1[u % R] += px;
-                        t2[u % R] = fma(px, xv[u], t2[u % R]);
+            for (int p = 0; p < 4; ++p) {
+                double ta[8], tb[8], ua[8], ub[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) ta[u] = tb[u] = ua[u] = ub[u] = 0.0;
+#pragma unroll
+                for (int i = 0; i < RMAX; ++i) {
+                    if (i < th[p].nr) {
+                        if (i < 8 * th[p].nfull) {   // a full block of eight: accumulator i mod 8
+                            nsum_add(ta[i & 7], ua[i & 7], pr[p][i], xv[p][i].x);
+                            nsum_add(tb[i & 7], ub[i & 7], pr[p][i], xv[p][i].y);
+                        } else {                     // the remainder: accumulator 0
+                            nsum_add(ta[0], ua[0], pr[p][i], xv[p][i].x);
+                            nsum_add(tb[0], ub[0], pr[p][i], xv[p][i].y);
+                        }
                     }
                 }
-                s1 = ((t1[0] + t1[1]) + (t1[2] + t1[3])) + ((t1[4] + t1[5]) + (t1[6] + t1[7]));
-                s2 = ((t2[0] + t2[1]) + (t2[2] + t2[3])) + ((t2[4] + t2[5]) + (t2[6] + t2[7]));
+                const double r[4] = {nsum_tree8(ta), nsum_tree8(tb), nsum_tree8(ua), nsum_tree8(ub)};
+                nsum_stage(sh, th[p], true, r);
             }
-            lds[lane] = s1;
-            lds[64 + lane] = s2;
-            __syncthreads();   // (a one-wave workgroup: orders the LDS stores before the loads)
-            if (lane < kl) {
-                double a1 = 0.0, a2 = 0.0;
-                for (int j = 0; j < q; ++j) { a1 += lds[j * kl + lane]; a2 += lds[64 + j * kl + lane]; }
-                st_sc1(&out[k0 + lane], a1);
-                st_sc1(&out[p.maxk + k0 + lane], a2);
-            }
-            __syncthreads();
-        }
-    }
-    // the folded update's conv segments: sum |x - xbar| and the status counts of its solve
-    if (cpre && t < p.n_cseg) {   // (the order of the loop below: lane-strided, then the butterfly)
-        const double acc = wave_sum(cv[0] + cv[1]);
-        const int nb = wave_sum((int)(cst[0] != 0) + (int)(cst[1] != 0));
-        const int nn = wave_sum((int)(cst[0] == 2) + (int)(cst[1] == 2));
-        if (lane == 0) {
-            st_sc1(&p.csegpart[t], acc);
-            st_sc1(&p.csegbad[2 * t], nb);
-            st_sc1(&p.csegbad[2 * t + 1], nn);
-        }
-    }
-    for (int b = t; !cpre && b < p.n_cseg; b += tl.T) {
-        const int s0 = p.cseg_s0[b], s1 = p.cseg_s1[b];
-        double acc = 0.0;
-        int nb = 0, nn = 0;
-        for (int s = s0 + lane; s < s1; s += 64) {
-            acc += p.conv_s[s];
-            const int st = p.fold_st[s];
-            nb += st != 0;
-            nn += st == 2;
-        }
-        acc = wave_sum(acc);
-        nb = wave_sum(nb);
-        nn = wave_sum(nn);
-        if (lane == 0) {
-            st_sc1(&p.csegpart[b], acc);
-            st_sc1(&p.csegbad[2 * b], nb);
-            st_sc1(&p.csegbad[2 * b + 1], nn);
-        }
-    }
-    // ---------------------------------------------------------------- arrival, ranks
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (t == 0) stamp(2);
-    int rank = -1;
-    if (lane == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rank = (int)prev - (tl.T - tl.R);
-    }
-    rank = __shfl(rank, 0, 64);
-    if (rank < 0) return;
-    if (!tail_wait(cnt + 1, (unsigned)tl.T, cnt + 3)) return;
-    if (rank == 0) stamp(3);
-    // ---------------------------------------------------------------- 2. final (rank of R)
-    double* cp = tl.out + 2 * (long)p.N_tot;
-    // this rank's slice of the node sums: TL lanes per element, each adding every TL-th segment of
-    // the element's node, then a fixed butterfly
-    const int e_lo = (int)((long)p.N_tot * rank / tl.R), e_hi = (int)((long)p.N_tot * (rank + 1) / tl.R);
-    const int ne = e_hi - e_lo;
-    int TL = 1;
-    while (TL < 64 && TL * 2 * ne <= 64) TL *= 2;
-    const int E = 64 / TL;
-    const int sub = lane % TL;
-    auto node_sum = [&](int e, double& a1, double& a2) {
-        a1 = a2 = 0.0;
-        if (e < e_hi) {
-            int lo = 0, hi = p.n_nodes - 1;   // node g with node_off[g] <= e
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (p.node_off[mid] <= e) lo = mid; else hi = mid - 1;
-            }
-            const int i = e - p.node_off[lo];
-#pragma unroll 8
-            for (int g = p.node_first_seg[lo] + sub; g < p.node_first_seg[lo + 1]; g += TL) {
-                a1 += p.segpart[(long)g * 2 * p.maxk + i];
-                a2 += p.segpart[(long)g * 2 * p.maxk + p.maxk + i];
+        } else {
+            for (int p = 0; p < 4; ++p) {   // (the plan recomputed: no dynamically indexed local array)
+                const NsumThread tp = nsum_thread(pairs, sg.klen, k0, len, lane + 64 * p);
+                double r[4];
+                nsum_thread_sums<false>(a, sg, k0, tp, pairs, r);
+                nsum_stage(sh, tp, pairs, r);
             }
         }
-        for (int o = 1; o < TL; o <<= 1) {
-            a1 += __shfl_xor(a1, o, 64);
-            a2 += __shfl_xor(a2, o, 64);
-        }
-    };
-    // one virtual rank and <= 128 conv segments (the usual case): their partials loaded first, then
-    // this rank's node sums (one pass when its slice fits), both in flight together
-    const bool fastc = p.P == 1 && p.n_cseg <= 128;
-    const bool one_pass = ne <= E;
-    double cA[2] = {0.0, 0.0};
-    int bA[4] = {0, 0, 0, 0};
-    if (fastc) {
+        __syncthreads();   // (a one-wave workgroup: orders the LDS stores before the loads)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int g = lane + 64 * h;
-            const int gc = g < p.n_cseg ? g : 0;
-            cA[h] = p.csegpart[gc];
-            bA[2 * h] = p.csegbad[2 * gc];
-            bA[2 * h + 1] = p.csegbad[2 * gc + 1];
-            if (!(g < p.n_cseg)) { cA[h] = 0.0; bA[2 * h] = bA[2 * h + 1] = 0; }
+        for (int p = 0; p < 4; ++p) {
+            const int tid = lane + 64 * p;
+            if (tid < kl) {
+                double t1 = 0.0, t2 = 0.0;
+                for (int j = 0; j < q; ++j) { t1 += sh[j * kl + tid]; t2 += sh[512 + j * kl + tid]; }
+                st_sc1(&out[k0 + tid], t1);
+                st_sc1(&out[a.maxk + k0 + tid], t2);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------- 2'. conv segment
+// fold_conv_segment (ph_update.hip) of conv segment b by one wave: the sum of the folded update's
+// per-scenario |x - x-bar| (lane-strided over the 256 virtual threads, a butterfly per quarter, the
+// four quarters in order) and the solve-status counts
+__device__ void tail_cseg_partial(const PhArgs& a, int b) {
+    const int lane = threadIdx.x;
+    const int s0 = a.cseg_s0[b], s1 = a.cseg_s1[b];
+    double r[4];
+    int nb = 0, nn = 0;
+    if (s1 - s0 <= 256) {   // one scenario per virtual thread: every load at once
+        double v[4];
+        int st[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int s = s0 + lane + 64 * p;
+            const int sc = s < s1 ? s : s0;
+            v[p] = a.conv_s[sc];
+            st[p] = a.fold_st[sc];
+            if (!(s < s1)) { v[p] = 0.0; st[p] = 0; }
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            r[p] = wave_sum(0.0 + v[p]);
+            nb += st[p] != 0;
+            nn += st[p] == 2;
+        }
+    } else {
+        for (int p = 0; p < 4; ++p) {
+            double acc = 0.0;
+            for (int s = s0 + lane + 64 * p; s < s1; s += 256) {
+                acc += a.conv_s[s];
+                const int st = a.fold_st[s];
+                nb += st != 0;
+                nn += st == 2;
+            }
+            r[p] = wave_sum(acc);
         }
     }
-    double f1 = 0.0, f2 = 0.0;
-    if (one_pass) node_sum(e_lo + lane / TL, f1, f2);
-    // convergence partials: per virtual rank v (sum |x - xbar|, count) in fixed order; the status
-    // counts; the flag -- the same sums in every rank
-    double conv = 0.0;
+    nb = wave_sum(nb);
+    nn = wave_sum(nn);
+    if (lane == 0) {
+        st_sc1(&a.csegpart[b], ((r[0] + r[1]) + r[2]) + r[3]);
+        st_sc1(&a.csegbad[2 * b], nb);
+        st_sc1(&a.csegbad[2 * b + 1], nn);
+    }
+}
+
+// ---------------------------------------------------------------------------- 3. final
+// node_sum_final's sums: fin slot v = lane + 64 p holds {element e, first segment, terms J, stride T,
+// position i of e in its node} (e < 0: empty); the slot adds its J strided segment partials in order,
+// then the xor butterfly over its T aligned lanes (o < T) gives node_sum_final's bits in the
+// element's first lane
+constexpr int kTailJ = 12;   // strided terms loaded at once per slot (more: a second pass)
+
+__device__ __forceinline__ void tail_fin_slot(const PhArgs& a, const int* fin, int v, double& t1, double& t2, int& e,
+                                              int& T) {
+    const int* f = fin + 5 * v;
+    e = f[0];
+    const int g0 = f[1], J = f[2], i = f[4];
+    T = f[3];
+    t1 = t2 = 0.0;
+    if (e < 0) return;
+    double v1[kTailJ], v2[kTailJ];
+#pragma unroll
+    for (int j = 0; j < kTailJ; ++j) {
+        const long gj = (long)(j < J ? g0 + j * T : g0) * 2 * a.maxk;
+        v1[j] = a.segpart[gj + i];
+        v2[j] = a.segpart[gj + a.maxk + i];
+    }
+#pragma unroll
+    for (int j = 0; j < kTailJ; ++j)
+        if (j < J) { t1 += v1[j]; t2 += v2[j]; }
+    for (int j = kTailJ; j < J; ++j) {
+        const long gj = (long)(g0 + j * T) * 2 * a.maxk;
+        t1 += a.segpart[gj + i];
+        t2 += a.segpart[gj + a.maxk + i];
+    }
+}
+
+__device__ void tail_final(const TailArgs& tl, double* lds) {
+    const int lane = threadIdx.x;
+    const PhArgs& p = tl.ph;
+    double* cp = tl.out + 2 * (long)p.N_tot;
+    // -- convergence partials (conv_partials_final): per virtual rank v, block_sum_range over its conv
+    // segments -- a lane-strided sum per virtual thread, a butterfly per quarter, the quarters in
+    // order; each rank's ratio sum / count kept in lds[256 + v] for the metric (P <= 512, host-checked)
     int tb = 0, tn = 0;
     for (int v = 0; v < p.P; ++v) {
         const int g0 = p.vr_first[v], g1 = p.vr_first[v + 1];
-        double sv = 0.0;
-        if (fastc) sv = cA[0] + cA[1];
-        else
-            for (int g = g0 + lane; g < g1; g += 64) sv += p.csegpart[g];
-        sv = wave_sum(sv);
-        const double c = g1 > g0 ? (double)(p.cseg_s1[g1 - 1] - p.cseg_s0[g0]) * (double)p.N : 0.0;
-        if (c > 0.0) conv += sv / c;
-        if (rank == 0 && lane == 0) {
-            cp[2 * v] = sv;
-            cp[2 * v + 1] = c;
+        double r[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double t = 0.0;
+            for (int g = g0 + lane + 64 * q; g < g1; g += 256) t += p.csegpart[g];
+            r[q] = wave_sum(t);
+        }
+        const double sum = ((r[0] + r[1]) + r[2]) + r[3];
+        const double cnt = g1 > g0 ? (double)(p.cseg_s1[g1 - 1] - p.cseg_s0[g0]) * (double)p.N : 0.0;
+        if (lane == 0) {
+            cp[2 * v] = sum;
+            cp[2 * v + 1] = cnt;
+            lds[256 + v] = cnt > 0.0 ? sum / cnt : 0.0;   // (a rank without nonants adds nothing)
         }
     }
-    if (fastc) {
-        tb = bA[0] + bA[2];
-        tn = bA[1] + bA[3];
-    } else {
-        for (int g = lane; g < p.n_cseg; g += 64) {
-            tb += p.csegbad[2 * g];
-            tn += p.csegbad[2 * g + 1];
-        }
-    }
+    for (int g = lane; g < p.n_cseg; g += 64) { tb += p.csegbad[2 * g]; tn += p.csegbad[2 * g + 1]; }
     tb = wave_sum(tb);
     tn = wave_sum(tn);
-    conv /= (double)p.P;
-    if (rank == 0 && lane == 0) {
+    if (lane == 0) {
         cp[2 * p.P] = (double)tb;
         cp[2 * p.P + 1] = (double)tn;
         cp[2 * p.P + 2] = 1.0;   // the partials are a W update's
     }
+    double conv = INFINITY;
+    if (tl.mode == 1) {
+        // conv_value_block: virtual thread t adds the ratios of ranks t, t + 256, ...; then the
+        // halving tree red[t] += red[t + w], w = 128 ... 1
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int t = lane + 64 * q;
+            double acc = 0.0;
+            for (int v = t; v < p.P; v += 256) acc += lds[256 + v];
+            lds[t] = acc;
+        }
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            for (int t = lane; t < w; t += 64) lds[t] += lds[t + w];
+            __syncthreads();
+        }
+        conv = lds[0] / (double)p.P;
+        __syncthreads();
+    }
     const bool keep = tl.mode == 1 && !(conv >= tl.thr);   // below convthresh: x-bar stays
-    auto put = [&](int e, double a1, double a2) {
-        if (e < e_hi && sub == 0) {
-            tl.out[e] = a1;
-            tl.out[p.N_tot + e] = a2;
-            if (tl.mode == 1) {
-                tl.xbar_next[e] = keep ? tl.xbar_cur[e] : a1;
-                tl.xbar_next[p.N_tot + e] = keep ? tl.xbar_cur[p.N_tot + e] : a2;
+    // -- node sums (node_sum_final's order), two slot quarters in flight at a time
+    for (int v0 = 0; v0 < tl.n_fin; v0 += 128) {
+        double t1[2], t2[2];
+        int e[2], T[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int v = v0 + 64 * h + lane;
+            if (v < tl.n_fin) tail_fin_slot(p, tl.fin, v, t1[h], t2[h], e[h], T[h]);
+            else { t1[h] = t2[h] = 0.0; e[h] = -1; T[h] = 1; }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const double u1 = __shfl_xor(t1[h], o, 64), u2 = __shfl_xor(t2[h], o, 64);
+                if (o < T[h]) { t1[h] += u1; t2[h] += u2; }
+            }
+            const int v = v0 + 64 * h + lane;
+            if (e[h] >= 0 && (v % T[h]) == 0) {
+                tl.out[e[h]] = t1[h];
+                tl.out[p.N_tot + e[h]] = t2[h];
+                if (tl.mode == 1) {
+                    tl.xbar_next[e[h]] = keep ? tl.xbar_cur[e[h]] : t1[h];
+                    tl.xbar_next[p.N_tot + e[h]] = keep ? tl.xbar_cur[p.N_tot + e[h]] : t2[h];
+                }
             }
         }
-    };
-    if (one_pass) {
-        put(e_lo + lane / TL, f1, f2);
-    } else {
-        for (int e0 = e_lo; e0 < e_hi; e0 += E) {
-            node_sum(e0 + lane / TL, f1, f2);
-            put(e0 + lane / TL, f1, f2);
-        }
     }
-    if (tl.prof && rank == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        stamp(4);
-    }
-    // ---------------------------------------------------------------- gate (one GPU), re-arm
-    if (tl.mode == 1 && rank == 0 && lane == 0) {
+    // -- the gate (one GPU): device copy for the next gated launch, pinned host ring for the host
+    if (tl.mode == 1 && lane == 0) {
         tl.gate[0] = conv;
         tl.gate[1] = (double)tb;
         tl.gate[2] = (double)tn;
@@ -320,12 +304,71 @@ __device__ __forceinline__ void ph_tail_end(const TailArgs& tl, double* lds) {
         __threadfence_system();
         __hip_atomic_store(&gh[3], tl.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (lane == 0 &&
-        __hip_atomic_fetch_add(cnt + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)tl.R - 1) {
-        // every rank is past both waits: re-arm for the next (stream-ordered) launch
-        __hip_atomic_store(cnt + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cnt + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------- the tail
+// run by every wave of the grid after its last epilogue; its G groups held scenarios scen[q] (-1:
+// none).  lds: the wave's dynamic LDS (its cold state is dead by now; >= 1 024 doubles)
+template <int G>
+__device__ __forceinline__ void ph_tail_end(const TailArgs& tl, const int (&scen)[G], double* lds) {
+    const int lane = threadIdx.x;
+    const PhArgs& p = tl.ph;
+    constexpr int LPS = 64 / G;
+    const int grp = lane / LPS;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through stores are out
+    const unsigned long long t_arrive = tl.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    // 1. count this wave's scenarios into their units: lane grp * LPS + l counts group grp's scenario
+    //    into its level-l node segment (l < L) or, at l = L, its conv segment
+    int unit = -1;    // the unit this lane completed: node segment g, or n_seg + conv segment b
+    {
+        int s = -1;
+#pragma unroll
+        for (int q = 0; q < G; ++q) s = grp == q ? scen[q] : s;
+        const int l = lane % LPS;
+        if (s >= 0 && l <= p.L) {
+            const bool cs = l == p.L;
+            const int u = cs ? tl.scen_cseg[s] : tl.scen_seg[(long)s * p.L + l];
+            unsigned* c = cs ? tl.csegcnt + u : tl.segcnt + u;
+            const int size = cs ? p.cseg_s1[u] - p.cseg_s0[u] : p.seg[u].s1 - p.seg[u].s0;
+            const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (prev + 1u == (unsigned)size) {
+                unit = cs ? p.n_seg + u : u;
+                __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed
+            }
+        }
+    }
+    unsigned long long done = __ballot(unit >= 0);
+    if (!done) return;
+    // 2. this wave completed units: their producers' stores are visible after one acquire
+    tail_acquire();
+    int n_units = 0;
+    while (done) {
+        const int src = __builtin_ctzll(done);
+        done &= done - 1ull;
+        const int u = __shfl(unit, src, 64);
+        if (u < p.n_seg) tail_seg_partial<4>(p, u, lds, tl.generic != 0);
+        else tail_cseg_partial(p, u - p.n_seg);
+        ++n_units;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the partials are out
+    int last = 0;
+    if (lane == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(tl.done, (unsigned)n_units, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev + (unsigned)n_units == (unsigned)(p.n_seg + p.n_cseg);
+        if (last) __hip_atomic_store(tl.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed
+    }
+    if (!__shfl(last, 0, 64)) return;
+    // 3. every unit is in: the final reduction
+    tail_acquire();
+    const unsigned long long t_final = tl.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    tail_final(tl, lds);
+    if (tl.prof) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            tl.prof[0] = t_arrive;
+            tl.prof[1] = t_final;
+            tl.prof[2] = __builtin_amdgcn_s_memrealtime();
+        }
     }
 }
 

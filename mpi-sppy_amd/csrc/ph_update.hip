@@ -14,6 +14,7 @@
 #include <type_traits>
 
 #include "phg_internal.h"
+#include "ph_sums.h"
 
 namespace phg {
 
@@ -146,127 +147,17 @@ __device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
     // element pairs with 16-byte loads when every row's slice starts 16-byte aligned (even N,
     // offset and length) and the probability is per node: thread (k2, so) adds nonants 2 k2, 2 k2 + 1
     // of rows s0 + so + j q2 (eight rows in flight), then the q2 row lanes are added in order
-    const bool pairs = (a.N % 2 == 0) && (sg.kofs % 2 == 0) && (sg.klen % 2 == 0) && !a.pcv;
-    for (int k0 = 256 * (int)blockIdx.y; pairs && k0 < sg.klen; k0 += 256 * (int)gridDim.y) {
-        const int kl = min(256, sg.klen - k0), kl2 = kl / 2;
-        const int q2 = 256 / kl2;
-        const int k2 = tid % kl2, so = tid / kl2;
-        double s1a = 0.0, s1b = 0.0, s2a = 0.0, s2b = 0.0;
-        if (so < q2) {
-            const long kg = sg.kofs + k0 + 2 * k2;
-            auto ld = [&](int s) {
-                const double2* p = reinterpret_cast<const double2*>(a.xN + (long)s * a.N + kg);
-                if constexpr (NTL) {   // (x is read once here)
-                    typedef double d2v __attribute__((ext_vector_type(2)));
-                    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
-                    return double2(v.x, v.y);
-                } else {
-                    return *p;
-                }
-            };
-            auto pr = [&](int s) { return a.pc[(long)s * a.L + sg.level]; };
-            int s = sg.s0 + so;
-            constexpr int R = 8;
-            double ta[R], tb[R], ua[R], ub[R];
-#pragma unroll
-            for (int u = 0; u < R; ++u) ta[u] = tb[u] = ua[u] = ub[u] = 0.0;
-            for (; s + (R - 1) * q2 < sg.s1; s += R * q2) {
-                double2 xv[R];
-                double p[R];
-#pragma unroll
-                for (int u = 0; u < R; ++u) { xv[u] = ld(s + u * q2); p[u] = pr(s + u * q2); }
-#pragma unroll
-                for (int u = 0; u < R; ++u) {
-                    ta[u] += p[u] * xv[u].x;
-                    tb[u] += p[u] * xv[u].y;
-                    ua[u] += p[u] * xv[u].x * xv[u].x;
-                    ub[u] += p[u] * xv[u].y * xv[u].y;
-                }
-            }
-            // the remainder (fewer than R rows of this lane): every load issued first, then the rows
-            // added in order into accumulator 0 (the same order, the same bits as one row at a time;
-            // small batches are all remainder: one round trip instead of one per row)
-            {
-                double2 xv[R];
-                double p[R];
-#pragma unroll
-                for (int u = 0; u < R; ++u)
-                    if (s + u * q2 < sg.s1) { xv[u] = ld(s + u * q2); p[u] = pr(s + u * q2); }
-#pragma unroll
-                for (int u = 0; u < R; ++u)
-                    if (s + u * q2 < sg.s1) {
-                        ta[0] += p[u] * xv[u].x;
-                        tb[0] += p[u] * xv[u].y;
-                        ua[0] += p[u] * xv[u].x * xv[u].x;
-                        ub[0] += p[u] * xv[u].y * xv[u].y;
-                    }
-            }
-            s1a = ((ta[0] + ta[1]) + (ta[2] + ta[3])) + ((ta[4] + ta[5]) + (ta[6] + ta[7]));
-            s1b = ((tb[0] + tb[1]) + (tb[2] + tb[3])) + ((tb[4] + tb[5]) + (tb[6] + tb[7]));
-            s2a = ((ua[0] + ua[1]) + (ua[2] + ua[3])) + ((ua[4] + ua[5]) + (ua[6] + ua[7]));
-            s2b = ((ub[0] + ub[1]) + (ub[2] + ub[3])) + ((ub[4] + ub[5]) + (ub[6] + ub[7]));
-        }
-        if (so < q2) {   // sh[so][k], k = 2 k2 + h
-            sh[so * kl + 2 * k2] = s1a;
-            sh[so * kl + 2 * k2 + 1] = s1b;
-            sh[512 + so * kl + 2 * k2] = s2a;
-            sh[512 + so * kl + 2 * k2 + 1] = s2b;
-        }
+    // (ph_sums.h: the per-thread sums, shared with the solve tail's one-wave form)
+    const bool pairs = nsum_pairs(a, sg);
+    for (int k0 = 256 * (int)blockIdx.y; k0 < sg.klen; k0 += 256 * (int)gridDim.y) {
+        const NsumThread th = nsum_thread(pairs, sg.klen, k0, sg.s1 - sg.s0, tid);
+        double r[4];
+        nsum_thread_sums<NTL>(a, sg, k0, th, pairs, r);
+        nsum_stage(sh, th, pairs, r);
         __syncthreads();
-        if (tid < kl) {
+        if (tid < th.kl) {
             double t1 = 0.0, t2 = 0.0;
-            for (int j = 0; j < q2; ++j) { t1 += sh[j * kl + tid]; t2 += sh[512 + j * kl + tid]; }
-            publish(&out[k0 + tid], t1);
-            publish(&out[a.maxk + k0 + tid], t2);
-        }
-        __syncthreads();
-    }
-    for (int k0 = 256 * (int)blockIdx.y; !pairs && k0 < sg.klen; k0 += 256 * (int)gridDim.y) {
-        const int kl = min(256, sg.klen - k0);
-        const int q = 256 / kl;
-        const int k = tid % kl;
-        const int so = tid / kl;
-        double s1 = 0.0, s2 = 0.0;
-        if (so < q) {
-            const int kg = sg.kofs + k0 + k;
-            auto px = [&](int s, double& p, double& xv) {
-                xv = a.xN[(long)s * a.N + kg];
-                p = a.pcv ? a.pcv[(long)s * a.N + kg] : a.pc[(long)s * a.L + sg.level];
-            };
-            int s = sg.s0 + so;
-            // eight independent rows per step (fixed pairing: deterministic), then the remainder
-            constexpr int R = 8;
-            double t1[R], t2[R];
-#pragma unroll
-            for (int u = 0; u < R; ++u) t1[u] = t2[u] = 0.0;
-            for (; s + (R - 1) * q < sg.s1; s += R * q) {
-                double p[R], xv[R];
-#pragma unroll
-                for (int u = 0; u < R; ++u) px(s + u * q, p[u], xv[u]);
-#pragma unroll
-                for (int u = 0; u < R; ++u) { t1[u] += p[u] * xv[u]; t2[u] += p[u] * xv[u] * xv[u]; }
-            }
-            {   // the remainder: loads first, then added in row order (as in the pairs path)
-                double p[R], xv[R];
-#pragma unroll
-                for (int u = 0; u < R; ++u)
-                    if (s + u * q < sg.s1) px(s + u * q, p[u], xv[u]);
-#pragma unroll
-                for (int u = 0; u < R; ++u)
-                    if (s + u * q < sg.s1) {
-                        t1[0] += p[u] * xv[u];
-                        t2[0] += p[u] * xv[u] * xv[u];
-                    }
-            }
-            s1 = ((t1[0] + t1[1]) + (t1[2] + t1[3])) + ((t1[4] + t1[5]) + (t1[6] + t1[7]));
-            s2 = ((t2[0] + t2[1]) + (t2[2] + t2[3])) + ((t2[4] + t2[5]) + (t2[6] + t2[7]));
-        }
-        sh[tid] = s1;
-        sh[512 + tid] = s2;
-        __syncthreads();
-        if (tid < kl) {
-            double t1 = 0.0, t2 = 0.0;
-            for (int j = 0; j < q; ++j) { t1 += sh[j * kl + tid]; t2 += sh[512 + j * kl + tid]; }
+            for (int j = 0; j < th.q; ++j) { t1 += sh[j * th.kl + tid]; t2 += sh[512 + j * th.kl + tid]; }
             publish(&out[k0 + tid], t1);
             publish(&out[a.maxk + k0 + tid], t2);
         }

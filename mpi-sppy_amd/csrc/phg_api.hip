@@ -39,6 +39,7 @@ hipError_t pdhg_local_launch(int v, const PdhgArgs& a, hipStream_t stream);
 hipError_t scale_cols_launch(double* cl, double* cu, const double* dc, long cnt, hipStream_t stream);
 bool pdhg_local_lone(int v, int S);
 int pdhg_local_loop_ops(int v);
+size_t pdhg_local_lds_bytes(int v);
 int pdhg_block_num_variants();
 void pdhg_block_variant_shape(int v, int* out12);
 size_t pdhg_block_lds_bytes(int v, int n_pad, int m_pad, int nd, int ecodes);
@@ -243,7 +244,14 @@ struct phg_handle {
         long long gated_seq = 0, seq = 0;
         double* out = nullptr;
     } tp;
-    unsigned* tail_cnt = nullptr;    // [4] TailArgs::cnt
+    // the tail's unit counters, scenario -> unit maps and final slot plan (TailArgs; build_ph_tables)
+    unsigned* tail_segcnt = nullptr;
+    unsigned* tail_csegcnt = nullptr;
+    unsigned* tail_done = nullptr;
+    int* tail_scen_seg = nullptr;
+    int* tail_scen_cseg = nullptr;
+    int* tail_fin = nullptr;
+    int tail_nfin = 0;
     double* xbar_next = nullptr;     // [2 N_tot] staging x-bar of the one-GPU tail
     // the launch schedule is recomputed after every sched_every()-th solve (iteration counts move
     // slowly under warm starts; the sort is a latency-bound single-workgroup launch)
@@ -1048,6 +1056,49 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
         NodeSeg* p;
         if (dput(h, &p, segs.data(), segs.size())) return -1;
         a.seg = p;
+    }
+    {   // the solve tail's tables (ph_tail.h): every scenario's node segment per level and conv
+        // segment, the unit counters, and the final reduction's slot plan -- node_sum_final's ranks
+        // (K = the node-sum grid's min(n_final, workgroups)), each element's T strided sums in T
+        // aligned slots, elements packed widest T first so every run stays T-aligned
+        std::vector<int> sseg((size_t)S * L, 0), scs(S, 0);
+        for (int g = 0; g < (int)segs.size(); ++g)
+            for (int s2 = segs[g].s0; s2 < segs[g].s1; ++s2) sseg[(size_t)s2 * L + segs[g].level] = g;
+        for (size_t c = 0; c < cs0.size(); ++c)
+            for (int s2 = cs0[c]; s2 < cs1[c]; ++s2) scs[s2] = (int)c;
+        const long ny = (maxk + 255) / 256;
+        const int K = (int)std::min<long>(a.n_final, (long)segs.size() * ny);
+        struct El { int e, T, g0, cnt, i; };
+        std::vector<El> els;
+        for (int r = 0; r < K; ++r) {
+            const int e_lo = (int)((long)b->N_tot * r / K), e_hi = (int)((long)b->N_tot * (r + 1) / K);
+            const int ne = e_hi - e_lo;
+            int T = 1;
+            while (T < 64 && T * 2 * ne <= 256) T *= 2;
+            for (int e = e_lo; e < e_hi; ++e) {
+                int lo = 0, hi = b->n_nodes - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (b->node_off[mid] <= e) lo = mid; else hi = mid - 1;
+                }
+                els.push_back({e, T, first[lo], first[lo + 1] - first[lo], e - b->node_off[lo]});
+            }
+        }
+        std::stable_sort(els.begin(), els.end(), [](const El& x, const El& y) { return x.T > y.T; });
+        std::vector<int> fin;
+        for (const El& el : els)
+            for (int sub = 0; sub < el.T; ++sub) {
+                const int J = sub < el.cnt ? (el.cnt - sub + el.T - 1) / el.T : 0;
+                fin.insert(fin.end(), {el.e, el.g0 + sub, J, el.T, el.i});
+            }
+        while ((fin.size() / 5) % 64) fin.insert(fin.end(), {-1, 0, 0, 1, 0});
+        h->tail_nfin = (int)(fin.size() / 5);
+        if (dput(h, &h->tail_scen_seg, sseg.data(), sseg.size())) return -1;
+        if (dput(h, &h->tail_scen_cseg, scs.data(), scs.size())) return -1;
+        if (dput(h, &h->tail_fin, fin.data(), fin.size())) return -1;
+        if (dalloc(h, &h->tail_segcnt, segs.size())) return -1;
+        if (dalloc(h, &h->tail_csegcnt, cs0.size())) return -1;
+        if (dalloc(h, &h->tail_done, 1)) return -1;
     }
     int* ip;
     double* dp;
@@ -2801,15 +2852,23 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         static const bool tail_off = [] { const char* e = std::getenv("PHG_TAIL"); return e && std::atoi(e) == 0; }();
         const int mode = h->tail_req;
         h->tail_req = 0;
-        if (mode && !tail_off && h->local_variant >= 0 && a.fold_w && a.gate && !o->fix_nonants && !a.prof) {
-            if (!h->tail_cnt && dalloc(h, &h->tail_cnt, 4)) return -1;
+        // (P <= 512: the metric's per-rank ratios fit the wave's LDS; every variant's LDS holds the
+        // 1 024 doubles of a segment's staging array)
+        if (mode && !tail_off && h->local_variant >= 0 && a.fold_w && a.gate && !o->fix_nonants && !a.prof &&
+            h->ph.P <= 512 && pdhg_local_lds_bytes(h->local_variant) >= 1024 * sizeof(double)) {
             if (mode == 1 && !h->xbar_next && dalloc(h, &h->xbar_next, 2 * (size_t)std::max(1, h->N_tot))) return -1;
             TailArgs& t = a.tl;
             t.mode = mode;
-            t.W = (h->S + 64 / h->lshape[0] - 1) / (64 / h->lshape[0]);
-            t.T = std::min(t.W, std::min(256, std::max(1, std::max(h->ph.n_seg, h->ph.n_cseg))));
-            t.R = std::min(t.T, 8);
-            // PHG_TAIL_PROF=1 (diagnostic): the tail's phase stamps, printed after the launch (syncs)
+            const char* eg = std::getenv("PHG_TAIL_GENERIC");   // (read per launch: tests switch it)
+            t.generic = (eg && std::atoi(eg)) ? 1 : 0;
+            t.segcnt = h->tail_segcnt;
+            t.csegcnt = h->tail_csegcnt;
+            t.done = h->tail_done;
+            t.scen_seg = h->tail_scen_seg;
+            t.scen_cseg = h->tail_scen_cseg;
+            t.fin = h->tail_fin;
+            t.n_fin = h->tail_nfin;
+            // PHG_TAIL_PROF=1 (diagnostic): the final wave's stamps, printed after the launch (syncs)
             static unsigned long long* tprof = nullptr;
             t.prof = nullptr;
             if (const char* e = std::getenv("PHG_TAIL_PROF"); e && std::atoi(e)) {
@@ -2817,7 +2876,6 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
                 CK(hipMemsetAsync(tprof, 0, 8 * sizeof(unsigned long long), h->stream));
                 t.prof = tprof;
             }
-            t.cnt = h->tail_cnt;
             t.out = h->tail_req_out;
             t.xbar_next = h->xbar_next;
             t.xbar_cur = h->xbar;
@@ -2918,6 +2976,8 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         }
         if (lprof) CK(hipMemsetAsync(pbuf, 0, pcap * sizeof(unsigned long long), h->stream));
         a.prof = lprof ? pbuf : nullptr;
+        const char* ew = std::getenv("PHG_WATCH_SCEN");
+        a.watch = ew ? std::atoi(ew) : -1;
         CK(pdhg_local_launch(h->local_variant, a, h->stream));
         if (lprof) {
             std::vector<unsigned long long> hb(pcap);
@@ -2977,9 +3037,8 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         CK(hipMemcpyAsync(st, a.tl.prof, sizeof st, hipMemcpyDeviceToHost, h->stream));
         CK(hipStreamSynchronize(h->stream));
         auto us = [&](int i, int j) { return st[i] && st[j] ? ((double)st[j] - (double)st[i]) / 100.0 : -1.0; };
-        fprintf(stderr, "PHG_TAIL_PROF T %d R %d waves %d: last wave -> rank0 past wait %.2f us, partials %.2f us, "
-                "-> final past wait %.2f us, final %.2f us, total %.2f us\n", a.tl.T, a.tl.R, a.tl.W, us(0, 1),
-                us(1, 2), us(2, 3), us(3, 4), us(0, 4));
+        fprintf(stderr, "PHG_TAIL_PROF final wave: its epilogue -> final start %.2f us, final %.2f us\n", us(0, 1),
+                us(1, 2));
     }
     h->xn_external = false;
     if (o->safe_bound && !o->fix_nonants) {   // bound.hip: certificates whatever the statuses
@@ -3204,6 +3263,24 @@ int phg_set_tail(phg_handle* h, int32_t mode, double convthresh, double* dev_pac
     h->tail_req = mode;
     h->tail_req_thr = convthresh;
     h->tail_req_out = mode == 1 ? h->packed : dev_packed;
+    return 0;
+}
+
+int phg_tail_info(phg_handle* h, int32_t* out4) {
+    if (!h || !h->loaded || !out4) return fail("phg_tail_info: no batch loaded / null argument");
+    CK(hipSetDevice(h->device));
+    const int ns = h->ph.n_seg, nc = h->ph.n_cseg;
+    std::vector<unsigned> c((size_t)ns + nc + 1);
+    CK(hipMemcpyAsync(c.data(), h->tail_segcnt, ns * sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+    CK(hipMemcpyAsync(c.data() + ns, h->tail_csegcnt, nc * sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+    CK(hipMemcpyAsync(c.data() + ns + nc, h->tail_done, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream));
+    CK(hipStreamSynchronize(h->stream));
+    long armed = 0;
+    for (unsigned v : c) armed += v != 0;
+    out4[0] = ns + nc;
+    out4[1] = h->tail_nfin;
+    out4[2] = (int32_t)armed;
+    out4[3] = h->tp.mode;
     return 0;
 }
 

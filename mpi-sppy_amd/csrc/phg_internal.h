@@ -240,14 +240,21 @@ struct PhArgs {
 
 // The PH update fused into the end of a lane-local solve (ph_tail.h): mode 0 off; 1 one GPU (node
 // sums into `out`, convergence partials, gate, next x-bar into xbar_next); 2 multi-GPU (node sums and
-// the folded update's convergence partials into the caller's exchange buffer `out`)
+// the folded update's convergence partials into the caller's exchange buffer `out`).  Units: the
+// node segments (PhArgs::seg) and the conv segments (PhArgs::cseg_*); the wave that completes a unit
+// computes its partial, the wave that completes the last unit the final reduction
 struct TailArgs {
     int mode;
-    int W;                   // waves of the solve's grid
-    int T;                   // the last T of them to finish run the update (<= W)
-    int R;                   // ranks of the final phase (<= T)
-    unsigned* cnt;           // [4] waves done, tail ranks arrived, final ranks done, give-up flag
-    unsigned long long* prof;   // diagnostic (PHG_TAIL_PROF): [8] s_memrealtime stamps of the tail, or null
+    int generic;             // 1 (diagnostic / tests, PHG_TAIL_GENERIC=1): segment partials through the
+                             // node-sum workgroup's own per-thread loops, one quarter at a time
+    unsigned* segcnt;        // [n_seg] scenarios of the node segment counted in (0 between launches)
+    unsigned* csegcnt;       // [n_cseg] ... of the conv segment
+    unsigned* done;          // [1] units finished
+    const int* scen_seg;     // [S*L] node segment of scenario s at level l
+    const int* scen_cseg;    // [S] conv segment of scenario s
+    const int* fin;          // [5 n_fin] final slots {element, first segment, terms, stride T, position}
+    int n_fin;
+    unsigned long long* prof;   // diagnostic (PHG_TAIL_PROF): [3] s_memrealtime stamps, or null
     double* out;             // [2 N_tot node sums | 2P+2 partials | flag]
     double* xbar_next;       // mode 1: [2 N_tot] the next x-bar / x-sq-bar (the current ones if conv < thr)
     const double* xbar_cur;  // mode 1: [2 N_tot]
@@ -304,6 +311,7 @@ struct PdhgArgs {
     // cycles, load cycles, KKT cycles, restart-block cycles, checks}; PHG_BORDER_PROF, the bordered
     // register-resident kernel: per workgroup [10] (pdhg_border.hip); null = off
     unsigned long long* prof;
+    int watch;              // with prof (lane-local kernel): scenario whose every check is printed (PHG_WATCH_SCEN), -1 none
     // outputs
     double* x_out;          // [S*n] unscaled, or null: left to phg_get / eval (xs * dc, see unscale_launch)
     double* y_out;          // [S*m] unscaled, or null (ys * dr)

@@ -22,6 +22,7 @@ __device__ __forceinline__ double dpp_d(double v) {
 
 // rows (0,1) and (2,3) exchanged: returns own + partner-row value, same bits in both rows
 __device__ __forceinline__ double swap16_add(double v) {
+#pragma clang fp contract(off)
     const int lo = __double2loint(v), hi = __double2hiint(v);
     const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
     const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
@@ -29,6 +30,7 @@ __device__ __forceinline__ double swap16_add(double v) {
 }
 
 __device__ __forceinline__ double swap32_add(double v) {
+#pragma clang fp contract(off)
     const int lo = __double2loint(v), hi = __double2hiint(v);
     const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
     const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
@@ -36,8 +38,15 @@ __device__ __forceinline__ double swap32_add(double v) {
 }
 
 // all-reduce over groups of LPS lanes; K independent values interleaved for ILP
+//
+// Contraction is OFF here: a partial that is a single product (farmer's coupling row: one entry per
+// lane) would otherwise be fused into the first DPP add -- fma(a_i, b_i, round(a_j b_j)) in lane i,
+// fma(a_j, b_j, round(a_i b_i)) in lane j -- and the lanes of a group would disagree in the last bit,
+// then on the restart / termination decisions that every lane takes from these sums (round 6: a
+// farmer 10k prox-QP ran to the 2e5-iteration cap at a gap its split group could no longer close)
 template <int LPS, int K>
 __device__ __forceinline__ void gsum_many(double (&v)[K]) {
+#pragma clang fp contract(off)
     static_assert(LPS == 16 || LPS == 32 || LPS == 64, "group of 16, 32 or 64 lanes");
 #pragma unroll
     for (int k = 0; k < K; ++k) v[k] += dpp_d<0x128>(v[k]);   // row_ror:8

@@ -339,6 +339,14 @@ class Engine:
         mode = 2 if self.exchange is not None else 1
         _lib.check(self.lib.phg_set_tail(self.h, mode, float(convthresh), self._ns_ptr()))
 
+    def tail_info(self):
+        """The solve tail's state (phg_tail_info, synchronises): units, final slots, counters not
+        re-armed (0 between launches), and the last solve's tail mode."""
+        out = np.zeros(4, np.int32)
+        _lib.check(self.lib.phg_tail_info(self.h, ptr(out)))
+        return {"units": int(out[0]), "final_slots": int(out[1]), "armed_counters": int(out[2]),
+                "last_mode": int(out[3])}
+
     def set_fold(self, on):
         """Folded PH update on / off (phg_set_fold); returns whether this batch's solves take it."""
         out = np.zeros(1, np.int32)

@@ -67,6 +67,8 @@ class MultiExtension(Extension):
     def __init__(self, ph, ext_classes):
         super().__init__(ph)
         self.extdict = {cls.__name__: cls(ph) for cls in ext_classes}
+        # the pipelined PH loop may run them only if every member only touches solver options
+        self.pipeline_safe = all(getattr(e, "pipeline_safe", False) for e in self.extdict.values())
 
     def post_solve(self, subproblem, results):
         for e in self.extdict.values():

@@ -345,8 +345,33 @@ class PHBase(SPBase):
         (miditer), no converger object, no per-solve timing.  (A time limit is checked before the
         solve is enqueued, see :meth:`iterk_loop`.)"""
         o = self.options
-        return (self.extobject is None and self.ph_converger is None
+        ext_ok = self.extobject is None or bool(getattr(self.extobject, "pipeline_safe", False))
+        return (ext_ok and self.ph_converger is None
                 and not o.get("display_timing", False) and o.get("pdhg_pipeline", True))
+
+    def _apply_eps_schedule(self):
+        """Built-in PDHG tolerance schedule (``options["pdhg_eps_schedule"]``): pairs (conv_above,
+        eps) in order; the next solve runs at the eps of the first pair whose conv_above the last
+        known convergence metric reaches (+inf before the first metric), and the schedule never
+        loosens again once it has tightened.  The reference's mechanism for a per-iteration solver
+        tolerance is ``current_solver_options`` (set by extensions such as the Gapper,
+        ``extensions/mipgapper.py:15-60``); this sets ``current_solver_options["pdhg_eps"]`` from the
+        metric instead of the iteration number.  In the pipelined loop the last known metric is
+        conv_{k-2} when solve k is enqueued (one iteration of lag)."""
+        sched = self.options.get("pdhg_eps_schedule")
+        if not sched:
+            return
+        conv = math.inf if self.conv is None else float(self.conv)
+        idx = len(sched) - 1
+        for i, (above, _eps) in enumerate(sched):
+            if conv >= above:
+                idx = i
+                break
+        idx = max(idx, getattr(self, "_eps_sched_idx", 0))
+        self._eps_sched_idx = idx
+        if self.current_solver_options is None:
+            self.current_solver_options = {}
+        self.current_solver_options["pdhg_eps"] = float(sched[idx][1])
 
     def update_and_solve(self, verbose=False, first=False):
         """One pipelined PH iteration k with ONE all-reduce (include/phg.h, phg_ph_head).
@@ -603,6 +628,11 @@ class PHBase(SPBase):
                         break
                 pipelined = False
             if pipelined:
+                # solver-option hooks keyed by the iteration (pipeline-safe extensions: the Gapper)
+                # and the conv-keyed eps schedule, before solve k is enqueued
+                self._apply_eps_schedule()
+                if self.extobject is not None:
+                    self.extobject.miditer()
                 c = self.update_and_solve(verbose, first=self._PHIter == 1)
                 if self._PHIter > 1:
                     self.conv = c
@@ -625,6 +655,7 @@ class PHBase(SPBase):
                     break
                 # nothing reads the bounds of the prox-QP solves inside the loop: no
                 # safe-bound pass, as in the pipelined form
+                self._apply_eps_schedule()
                 self.solve_loop(solver_options=self.current_solver_options, dtiming=self.options["display_timing"],
                                 gripe=verbose, verbose=verbose, safe_bound=False)
             if self.extobject is not None:

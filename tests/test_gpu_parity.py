@@ -424,16 +424,23 @@ def test_field_read_between_head_and_solve_keeps_fold_trajectory(monkeypatch, th
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("S,exch,thr", [(10000, False, 1e-10), (10000, True, 1e-10), (1000, False, 5.0),
-                                        (1000, True, 5.0), (30, False, 1e-4)])
-def test_solve_tail_matches_separate_launches(S, exch, thr):
+@pytest.mark.parametrize("S,exch,thr,generic", [(10000, False, 1e-10, "0"), (10000, True, 1e-10, "0"),
+                                                (1000, False, 5.0, "0"), (1000, True, 5.0, "0"),
+                                                (1000, False, 5.0, "1"), (1000, True, 1e-10, "1"),
+                                                (30, False, 1e-4, "0"), (20000, False, 1e-10, "0")])
+def test_solve_tail_matches_separate_launches(S, exch, thr, generic, monkeypatch):
     """The PH update fused into the end of the solve (ph_tail.h, phg_set_tail): one GPU (mode 1:
     node sums, conv, gate and the staged next x-bar) and the exchange form (mode 2: node sums and
     partials into the packed buffer, then the all-reduce and the head) against the same pipelined
-    iterations with separate launches.  The tail's sums are fixed-order but associated differently
-    (node segments summed by 64-lane waves), so the trajectories agree to rounding: the same PH
-    iteration count and break (thr 5 stops on convthresh; S = 30 runs to conv < 1e-4), conv history
-    to 1e-10 relative, W / x-bar / x to 1e-9."""
+    iterations with separate launches.  Every segment sum is associated as node_sums_kernel's
+    workgroups associate it (ph_sums.h) and the final reduction in node_sum_final /
+    conv_partials_final / conv_value_block order, so the two runs are the same bit for bit: the
+    same PH iteration count and break (thr 5 stops on convthresh; S = 30 runs to conv < 1e-4), conv
+    history, W, x-bar and x.  generic = 1 runs the segment partials through the workgroup's own
+    per-thread loops (PHG_TAIL_GENERIC); S = 20 000 has 79-scenario segments, past the one-pass form's
+    four rows per thread.  After the run every unit counter is back at zero (each re-armed by the wave
+    that completed it)."""
+    monkeypatch.setenv("PHG_TAIL_GENERIC", generic)
     res = []
     for tail in (True, False):
         opts = dict(PHIterLimit=30 if S > 30 else 20000, convthresh=thr, pdhg_tail=tail)
@@ -441,21 +448,39 @@ def test_solve_tail_matches_separate_launches(S, exch, thr):
             opts["pdhg_exchange"] = True
         ph = _farmer_ph(S, cm=10, **opts)
         ph.ph_main(finalize=False)
+        if tail:
+            ti = ph.engine.tail_info()
+            assert ti["units"] > 0 and ti["armed_counters"] == 0, ti
         res.append((list(ph.conv_history), ph.Ws().copy(), ph.xbars().copy(), ph.nonants().copy(), ph._PHIter))
     (h1, W1, xb1, x1, it1), (h0, W0, xb0, x0, it0) = res
-    assert it1 == it0 and len(h1) == len(h0), (it1, it0)
-    # over 30 PH iterations the rounding stays at 1e-10; over the ~9 500 of the S = 30 run to
-    # convergence it grows (each prox-QP is solved to a 1e-9 KKT error) -- there the north star's
-    # tolerances: x-bar 1e-6 relative, W 1e-5
-    long_run = len(h0) > 100
-    tol = 1e-6 if long_run else 1e-9
-    np.testing.assert_allclose(h1, h0, rtol=1e-5 if long_run else 1e-10)
+    assert it1 == it0 and h1 == h0, (it1, it0)
     if thr > 1e-9:
         assert h1[-1] < thr
-    sc = max(1.0, float(np.abs(x0).max()))
-    np.testing.assert_allclose(xb1, xb0, rtol=tol, atol=tol * sc)
-    np.testing.assert_allclose(x1, x0, rtol=tol, atol=tol * sc)
-    np.testing.assert_allclose(W1, W0, rtol=tol, atol=1e-5 if long_run else 1e-9 * max(1.0, float(np.abs(W0).max())))
+    assert np.array_equal(xb1, xb0) and np.array_equal(x1, x0) and np.array_equal(W1, W0)
+
+
+def test_tail_results_discarded_then_next_tail_correct():
+    """A tail whose results the host does not take over (phg_set between the solve and the next
+    PH step: the separate launches run instead) leaves no counter armed, and the following tails
+    are correct: the run equals the separate-launch run with the same interruptions bit for bit."""
+    res = []
+    for tail in (True, False):
+        ph = _farmer_ph(1000, cm=10, PHIterLimit=12, convthresh=1e-10, pdhg_tail=tail)
+        ph.PH_Prep()
+        ph.Iter0()
+        ph.current_solver_options = ph.iterk_solver_options
+        hist = []
+        for k in range(12):
+            hist.append(ph.update_and_solve(first=k == 0))
+            if k in (3, 4, 8):
+                ph.W_from_flat_list(ph.Ws().ravel())     # (the same W: only the tail's results are dropped)
+            if tail:
+                assert ph.engine.tail_info()["armed_counters"] == 0
+        c, _ = ph._drain_speculation()
+        res.append((hist + [c], ph.Ws().copy(), ph.xbars().copy(), ph.nonants().copy()))
+    assert res[0][0] == res[1][0]
+    for u, v in zip(res[0][1:], res[1][1:]):
+        assert np.array_equal(u, v)
 
 
 # ----------------------------------------------------------------------------- non-uniform trees (M3)
