@@ -48,7 +48,8 @@ struct MCold {
     static constexpr int N = SC + NSC;
 };
 
-template <int TM, int TN>
+// WATCH (diagnostic, PHG_WATCH_SCEN): the watched scenario's every check printed
+template <int TM, int TN, bool WATCH>
 __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
     if (a.gate && a.gate[0] < a.gate_below) return;   // PH converged: skip (PdhgArgs::gate)
     constexpr int KC = 4 * TN, KR = 4 * TM, NF = 4 * TM * TN;
@@ -389,6 +390,13 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
         const bool restart = live && ((cand <= a.beta_suf * a.beta_suf * krst) ||
                                       (cand <= a.beta_nec * a.beta_nec * krst && cand > SS(CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
+        if constexpr (WATCH) {
+            if (live && valid && s == a.watch && g == 0)
+                printf("PHG_WATCH s %d it %d since %d kc %.6e ka %.6e krst %.6e kprev %.6e rst %d ua %d om %.6e "
+                       "pres2 %.6e dres2 %.6e tp %.3e td %.3e pobj %.15e dobj %.15e koff %.6e\n",
+                       s, it, since, k_cur, k_avg, krst, SS(CI::KPREV), (int)restart, (int)use_avg, omega, oc[2], oc[3],
+                       SS(CI::TP), SS(CI::TD), oc[4], oc[5], SS(CI::KOFF));
+        }
         SS(CI::KPREV) = cand;
         if (wave_any(restart)) {
             const bool ra = restart && use_avg;
@@ -435,9 +443,10 @@ __global__ __launch_bounds__(64, 2) void pdhg_mfma_kernel(PdhgArgs a) {
 struct MfmaVariant {
     int TM, TN;
     void (*fn)(PdhgArgs);
+    void (*fn_watch)(PdhgArgs);
 };
 
-#define PHG_M(m_, n_) {m_, n_, pdhg_mfma_kernel<m_, n_>}
+#define PHG_M(m_, n_) {m_, n_, pdhg_mfma_kernel<m_, n_, false>, pdhg_mfma_kernel<m_, n_, true>}
 // smallest tile grid that holds (m, n) first
 // one 16 x 16 tile: 224 VGPRs, no spills; the 16 x 32 / 32 x 16 grids spill 220-324 bytes per
 // lane (8 TM TN fragments + 8 x 4 TN + 5 x 4 TM iterate values per lane), so they are left out
@@ -462,7 +471,7 @@ size_t pdhg_mfma_lds_bytes(int v) {
 
 hipError_t pdhg_mfma_launch(int v, const PdhgArgs& a, hipStream_t stream) {
     const MfmaVariant& V = kMfmaVariants[v];
-    hipLaunchKernelGGL(V.fn, dim3((a.S + 15) / 16), dim3(64), pdhg_mfma_lds_bytes(v), stream, a);
+    hipLaunchKernelGGL(a.watch >= 0 ? V.fn_watch : V.fn, dim3((a.S + 15) / 16), dim3(64), pdhg_mfma_lds_bytes(v), stream, a);
     return hipGetLastError();
 }
 

@@ -2822,6 +2822,11 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     a.bd = h->bd;
     a.gap_const = h->gap_const;
     a.sum_stride = h->sum_stride;
+    {   // PHG_WATCH_SCEN (diagnostic): a scenario whose every PDHG check is printed (the lane-local
+        // kernel's PROF instantiation, with PHG_LOCAL_PROF; the MFMA kernel's WATCH instantiation)
+        const char* ew = std::getenv("PHG_WATCH_SCEN");
+        a.watch = ew ? std::atoi(ew) : -1;
+    }
     if (h->fold_w_pending) {
         // the prologue's x = xs dc would not be the caller's xN (xn_external); or the caller did not
         // gate this solve on conv although the head that left the update pending had a convthresh
@@ -2976,8 +2981,6 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         }
         if (lprof) CK(hipMemsetAsync(pbuf, 0, pcap * sizeof(unsigned long long), h->stream));
         a.prof = lprof ? pbuf : nullptr;
-        const char* ew = std::getenv("PHG_WATCH_SCEN");
-        a.watch = ew ? std::atoi(ew) : -1;
         CK(pdhg_local_launch(h->local_variant, a, h->stream));
         if (lprof) {
             std::vector<unsigned long long> hb(pcap);
