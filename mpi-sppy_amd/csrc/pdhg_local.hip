@@ -821,26 +821,6 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         const bool restart = live && ((cand <= a.beta_suf * a.beta_suf * krst) ||
                                       (cand <= a.beta_nec * a.beta_nec * krst && cand > GS(CI::SC + CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
-        if constexpr (PROF) {   // PHG_WATCH_SCEN (diagnostic): one scenario's slots at iteration 4096 of a prox solve
-            if (live && s == a.watch && it == 4096 && a.prox_on && CPL == 4 && RPL == 2) {
-                double v[4][6];
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    const double ck = FOLD ? CS(CI::C + k) : c[k];
-                    const double qk = qon(k) ? CS(CI::Q + k) : 0.0;
-                    v[k][0] = x[k]; v[k][1] = lo[k]; v[k][2] = hi[k]; v[k][3] = ck; v[k][4] = qk; v[k][5] = aty[k];
-                }
-                printf("PHG_SLOT gl %d c0 %.17e %.17e %.17e %.17e %.17e %.17e c1 %.17e %.17e %.17e %.17e %.17e %.17e "
-                       "c2 %.17e %.17e %.17e %.17e %.17e %.17e c3 %.17e %.17e %.17e %.17e %.17e %.17e "
-                       "r0 %.17e %.17e %.17e %.17e %.17e r1 %.17e %.17e %.17e %.17e %.17e d0 %.17e %.17e %.17e %.17e "
-                       "ts %.17e %.17e %.17e\n",
-                       gl, v[0][0], v[0][1], v[0][2], v[0][3], v[0][4], v[0][5], v[1][0], v[1][1], v[1][2], v[1][3],
-                       v[1][4], v[1][5], v[2][0], v[2][1], v[2][2], v[2][3], v[2][4], v[2][5], v[3][0], v[3][1],
-                       v[3][2], v[3][3], v[3][4], v[3][5], y[0], ax[0], CS(CI::BLO + 0), CS(CI::BHI + 0), roff[0],
-                       y[RPL - 1], ax[RPL - 1], CS(CI::BLO + RPL - 1), CS(CI::BHI + RPL - 1), roff[RPL - 1], yd[0],
-                       axd[0], GS(CI::DLO + 0), GS(CI::DHI + 0), tau, sig, GS(CI::SC + CI::KOFF));
-            }
-        }
         if constexpr (PROF) {   // PHG_WATCH_SCEN (diagnostic): one scenario's restart / primal-weight history
             if (live && gl == 0 && s == a.watch)
                 printf("PHG_WATCH s %d it %d since %d avg %d kc %.6e ka %.6e krst %.6e kprev %.6e rst %d ua %d "

@@ -179,34 +179,34 @@ __device__ void tail_cseg_partial(const PhArgs& a, int b) {
 }
 
 // ---------------------------------------------------------------------------- 3. final
-// node_sum_final's sums: fin slot v = lane + 64 p holds {element e, first segment, terms J, stride T,
-// position i of e in its node} (e < 0: empty); the slot adds its J strided segment partials in order,
-// then the xor butterfly over its T aligned lanes (o < T) gives node_sum_final's bits in the
-// element's first lane
-constexpr int kTailJ = 12;   // strided terms loaded at once per slot (more: a second pass)
+// node_sum_final's sums: fin slot v = lane + 64 q holds {element e (< 0: empty), first segment, terms J
+// | stride T << 16, position i of e in its node}; the slot adds its J strided segment partials in
+// order, then the xor butterfly over its T aligned lanes (o < T) gives node_sum_final's bits in the
+// element's first lane.  Every load the final needs is issued in a few batches (the wave's loads
+// after the acquire miss the XCD's L2: each dependent round trip is a microsecond or more), and
+// every store comes after the last load.
+constexpr int kTailJ = 12;    // strided terms of a slot loaded at once (more: a second round)
+constexpr int kTailQ = 8;     // slot passes held in registers (512 slots; more: the plan in rounds)
+constexpr int kTailP = 128;   // virtual ranks the final keeps in LDS (host-checked)
 
-__device__ __forceinline__ void tail_fin_slot(const PhArgs& a, const int* fin, int v, double& t1, double& t2, int& e,
-                                              int& T) {
-    const int* f = fin + 5 * v;
-    e = f[0];
-    const int g0 = f[1], J = f[2], i = f[4];
-    T = f[3];
+__device__ __forceinline__ void tail_fin_sum(const PhArgs& p, const int4& f, double& t1, double& t2) {
+    const int e = f.x, g0 = f.y, J = f.z & 0xFFFF, T = f.z >> 16, i = f.w;
     t1 = t2 = 0.0;
     if (e < 0) return;
     double v1[kTailJ], v2[kTailJ];
 #pragma unroll
     for (int j = 0; j < kTailJ; ++j) {
-        const long gj = (long)(j < J ? g0 + j * T : g0) * 2 * a.maxk;
-        v1[j] = a.segpart[gj + i];
-        v2[j] = a.segpart[gj + a.maxk + i];
+        const long gj = (long)(j < J ? g0 + j * T : g0) * 2 * p.maxk;
+        v1[j] = p.segpart[gj + i];
+        v2[j] = p.segpart[gj + p.maxk + i];
     }
 #pragma unroll
     for (int j = 0; j < kTailJ; ++j)
         if (j < J) { t1 += v1[j]; t2 += v2[j]; }
     for (int j = kTailJ; j < J; ++j) {
-        const long gj = (long)(g0 + j * T) * 2 * a.maxk;
-        t1 += a.segpart[gj + i];
-        t2 += a.segpart[gj + a.maxk + i];
+        const long gj = (long)(g0 + j * T) * 2 * p.maxk;
+        t1 += p.segpart[gj + i];
+        t2 += p.segpart[gj + p.maxk + i];
     }
 }
 
@@ -214,10 +214,17 @@ __device__ void tail_final(const TailArgs& tl, double* lds) {
     const int lane = threadIdx.x;
     const PhArgs& p = tl.ph;
     double* cp = tl.out + 2 * (long)p.N_tot;
+    const int4* fin = reinterpret_cast<const int4*>(tl.fin);
+    const int nq = tl.n_fin / 64;
+    // -- round 1: the status counts, the slot plan and the ranks' conv-segment ranges
+    int tb = 0, tn = 0;
+    for (int g = lane; g < p.n_cseg; g += 64) { tb += p.csegbad[2 * g]; tn += p.csegbad[2 * g + 1]; }
+    int4 pl[kTailQ];
+#pragma unroll
+    for (int q = 0; q < kTailQ; ++q) pl[q] = q < nq ? fin[q * 64 + lane] : make_int4(-1, 0, 0, 0);
     // -- convergence partials (conv_partials_final): per virtual rank v, block_sum_range over its conv
     // segments -- a lane-strided sum per virtual thread, a butterfly per quarter, the quarters in
-    // order; each rank's ratio sum / count kept in lds[256 + v] for the metric (P <= 512, host-checked)
-    int tb = 0, tn = 0;
+    // order; sum, count and ratio kept in LDS (lds[256 + v], lds[384 + 2 v], + 1) until the stores
     for (int v = 0; v < p.P; ++v) {
         const int g0 = p.vr_first[v], g1 = p.vr_first[v + 1];
         double r[4];
@@ -230,19 +237,13 @@ __device__ void tail_final(const TailArgs& tl, double* lds) {
         const double sum = ((r[0] + r[1]) + r[2]) + r[3];
         const double cnt = g1 > g0 ? (double)(p.cseg_s1[g1 - 1] - p.cseg_s0[g0]) * (double)p.N : 0.0;
         if (lane == 0) {
-            cp[2 * v] = sum;
-            cp[2 * v + 1] = cnt;
             lds[256 + v] = cnt > 0.0 ? sum / cnt : 0.0;   // (a rank without nonants adds nothing)
+            lds[384 + 2 * v] = sum;
+            lds[384 + 2 * v + 1] = cnt;
         }
     }
-    for (int g = lane; g < p.n_cseg; g += 64) { tb += p.csegbad[2 * g]; tn += p.csegbad[2 * g + 1]; }
     tb = wave_sum(tb);
     tn = wave_sum(tn);
-    if (lane == 0) {
-        cp[2 * p.P] = (double)tb;
-        cp[2 * p.P + 1] = (double)tn;
-        cp[2 * p.P + 2] = 1.0;   // the partials are a W update's
-    }
     double conv = INFINITY;
     if (tl.mode == 1) {
         // conv_value_block: virtual thread t adds the ratios of ranks t, t + 256, ...; then the
@@ -251,9 +252,7 @@ __device__ void tail_final(const TailArgs& tl, double* lds) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int t = lane + 64 * q;
-            double acc = 0.0;
-            for (int v = t; v < p.P; v += 256) acc += lds[256 + v];
-            lds[t] = acc;
+            lds[t] = t < p.P ? lds[256 + t] : 0.0;
         }
         __syncthreads();
         for (int w = 128; w > 0; w >>= 1) {
@@ -261,48 +260,57 @@ __device__ void tail_final(const TailArgs& tl, double* lds) {
             __syncthreads();
         }
         conv = lds[0] / (double)p.P;
-        __syncthreads();
     }
     const bool keep = tl.mode == 1 && !(conv >= tl.thr);   // below convthresh: x-bar stays
-    // -- node sums (node_sum_final's order), two slot quarters in flight at a time
-    for (int v0 = 0; v0 < tl.n_fin; v0 += 128) {
-        double t1[2], t2[2];
-        int e[2], T[2];
+    // -- node sums (node_sum_final's order), two slot passes per round of loads
+    auto do_pass = [&](const int4& f, int v, double t1, double t2) {
+        const int T = f.z >> 16;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int v = v0 + 64 * h + lane;
-            if (v < tl.n_fin) tail_fin_slot(p, tl.fin, v, t1[h], t2[h], e[h], T[h]);
-            else { t1[h] = t2[h] = 0.0; e[h] = -1; T[h] = 1; }
+        for (int o = 1; o < 64; o <<= 1) {
+            const double u1 = __shfl_xor(t1, o, 64), u2 = __shfl_xor(t2, o, 64);
+            if (o < T) { t1 += u1; t2 += u2; }
         }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const double u1 = __shfl_xor(t1[h], o, 64), u2 = __shfl_xor(t2[h], o, 64);
-                if (o < T[h]) { t1[h] += u1; t2[h] += u2; }
-            }
-            const int v = v0 + 64 * h + lane;
-            if (e[h] >= 0 && (v % T[h]) == 0) {
-                tl.out[e[h]] = t1[h];
-                tl.out[p.N_tot + e[h]] = t2[h];
-                if (tl.mode == 1) {
-                    tl.xbar_next[e[h]] = keep ? tl.xbar_cur[e[h]] : t1[h];
-                    tl.xbar_next[p.N_tot + e[h]] = keep ? tl.xbar_cur[p.N_tot + e[h]] : t2[h];
-                }
+        const int e = f.x;
+        if (e >= 0 && (v % T) == 0) {
+            tl.out[e] = t1;
+            tl.out[p.N_tot + e] = t2;
+            if (tl.mode == 1) {
+                tl.xbar_next[e] = keep ? tl.xbar_cur[e] : t1;
+                tl.xbar_next[p.N_tot + e] = keep ? tl.xbar_cur[p.N_tot + e] : t2;
             }
         }
+    };
+#pragma unroll
+    for (int q = 0; q < kTailQ; q += 2) {
+        if (q >= nq) break;
+        double a1, a2, b1, b2;
+        tail_fin_sum(p, pl[q], a1, a2);
+        tail_fin_sum(p, pl[q + 1], b1, b2);
+        do_pass(pl[q], q * 64 + lane, a1, a2);
+        do_pass(pl[q + 1], (q + 1) * 64 + lane, b1, b2);
     }
-    // -- the gate (one GPU): device copy for the next gated launch, pinned host ring for the host
-    if (tl.mode == 1 && lane == 0) {
-        tl.gate[0] = conv;
-        tl.gate[1] = (double)tb;
-        tl.gate[2] = (double)tn;
-        double* gh = tl.gate_host + 4 * ((long long)tl.seq & 1);   // (the host reads slot seq mod 2)
-        __hip_atomic_store(&gh[0], conv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&gh[1], (double)tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&gh[2], (double)tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-        __hip_atomic_store(&gh[3], tl.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int q = kTailQ; q < nq; ++q) {   // (plans beyond the registers' passes)
+        const int4 f = fin[q * 64 + lane];
+        double a1, a2;
+        tail_fin_sum(p, f, a1, a2);
+        do_pass(f, q * 64 + lane, a1, a2);
+    }
+    // -- the convergence partials, then the gate (one GPU): device copy for the next gated launch,
+    // pinned host ring for the host
+    if (lane == 0) {
+        for (int v = 0; v < p.P; ++v) {
+            cp[2 * v] = lds[384 + 2 * v];
+            cp[2 * v + 1] = lds[384 + 2 * v + 1];
+        }
+        cp[2 * p.P] = (double)tb;
+        cp[2 * p.P + 1] = (double)tn;
+        cp[2 * p.P + 2] = 1.0;   // the partials are a W update's
+        if (tl.mode == 1) {
+            tl.gate[0] = conv;
+            tl.gate[1] = (double)tb;
+            tl.gate[2] = (double)tn;
+            publish_host_gate(tl.gate_host, conv, (double)tb, (double)tn, tl.seq);   // (slot seq mod 2)
+        }
     }
 }
 

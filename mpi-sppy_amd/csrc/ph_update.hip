@@ -72,7 +72,7 @@ __device__ double conv_value_block(const double* convpart, int P, double* red) {
 }
 
 // gate = {conv, not optimal, NaN} (the status counts ride in convpart[2P], [2P+1]).  The same
-// three values go to fine-grained pinned host memory followed (system-scope fences) by the
+// three values go to fine-grained pinned host memory followed (drained, publish_host_gate) by the
 // sequence number `seq` in word 3 of slot seq mod 2 of the [2][4] ring: the host polls that word,
 // so no event has to pass through the GPU's queue (two slots: a solve's fused tail, ph_tail.h, may
 // publish the NEXT value before the host has read this one).  Called by one thread.
@@ -80,12 +80,7 @@ __device__ void publish_gate(double conv, const double* convpart, int P, double*
                              double seq) {
     const double g[3] = {conv, convpart[2 * P], convpart[2 * P + 1]};
     for (int i = 0; i < 3; ++i) gate[i] = g[i];
-    if (gate_host) {
-        double* gh = gate_host + 4 * ((long long)seq & 1);
-        for (int i = 0; i < 3; ++i) __hip_atomic_store(&gh[i], g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-        __hip_atomic_store(&gh[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (gate_host) publish_host_gate(gate_host, g[0], g[1], g[2], seq);
 }
 
 __device__ void conv_gate_block(const double* convpart, int P, double* gate, double* gate_host, double seq) {

@@ -1085,14 +1085,15 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
             }
         }
         std::stable_sort(els.begin(), els.end(), [](const El& x, const El& y) { return x.T > y.T; });
+        // slot = int4 {element, first segment, terms | stride << 16, position in the node}
         std::vector<int> fin;
         for (const El& el : els)
             for (int sub = 0; sub < el.T; ++sub) {
                 const int J = sub < el.cnt ? (el.cnt - sub + el.T - 1) / el.T : 0;
-                fin.insert(fin.end(), {el.e, el.g0 + sub, J, el.T, el.i});
+                fin.insert(fin.end(), {el.e, el.g0 + sub, J | (el.T << 16), el.i});
             }
-        while ((fin.size() / 5) % 64) fin.insert(fin.end(), {-1, 0, 0, 1, 0});
-        h->tail_nfin = (int)(fin.size() / 5);
+        while ((fin.size() / 4) % 64) fin.insert(fin.end(), {-1, 0, 1 << 16, 0});
+        h->tail_nfin = (int)(fin.size() / 4);
         if (dput(h, &h->tail_scen_seg, sseg.data(), sseg.size())) return -1;
         if (dput(h, &h->tail_scen_cseg, scs.data(), scs.size())) return -1;
         if (dput(h, &h->tail_fin, fin.data(), fin.size())) return -1;
@@ -2857,10 +2858,10 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         static const bool tail_off = [] { const char* e = std::getenv("PHG_TAIL"); return e && std::atoi(e) == 0; }();
         const int mode = h->tail_req;
         h->tail_req = 0;
-        // (P <= 512: the metric's per-rank ratios fit the wave's LDS; every variant's LDS holds the
+        // (P <= 128: the metric's per-rank values fit the wave's LDS; every variant's LDS holds the
         // 1 024 doubles of a segment's staging array)
         if (mode && !tail_off && h->local_variant >= 0 && a.fold_w && a.gate && !o->fix_nonants && !a.prof &&
-            h->ph.P <= 512 && pdhg_local_lds_bytes(h->local_variant) >= 1024 * sizeof(double)) {
+            h->ph.P <= 128 && pdhg_local_lds_bytes(h->local_variant) >= 1024 * sizeof(double)) {
             if (mode == 1 && !h->xbar_next && dalloc(h, &h->xbar_next, 2 * (size_t)std::max(1, h->N_tot))) return -1;
             TailArgs& t = a.tl;
             t.mode = mode;

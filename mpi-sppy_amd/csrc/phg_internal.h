@@ -252,7 +252,7 @@ struct TailArgs {
     unsigned* done;          // [1] units finished
     const int* scen_seg;     // [S*L] node segment of scenario s at level l
     const int* scen_cseg;    // [S] conv segment of scenario s
-    const int* fin;          // [5 n_fin] final slots {element, first segment, terms, stride T, position}
+    const int* fin;          // [4 n_fin] final slots (int4) {element, first segment, terms | stride T << 16, position}
     int n_fin;
     unsigned long long* prof;   // diagnostic (PHG_TAIL_PROF): [3] s_memrealtime stamps, or null
     double* out;             // [2 N_tot node sums | 2P+2 partials | flag]
@@ -372,6 +372,21 @@ __device__ __forceinline__ KP kargs() {
     KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(p));
     return p;
+}
+
+// The convergence gate for the host: three values, then the sequence number `seq` the host polls,
+// into slot seq mod 2 of the fine-grained pinned ring gh[2][4].  Every store is a system-scope
+// relaxed store (write-through to host memory: sc0 sc1), and the values are drained (s_waitcnt
+// vmcnt(0)) before seq is stored -- so seq never overtakes them, without the system-scope release
+// (__threadfence_system / a release store: a write-back of the whole XCD L2, several microseconds
+// after a solve has dirtied megabytes of it).  Called by one lane.
+__device__ __forceinline__ void publish_host_gate(double* gh_ring, double v0, double v1, double v2, double seq) {
+    double* gh = gh_ring + 4 * ((long long)seq & 1);
+    __hip_atomic_store(&gh[0], v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&gh[1], v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&gh[2], v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&gh[3], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // relative-gap denominator of the termination test (PdhgArgs::gap_const): K = the objective constant.
