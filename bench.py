@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--scen", type=int, default=None,
                     help="scenarios PER GPU (weak scaling); default 10000 farmer, 2048 sslp, 1024 netdes, 2000 hydro, 64 uc")
     ap.add_argument("--cm", type=int, default=10)
+    ap.add_argument("--instance", default=None,
+                    help="sslp / netdes instance (default sslp_15_45_10 / network-50-30-H-01; held out: "
+                         "sslp_5_25_50, network-10-20-H-01)")
     ap.add_argument("--rho", type=float, default=None,
                     help="PH default rho (default 1.0; netdes 10000, the reference's netdes_demo.bash:6 "
                          "--default-rho: PH conv < 1e-4 in 33 s there, 4.3e-3 after 60 s at 1.0)")
@@ -54,6 +57,11 @@ def parse():
     ap.add_argument("--eps", type=float, default=None,
                     help="PDHG relative KKT tolerance (default 1e-9; uc 1e-7, where its bounds are within the "
                          "north star's 1e-6 -- at n ~ 2e4 PDHG needs > 2e5 iterations per solve for 1e-9)")
+    ap.add_argument("--eps-schedule", default=None,
+                    help="conv-keyed PDHG tolerance schedule 'conv:eps,conv:eps,...' (PHBase pdhg_eps_schedule: "
+                         "the first pair whose conv the last known convergence metric reaches, never loosening), "
+                         "e.g. '1e-2:1e-5,1e-3:1e-6,0:1e-7'; the solver-option mechanism of the reference's Gapper "
+                         "(extensions/mipgapper.py:15-60) keyed by conv instead of the iteration")
     ap.add_argument("--conv-iters", type=int, default=20000, help="PH iteration cap for time-to-conv (0: skip)")
     ap.add_argument("--conv-time", type=float, default=120.0,
                     help="wall cap (s) for time-to-conv (PHBase time_limit; not set for farmer, whose "
@@ -133,8 +141,9 @@ def _case_setup(args, S, farmer, hydro, netdes, sslp, uc=None):
         ckw = {"crops_multiplier": args.cm, "num_scens": S}
         desc = f"farmer crops_multiplier={args.cm}"
     elif args.case == "sslp":
-        names, creator, ckw = sslp.scenario_names_creator(S), sslp.scenario_creator, {}
-        desc = "sslp_15_45_10 LP relaxation"
+        inst = args.instance or "sslp_15_45_10"
+        names, creator, ckw = sslp.scenario_names_creator(S), sslp.scenario_creator, {"instance": inst}
+        desc = f"{inst} LP relaxation"
     elif args.case == "hydro":
         fan = hydro.synthetic_fanouts(S)
         names, creator, ckw = hydro.scenario_names_creator(S), hydro.synthetic_scenario_creator, {"fanouts": fan}
@@ -146,8 +155,9 @@ def _case_setup(args, S, farmer, hydro, netdes, sslp, uc=None):
         if args.uc_rho == "cost":
             desc += ", cost-based rho (the reference's uc rho setter)"
     else:
-        names, creator, ckw = netdes.scenario_names_creator(S), netdes.scenario_creator, {"num_scens": S}
-        desc = "netdes network-50-30-H-01 LP relaxation"
+        inst = args.instance or "network-50-30-H-01"
+        names, creator, ckw = netdes.scenario_names_creator(S), netdes.scenario_creator, {"num_scens": S, "instance": inst}
+        desc = f"netdes {inst} LP relaxation"
     return names, creator, ckw, nodenames, desc
 
 
@@ -234,6 +244,10 @@ def main():
             "pdhg_keep_omega": {None: None, "fresh": False, "carry": True, "blend": "blend"}[args.keep_omega],
             "iterk_solver_options": {"pdhg_eps": args.eps}, "iter0_solver_options": {"pdhg_eps": args.eps},
             "pdhg_exchange": force_dist}
+    if args.eps_schedule:
+        opts["pdhg_eps_schedule"] = [tuple(float(v) for v in pair.split(":")) for pair in args.eps_schedule.split(",")]
+        # Iter0 (no metric yet) at the schedule's first tolerance, as a Gapper's key 0 would set it
+        opts["iter0_solver_options"] = {"pdhg_eps": opts["pdhg_eps_schedule"][0][1]}
     args.creator_kwargs = ckw
     t_setup = time.perf_counter()
     rho_setter = uc.rho_setter if args.case == "uc" and args.uc_rho == "cost" else None
@@ -441,7 +455,7 @@ def main():
                        "seeded generator data, per-scenario demand and unit derates",
                  }[args.case],
         "config": {"workload": f"{desc}, {S} scenarios ({args.scen} per GPU), PH rho={args.rho}, "
-                               f"PDHG eps_rel={args.eps}",
+                               f"PDHG eps_rel={args.eps}" + (f", eps schedule {args.eps_schedule}" if args.eps_schedule else ""),
                    "scenarios": S, "n": b.n, "m": b.m, "nnz": b.nnz, "nonants": b.N,
                    "parallelism": f"scenario shards over {world} GPU(s), one packed all-reduce per PH iteration"
                        + (" (libphg RCCL group)" if type(comm).__name__ == "PhgGroupComm" else ""),
@@ -568,6 +582,7 @@ def main():
         if comm is not None:
             comm.barrier()
         tc = time.perf_counter()
+        tc0 = tc
         conv2, _, tb2 = ph2.ph_main(finalize=False)
         torch.cuda.synchronize()
         tc = time.perf_counter() - tc
@@ -582,6 +597,15 @@ def main():
                "scaling": "strong (the same instance at every N)",
                "trivial_bound": tb2, "Eobj": eobj, "cap_iters": args.conv_iters,
                "cap_s": copts["time_limit"]}
+        hist = list(getattr(ph2, "conv_history", []))
+        if hist:   # the metric along the run (every ~1/20 of it) and the schedule's last tolerance
+            step = max(1, len(hist) // 20)
+            ttc["conv_trace"] = [[k + 1, float(hist[k])] for k in range(0, len(hist), step)] + [[len(hist), float(hist[-1])]]
+        wt = getattr(ph2, "iter_walltimes", [])
+        if len(wt) >= 20:
+            ttc["seconds_iter0_and_first_20_ph_iters"] = round(wt[19] - tc0, 3)
+        if args.eps_schedule:
+            ttc["final_pdhg_eps"] = (ph2.current_solver_options or {}).get("pdhg_eps")
         # inner bound of the converged root xbar (every scenario's nonants fixed to it, W / prox off:
         # xhat_eval.py:102-170) and the gaps to the EF optimum of the same instance
         if b.L == 1:

@@ -610,6 +610,7 @@ class PHBase(SPBase):
         self.conv = None
         max_iterations = int(self.options["PHIterLimit"])
         self.conv_history = []
+        self.iter_walltimes = []    # perf_counter at the end of every PH iteration (diagnostics)
         pipelined = self._can_pipeline()
         self._spec_pending = False
         for self._PHIter in range(1, max_iterations + 1):
@@ -666,6 +667,7 @@ class PHBase(SPBase):
                     break
             if self.extobject is not None:
                 self.extobject.enditer_after_sync()
+            self.iter_walltimes.append(time.perf_counter())
             if dprogress and self.cylinder_rank == 0:
                 print("")
                 print("After PH Iteration", self._PHIter)

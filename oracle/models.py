@@ -236,9 +236,9 @@ def _npz(name):
     return {k: z[k] for k in z.files}
 
 
-def sslp(scenario_name, penalty=1000.0):
+def sslp(scenario_name, penalty=1000.0, instance="sslp_15_45_10"):
     k = extract_num(scenario_name)
-    d = _npz("sslp_15_45_10.npz")
+    d = _npz(f"{instance}.npz")
     P = d["client_present"]
     if 1 <= k <= P.shape[0]:
         present = P[k - 1].astype(float)
@@ -274,9 +274,9 @@ def sslp_names(num_scens, start=1):
 # ------------------------------------------------------------------------------------------------
 # netdes LP relaxation: examples/netdes/netdes.py:39-80 + parse.py, instance network-50-30-H-01
 # ------------------------------------------------------------------------------------------------
-def netdes(scenario_name, num_scens=None):
+def netdes(scenario_name, num_scens=None, instance="network-50-30-H-01"):
     k = extract_num(scenario_name)
-    d = _npz("network-50-30-H-01.npz")
+    d = _npz(f"{instance}.npz")
     K = d["p"].shape[0]
     base = k % K
     dk, uk, bk = d["d"][base].copy(), d["u"][base].copy(), d["b"][base]

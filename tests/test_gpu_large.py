@@ -42,6 +42,45 @@ CASES = {
 }
 
 
+# held-out instances: the round-5 per-layout defaults were swept on the two
+# instances above only
+HELDOUT = {
+    "sslp_5_25_50": (lambda S: sslp.scenario_names_creator(S), sslp.scenario_creator, {"instance": "sslp_5_25_50"},
+                     lambda S: om.sslp_names(S), om.sslp, {"instance": "sslp_5_25_50"}),
+    "network-10-20-H-01": (lambda S: netdes.scenario_names_creator(S), netdes.scenario_creator,
+                           {"num_scens": 4, "instance": "network-10-20-H-01"},
+                           lambda S: om.netdes_names(S), om.netdes, {"num_scens": 4, "instance": "network-10-20-H-01"}),
+}
+
+
+@pytest.mark.parametrize("case", sorted(HELDOUT))
+def test_heldout_iter0_and_prox_qp_vs_oracle(case):
+    """The held-out sslp_5_25_50 / network-10-20-H-01 LP relaxations on whatever layout AUTO picks:
+    Iter0 objectives and bounds at 1e-6 against HiGHS, then two prox-QP rounds with the oracle's W /
+    x-bar fed to the device: nonants at 1e-5, objectives at 1e-6."""
+    S = 4
+    pn, pc, pkw, on, oc, okw = HELDOUT[case]
+    ph = PH(_opts(), pn(S), pc, scenario_creator_kwargs=pkw)
+    ph.PH_Prep()
+    tb = ph.Iter0()
+    o = oph.OraclePH(_opts(), on(S), oc, okw)
+    otb = o.Iter0()
+    assert abs(tb - otb) <= 1e-6 * max(1.0, abs(otb)), (ph.engine.layout, tb, otb)
+    np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6, atol=1e-6)
+    assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all()
+    for it in range(2):
+        o.Compute_Xbar()
+        o.Update_W()
+        ph.engine.set(_lib.F_W, o.W.ravel())
+        ph.engine.set(_lib.F_XBAR, o.xbar[0])
+        ph.solve_loop()
+        o.solve_loop()
+        xg = ph.nonants()
+        xo = np.array([o.nonants(k) for k in range(S)])
+        np.testing.assert_allclose(xg, xo, rtol=1e-5, atol=1e-5 * max(1.0, float(np.abs(xo).max())))
+        np.testing.assert_allclose(ph.engine.get(_lib.F_OBJ), o.obj, rtol=1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("case,S", [("sslp", 4), ("netdes", 3)])
 def test_iter0_lp_block_kernel(case, S):
     pn, pc, pkw, on, oc, okw = CASES[case]

@@ -1,0 +1,56 @@
+"""GPU: solver-tolerance schedules.  The reference lets extensions set the
+solver's tolerance per PH iteration through ``current_solver_options`` (the Gapper,
+``mpisppy/extensions/mipgapper.py:15-60``); here the Gapper drives ``pdhg_eps`` and runs inside the
+pipelined loop, and PHBase's built-in conv-keyed ``pdhg_eps_schedule`` does the same from the
+convergence metric.  Loose early solves must not change where PH ends up: the scheduled runs reach
+conv < 1e-4 on farmer cm=10 x 1 000 with E[obj] and x-bar within 1e-6 (relative) of the fixed-eps
+run, with fewer PDHG iterations in all."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from mpisppy_amd import _lib  # noqa: E402
+from mpisppy_amd.examples import farmer  # noqa: E402
+from mpisppy_amd.extensions.gapper import Gapper  # noqa: E402
+from mpisppy_amd.ph import PH  # noqa: E402
+
+S = 1000
+
+
+def _run(**extra):
+    opts = {"solver_name": "phg", "PHIterLimit": 20000, "defaultPHrho": 1.0, "convthresh": 1e-4,
+            "verbose": False, "display_progress": False,
+            "iter0_solver_options": {"pdhg_eps": 1e-9}, "iterk_solver_options": {"pdhg_eps": 1e-9}}
+    ext = extra.pop("extensions", None)
+    opts.update(extra)
+    ph = PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator,
+            scenario_creator_kwargs={"crops_multiplier": 10, "num_scens": S}, extensions=ext)
+    ph.PH_Prep()
+    ph.engine.timing_reset(solves=True)
+    conv, eobj, tb = ph.ph_main(finalize=True)
+    _ms, _n, iters = ph.engine.timing(0)
+    return ph, conv, eobj, ph.xbars().copy(), iters
+
+
+def test_eps_schedules_reach_the_fixed_eps_answer():
+    ref, c0, e0, xb0, it0 = _run()
+    assert c0 < 1e-4
+    runs = {
+        "conv-keyed": _run(pdhg_eps_schedule=[(1e-2, 1e-6), (1e-3, 1e-7), (0.0, 1e-9)]),
+        # the reference's extension, iteration-keyed, in the pipelined loop (pipeline_safe)
+        "gapper": _run(extensions=Gapper, gapperoptions={"mipgapdict": {0: 1e-6, 200: 1e-7, 1000: 1e-9},
+                                                         "solver_option": "pdhg_eps"}),
+    }
+    for name, (ph, c, e, xb, it) in runs.items():
+        assert c < 1e-4, name
+        assert ph._can_pipeline(), name
+        assert abs(e - e0) <= 1e-6 * abs(e0), (name, e, e0)
+        np.testing.assert_allclose(xb, xb0, rtol=1e-6, atol=1e-6 * float(np.abs(xb0).max()))
+        assert ph.current_solver_options["pdhg_eps"] == 1e-9, name   # ended at the tight tolerance
+        assert it < it0, (name, it, it0)
+        assert (ph.engine.get_i32(_lib.I_STATUS) == 0).all(), name

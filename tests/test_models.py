@@ -109,6 +109,32 @@ def test_netdes_sizes_and_balance():
     assert abs(a["row_lo"][1470:].sum()) < 1e-9       # flow balance: sum of node demands is zero
 
 
+@pytest.mark.parametrize("sn", ["Scenario1", "Scenario25", "Scenario50", "Scenario51", "Scenario512"])
+def test_sslp_heldout_bit_exact(sn):
+    """the held-out sslp_5_25_50 (reference examples/sslp/data/sslp_5_25_50),
+    picked by name or by the reference's data_dir."""
+    from mpisppy_amd.examples import sslp
+    _same(sslp.scenario_creator(sn, instance="sslp_5_25_50"), om.sslp(sn, instance="sslp_5_25_50"))
+    m = sslp.scenario_creator(sn, data_dir="examples/sslp/data/sslp_5_25_50/scenariodata")
+    _same(m, om.sslp(sn, instance="sslp_5_25_50"))
+    assert (m.n, m.m) == (5 + 125 + 5, 5 + 25) and len(m._mpisppy_node_list[0].nonant_vardata_list) == 5
+
+
+@pytest.mark.parametrize("sn,S", [("Scenario0", None), ("Scenario19", None), ("Scenario20", 64), ("Scenario300", 512)])
+def test_netdes_heldout_bit_exact(sn, S):
+    """The held-out network-10-20-H-01 (reference examples/netdes/data), by name or by its path."""
+    from mpisppy_amd.examples import netdes
+    mp = netdes.scenario_creator(sn, num_scens=S, instance="network-10-20-H-01")
+    o = om.netdes(sn, num_scens=S, instance="network-10-20-H-01")
+    _same(mp, o)
+    assert mp._mpisppy_probability == o.prob
+    mq = netdes.scenario_creator(sn, path="examples/netdes/data/network-10-20-H-01.dat", num_scens=S)
+    _same(mq, o)
+    a = mp.arrays()
+    E = len(mp._mpisppy_node_list[0].nonant_vardata_list)
+    assert mp.n == 2 * E and mp.m == E + 10 and abs(a["row_lo"][E:].sum()) < 1e-9
+
+
 @pytest.mark.parametrize("fan", [(50, 150, 300), (2, 1, 4)])
 def test_hydro_synthetic_tree_bit_exact(fan):
     S = sum(fan)

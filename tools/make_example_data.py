@@ -1,9 +1,10 @@
 """Extract the example instance DATA the GPU box needs (it has no /root/reference) into compact
 npz files under mpi-sppy_amd/examples/data/ (data only -- no reference code is copied):
 
-* sslp_15_45_10: examples/sslp/data/sslp_15_45_10/scenariodata/Scenario{1..10}.dat
-  (NumServers, NumClients, Capacity, FixedCost, Revenue, Demand, ClientPresent per scenario)
-* network-50-30-H-01: examples/netdes/data/network-50-30-H-01.dat (file format of
+* sslp_15_45_10 and (held-out, round 6) sslp_5_25_50: examples/sslp/data/<inst>/scenariodata/
+  Scenario{1..K}.dat (NumServers, NumClients, Capacity, FixedCost, Revenue, Demand, ClientPresent
+  per scenario)
+* network-50-30-H-01 and (held-out, round 6) network-10-20-H-01: examples/netdes/data/<inst>.dat (file format of
   examples/netdes/parse.py:21-64: header, N, density, ratio, adjacency, first-stage cost, K,
   probabilities, then K x (variable cost matrix, capacity matrix, demand vector)); stored per edge
   in the row-major edge order np.where(A > 0) gives.
@@ -11,6 +12,7 @@ npz files under mpi-sppy_amd/examples/data/ (data only -- no reference code is c
 Usage: python tools/make_example_data.py [reference_root]
 """
 import os
+import re
 import sys
 
 import numpy as np
@@ -53,9 +55,10 @@ def read_dat_params(path):
     return out
 
 
-def sslp(ref):
-    d = os.path.join(ref, "examples", "sslp", "data", "sslp_15_45_10", "scenariodata")
-    scen = [read_dat_params(os.path.join(d, f"Scenario{k}.dat")) for k in range(1, 11)]
+def sslp(ref, inst="sslp_15_45_10"):
+    d = os.path.join(ref, "examples", "sslp", "data", inst, "scenariodata")
+    K = len([f for f in os.listdir(d) if re.fullmatch(r"Scenario\d+\.dat", f)])
+    scen = [read_dat_params(os.path.join(d, f"Scenario{k}.dat")) for k in range(1, K + 1)]
     p0 = scen[0]
     ns, nc = int(p0["NumServers"]), int(p0["NumClients"])
     for p in scen[1:]:   # only ClientPresent differs between scenarios
@@ -65,7 +68,7 @@ def sslp(ref):
     rev = np.array([[p0["Revenue"].get((i, j), 0.0) for j in range(1, ns + 1)] for i in range(1, nc + 1)])
     dem = np.array([[p0["Demand"].get((i, j), 0.0) for j in range(1, ns + 1)] for i in range(1, nc + 1)])
     pres = np.array([[p["ClientPresent"].get(i, 1.0) for i in range(1, nc + 1)] for p in scen])
-    np.savez_compressed(os.path.join(OUT, "sslp_15_45_10.npz"), capacity=np.array(p0["Capacity"]),
+    np.savez_compressed(os.path.join(OUT, f"{inst}.npz"), capacity=np.array(p0["Capacity"]),
                         fixed_cost=fixed, revenue=rev, demand=dem, client_present=pres)
 
 
@@ -98,7 +101,9 @@ def netdes(ref, inst="network-50-30-H-01"):
 if __name__ == "__main__":
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     os.makedirs(OUT, exist_ok=True)
-    sslp(ref)
-    netdes(ref)
+    for inst in ("sslp_15_45_10", "sslp_5_25_50"):
+        sslp(ref, inst)
+    for inst in ("network-50-30-H-01", "network-10-20-H-01"):
+        netdes(ref, inst)
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
