@@ -1047,6 +1047,9 @@ static const LocalVariant kLocalVariants[] = {
     PHG_L(64, 4, 2, 1),
     PHG_L(64, 4, 3, 1),
     PHG_L(64, 4, 4, 2),
+    // one column per lane, every row a coupling row: small dense-coupled scenarios (hydro,
+    // examples/hydro/hydro.py:79-152: 16 columns, 10 rows, every row spanning 2-5 stages' columns)
+    PHG_L(16, 1, 1, 10),
     // farmer (examples/farmer/farmer.py:157-203): per crop lane, columns DevotedAcreage, SubQuota,
     // SuperQuota, Purchased; rows cattle feed (all four) and limit sold (no Purchased); the
     // total-acreage coupling row on DevotedAcreage only
@@ -1061,6 +1064,8 @@ static const LocalVariant kLocalVariants[] = {
     PHG_LM1(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
     PHG_LM1(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
     PHG_LM1(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
+    // hydro's: no row local to a lane (the block slot dropped), all 10 coupling slots
+    PHG_LM1(16, 1, 1, 10, 0x0u, 0x3FFu, 0ull, 0ull, 0x1u),
 };
 #undef PHG_FARMER_BI
 #undef PHG_FARMER_BF
@@ -1068,7 +1073,7 @@ static const LocalVariant kLocalVariants[] = {
 #undef PHG_LM
 #undef PHG_LM1
 #undef PHG_LK
-constexpr int kLocalShapes = 9;   // the generic entries; the planner walks these
+constexpr int kLocalShapes = 10;   // the generic entries; the planner walks these
 
 int pdhg_local_num_variants() { return kLocalShapes; }
 

@@ -882,9 +882,17 @@ static void local_slot_masks(const LocalPlan& plan, const int* sh, unsigned* mb,
     }
 }
 
+// Shapes the default policy may take.  The all-coupling shape (one column per lane, up to 10
+// replicated coupling rows: hydro) is correct but measured 3x slower than the wave-gather kernel on
+// hydro 500-4 000 (0.966 vs 0.316 ms per PH iteration at 2 000: every row an all-reduce over 16 lanes
+// each iteration, and twice the gather kernel's slowest solve; profiles/r06/hydro_layouts.json), so
+// only an explicit PHG_LAYOUT_LOCAL gets it.
+static bool local_shape_default(const int* sh) { return sh[3] <= 2; }
+
 static int pick_local_variant(const phg_batch* b, LocalPlan& plan, int* sh) {
     for (int v = 0; v < pdhg_local_num_variants(); ++v) {
         pdhg_local_variant_shape(v, sh);
+        if (!local_shape_default(sh)) continue;
         const int r = plan_local(b, sh[0], sh[1], sh[2], sh[3], plan);
         if (r < 0) return -2;
         if (r == 0) return v;
@@ -892,11 +900,12 @@ static int pick_local_variant(const phg_batch* b, LocalPlan& plan, int* sh) {
     return -1;
 }
 
-static int build_local_layout(phg_handle* h, const phg_batch* b) {
+static int build_local_layout(phg_handle* h, const phg_batch* b, bool any_shape) {
     int sh[4];
     LocalPlan plan;
     for (int v = 0; v < pdhg_local_num_variants(); ++v) {
         pdhg_local_variant_shape(v, sh);
+        if (!any_shape && !local_shape_default(sh)) continue;
         const int r = plan_local(b, sh[0], sh[1], sh[2], sh[3], plan);
         if (r < 0) return -1;
         if (r > 0) continue;
@@ -2383,7 +2392,7 @@ int phg_load_batch(phg_handle* h, const phg_batch* b_arg) {
         if (h->mfma_variant >= 0) lr = gr = br = 0;
     }
     if (h->mfma_variant < 0 && (pol == PHG_LAYOUT_AUTO || pol == PHG_LAYOUT_LOCAL)) {
-        lr = build_local_layout(h, b);
+        lr = build_local_layout(h, b, pol == PHG_LAYOUT_LOCAL);
         if (lr < 0) return -1;
         if (lr > 0 && pol == PHG_LAYOUT_LOCAL) return -1;
     }

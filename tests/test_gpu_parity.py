@@ -176,7 +176,7 @@ def test_prox_qp_solves_vs_oracle(S, cm, layout):
 
 
 @pytest.mark.parametrize("check_every", [32, 64])
-@pytest.mark.parametrize("layout", ["gather", "block", "mfma"])
+@pytest.mark.parametrize("layout", ["gather", "block", "mfma", "local"])
 @pytest.mark.parametrize("tree", ["bf33", (2, 1, 4), (5, 15, 30)])
 def test_hydro_prox_qp_solves_vs_oracle(tree, layout, check_every):
     """Multistage prox-QPs with identical W and per-NODE xbar in both solvers (the xbar slot of each
