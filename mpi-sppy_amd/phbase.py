@@ -54,11 +54,11 @@ def check_every_default(layout, threads=0):
     5: 0.565 vs 0.688 ms per PH iteration; 96 / 128: 0.80 / 0.77 ms; its round-2 parity miss at 64
     predates the gap test on the whole objective), 32 elsewhere (farmer: 40 / 48 / 64 cost time to
     conv)."""
-    if layout == "block" and 0 < threads <= 256:
-        # 256-thread workgroups (sslp's register-resident pieces): 96 with the block kernel's
-        # artificial-restart fraction 0.15 -- 5.14 vs 5.25-5.27 ms per PH iteration at 4 096 (128:
-        # 5.43); netdes' 1 024-thread kernel stays at 64 (96: 8.56 vs 8.04 ms) -- round 5
-        return 96
+    # (Round 5 gave the 256-thread block kernel 96 with an artificial-restart fraction of 0.15, from
+    # the per-iteration time of sslp_15_45_10 early in PH.  Held out, round 6 (profiles/r06/heldout_ab.json):
+    # on sslp_5_25_50 the pair reached conv 1.3e-3 in 120 s against 4.1e-4 at 64 / 0.25 (23.7 vs
+    # 13.2 ms per PH iteration over the run; 96 alone: 1.3e-2 in 60 s), and on sslp_15_45_10 itself
+    # the time to conv was 27.7 vs 26.2 s -- so it is gone.)
     return 64 if layout in ("gather", "block", "mfma") else 32
 
 
@@ -74,8 +74,9 @@ def beta_artificial_default(layout, threads=0):
     sweeps on MI355X (`profiles/r05/betaart/`, `profiles/r05/uc/sweep/`):
     * bordered / range-split (UC 64, eps 1e-7): PDLP's 0.36 -- 477 vs 581 ms per PH iteration
       (0.5: 478, 0.6: 507, 0.8: 536);
-    * workgroup block (sslp 4 096): 0.15 -- 5.24-5.26 vs 5.46-5.47 ms per PH iteration, 1 096 vs
-      1 145 PDHG iterations per solve (0.1: 5.44, 0.2: 5.26, 0.36: 6.10); netdes within noise;
+    * workgroup block: the library's 0.25.  (Round 5's 0.15 for 256-thread workgroups -- 5.24-5.26
+      vs 5.46-5.47 ms per PH iteration on sslp 4 096 -- lost the time to PH conv on the held-out
+      sslp_5_25_50 and on sslp_15_45_10 itself in round 6: see check_every_default);
     * wave gather (hydro 2 000): per iteration 0.15 -- 0.318 vs 0.325 ms (0.1: 0.315, 0.36: 0.353),
       but see below;
     * lane-local (farmer 10k): the library's 0.25 (0.15: 0.2924, 0.2: 0.2897, 0.36: 0.3009 vs
@@ -85,8 +86,6 @@ def beta_artificial_default(layout, threads=0):
     Time to PH conv decides where the per-iteration gain does not carry over: the gather kernel's
     0.15 made hydro 2 000's conv leg 0.141 vs 0.030 s over the same 105 PH iterations, and netdes'
     1 024-thread block kernel converged in 37.3 vs 32.8 s -- both keep the library's 0.25."""
-    if layout == "block":
-        return 0.15 if 0 < threads <= 256 else 0.0
     return {"border": 0.36, "stream": 0.36, "wave": 0.15}.get(layout, 0.0)
 
 
