@@ -171,7 +171,9 @@ enum {
 };
 enum {
     PHG_I_ITERS = 0,    /* [S] PDHG iterations of the last solve                           */
-    PHG_I_STATUS = 1    /* [S] 0 optimal (KKT <= eps), 1 iteration limit, 2 numerical error */
+    PHG_I_STATUS = 1,   /* [S] 0 optimal (KKT <= eps), 1 iteration limit, 2 numerical error */
+    PHG_I_ORDER = 2     /* [S] launch order of the next solve (heaviest first; a due schedule is
+                           computed first).  Undefined until the first scheduled solve          */
 };
 
 int  phg_create(int device, phg_handle** out);

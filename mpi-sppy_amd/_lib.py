@@ -44,7 +44,7 @@ class PhgOpts(C.Structure):
 
 (F_X, F_Y, F_XN, F_W, F_RHO, F_XBAR, F_XSQBAR, F_OBJ, F_BOUND, F_EVAL, F_KKT, F_FIXED, F_CONV_PART, F_OMEGA,
  F_Z, F_SMOOTH_P, F_SMOOTH_BETA, F_WARM) = range(18)
-I_ITERS, I_STATUS = 0, 1
+I_ITERS, I_STATUS, I_ORDER = 0, 1, 2
 
 # every symbol include/phg.h declares, with its ctypes signature
 SIGNATURES = {

@@ -15,6 +15,7 @@
 
 #include "phg_internal.h"
 #include "ph_sums.h"
+#include "schedule.h"
 
 namespace phg {
 
@@ -95,8 +96,8 @@ __device__ void conv_gate_block(const double* convpart, int P, double* gate, dou
 // does not depend on which workgroup holds it.  The K ranked workgroups spin only on arrivals of
 // workgroups that are already running (K is far below the resident capacity).  finish_k() re-arms
 // the counters for the next launch once all K are done.
-__device__ __forceinline__ int last_k_workgroups(unsigned* counter, int K) {
-    const int total = (int)(gridDim.x * gridDim.y);
+// (total: the workgroups that take a ticket -- the whole grid unless it carries extra ones)
+__device__ __forceinline__ int last_k_workgroups(unsigned* counter, int K, int total) {
     __shared__ int s_rank;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -251,14 +252,27 @@ __device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* con
 // the K ranks to finish (every node sum published) reduces the conv partials, computes conv
 // exactly as xbar_head_kernel does from the same buffer, publishes the gate and, unless conv is
 // below head_thr, copies the node sums into x-bar / x-sq-bar: one launch instead of two.
+//
+// HEADX with PhArgs::sched_order set: the grid has one more column of workgroups, whose first
+// (blockIdx.x == n_seg, blockIdx.y == 0) computes the next solve's launch order (schedule.h) beside
+// the node sums -- nothing else reads or waits for it in this launch, and it takes no ticket.
 template <bool NTL, bool HEADX>
 __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesum, double head_thr, int first) {
+    if constexpr (HEADX) {
+        if ((int)blockIdx.x >= a.n_seg) {
+            __shared__ int s_cnt[kSchedBuckets];
+            __shared__ int s_wsum[4];
+            if (blockIdx.y == 0) schedule_block<256>(a.sched_iters, a.S, a.sched_unit, a.sched_order, s_cnt, s_wsum);
+            return;
+        }
+    }
     // folded update pending: its conv segments ride along (the packed buffer's partials region)
     if (a.fold_conv && blockIdx.y == 0)
-        for (int b = blockIdx.x; b < a.n_cseg; b += gridDim.x) fold_conv_segment(a, b);
+        for (int b = blockIdx.x; b < a.n_cseg; b += a.n_seg) fold_conv_segment(a, b);
     node_sum_partials<NTL>(a);
-    const int K = min(a.n_final, (int)(gridDim.x * gridDim.y));
-    const int rank = last_k_workgroups(a.ticket, K);
+    const int total = a.n_seg * (int)gridDim.y;
+    const int K = min(a.n_final, total);
+    const int rank = last_k_workgroups(a.ticket, K, total);
     if (rank < 0) return;
     if constexpr (!HEADX) {
         node_sum_final<0>(a, nodesum, rank, K);
@@ -547,7 +561,7 @@ __global__ __launch_bounds__(256) void ph_step_kernel(PhArgs a, double* packed, 
     // K: enough workgroups for the W update (the node sums' own final reduction needs far fewer,
     // PhArgs::n_final), still far below the resident capacity (the ranked ones spin)
     const int K = min(min(128, a.n_cseg), (int)(gridDim.x * gridDim.y));
-    const int rank = last_k_workgroups(a.fticket, K);
+    const int rank = last_k_workgroups(a.fticket, K, (int)(gridDim.x * gridDim.y));
     if (rank < 0) return;
     node_sum_final<1>(a, nodesum, rank, K);
     // the K ranks meet: every node sum / x-bar published (sc1 stores, drained) before the W update
@@ -710,7 +724,7 @@ hipError_t node_sums_launch(const PhArgs& a, double* nodesum, hipStream_t st) {
 // HEADX; one GPU: packed is the handle's own buffer, nothing is exchanged between the two)
 hipError_t node_sums_head_launch(const PhArgs& a, double* packed, double thr, int first, hipStream_t st) {
     const bool ntl = node_sums_nontemporal(a);
-    const dim3 grid(a.n_seg, (a.maxk + 255) / 256);
+    const dim3 grid(a.n_seg + (a.sched_order ? 1 : 0), (a.maxk + 255) / 256);
     if (ntl) hipLaunchKernelGGL((node_sums_kernel<true, true>), grid, dim3(256), 0, st, a, packed, thr, first);
     else hipLaunchKernelGGL((node_sums_kernel<false, true>), grid, dim3(256), 0, st, a, packed, thr, first);
     return hipGetLastError();

@@ -192,6 +192,13 @@ struct phg_handle {
     // 0.364 vs 0.361 ms per PH iteration; same bits either way (test_pipelined_iteration_matches_sequential)
     bool no_fuse = true;
     bool have_order = false;
+    // a launch schedule due (the last solve's iteration counts, sched_src, in units of sched_unit):
+    // carried by the next HEADX node-sum launch (phg_ph_step) or, if a solve comes first, launched
+    // on its own just before it (sched_flush) -- either way it runs between the two solves, as a
+    // launch right behind the solve would
+    bool sched_pending = false;
+    const int* sched_src = nullptr;
+    int sched_unit = 1;
     double* pinned = nullptr;  // page-locked readback buffer (convergence partials)
     // page-locked staging of phg_set's uploads (a ring: each slot reused once its copy has run, so
     // phg_set returns without a stream synchronisation) and of phg_solve_results' one readback
@@ -387,6 +394,18 @@ static void swap_state(phg_handle* h) {
     h->ph.xN = h->xN;          // the PH update kernels read the front copy
     h->ph.status = h->status;
     h->out_stale = true;
+}
+
+// the due launch schedule on a launch of its own (phg_handle::sched_pending)
+// largest shard whose launch schedule rides in the node-sum launch (phg_ph_step)
+constexpr int kSchedFuseMaxS = 4096;
+
+static int sched_flush(phg_handle* h) {
+    if (!h->sched_pending) return 0;
+    h->sched_pending = false;
+    CK(schedule_launch(h->sched_src, h->S, h->sched_unit, h->order, h->stream));
+    h->have_order = true;
+    return 0;
 }
 
 extern "C" {
@@ -2737,7 +2756,9 @@ int phg_get(phg_handle* h, int32_t f, double* out) {
 
 int phg_get_i32(phg_handle* h, int32_t f, int32_t* out) {
     if (!h || !h->loaded) return fail("phg_get_i32: no batch loaded");
-    int* p = f == PHG_I_ITERS ? h->iters : f == PHG_I_STATUS ? h->status : nullptr;
+    CK(hipSetDevice(h->device));
+    if (f == PHG_I_ORDER && sched_flush(h)) return -1;
+    int* p = f == PHG_I_ITERS ? h->iters : f == PHG_I_STATUS ? h->status : f == PHG_I_ORDER ? h->order : nullptr;
     if (!p) return fail("phg_get_i32: unknown field");
     CK(hipMemcpyAsync(out, p, (size_t)h->S * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     CK(hipStreamSynchronize(h->stream));
@@ -2793,6 +2814,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     if (!o) return fail("phg_solve: opts is NULL");
     if (o->check_every <= 0 || o->max_iter <= 0) return fail("phg_solve: bad iteration options");
     CK(hipSetDevice(h->device));
+    if (sched_flush(h)) return -1;
     PdhgArgs a{};
     a.S = h->S; a.n = h->n; a.m = h->m; a.nnz = h->nnz; a.N = h->N; a.n_pad = h->n_pad;
     a.lay = h->lay;
@@ -3067,8 +3089,9 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
     swap_state(h);
     ++h->swaps;
     if (o->schedule && (h->solves % sched_every() == 0 || !h->have_order)) {
-        CK(schedule_launch(h->iters, h->S, a.check_every, h->order, h->stream));
-        h->have_order = true;
+        h->sched_pending = true;
+        h->sched_src = h->iters;   // (this solve's counts: the front copy after the swap)
+        h->sched_unit = a.check_every > 0 ? a.check_every : 1;
     }
     ++h->solves;
     return 0;
@@ -3185,6 +3208,21 @@ int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fu
         a.gate = h->gate;
         a.gate_host = h->gate_host;
         a.gate_seq = (double)(h->wait_seq = ++h->gate_seq);
+        // a due launch schedule rides in this launch as one 256-thread workgroup on small shards,
+        // where it finishes under the node sums (farmer 1 250: 0.1016 vs 0.1039 ms per PH
+        // iteration); at 10 000 it outlasts them (32 vs 15 us) and keeps its own 1 024-thread
+        // launch.  PHG_SCHED_FUSE=0 / 1 forces either (A/B)
+        const char* esf = std::getenv("PHG_SCHED_FUSE");
+        const int sfuse = esf ? std::atoi(esf) : -1;
+        if (h->sched_pending && (sfuse == 1 || (sfuse < 0 && h->S <= kSchedFuseMaxS))) {
+            a.sched_iters = h->sched_src;
+            a.sched_order = h->order;
+            a.sched_unit = h->sched_unit;
+            h->sched_pending = false;
+            h->have_order = true;
+        } else if (sched_flush(h)) {
+            return -1;
+        }
         CK(node_sums_head_launch(a, h->packed, convthresh, first, h->stream));
         h->fold_conv_pending = false;
         if (carry_flushed_partials(h, nullptr)) return -1;

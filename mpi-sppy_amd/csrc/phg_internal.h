@@ -236,6 +236,12 @@ struct PhArgs {
     // reference's break before Update_W, phbase.py:1008-1010); null: no gate
     const double* skip_gate;
     double skip_below;
+    // the launch schedule of the next solve, carried by node_sums_kernel HEADX as one extra
+    // workgroup (blockIdx.x == n_seg; schedule.h) when sched_order is set: the last solve's
+    // iteration counts (sched_iters) in units of its check interval
+    const int* sched_iters;
+    int* sched_order;
+    int sched_unit;
 };
 
 // The PH update fused into the end of a lane-local solve (ph_tail.h): mode 0 off; 1 one GPU (node

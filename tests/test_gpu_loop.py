@@ -81,3 +81,45 @@ def test_ungated_solve_after_converged_head_is_fresh():
     np.testing.assert_array_equal(eng.get(_lib.F_W), W0)     # the flushed update was gated: W unchanged
     # this launch's counts (<= its cap of 32), not the last PH solve's (hundreds at eps 1e-9)
     assert ((it > 0) & (it <= 32)).all(), it
+
+
+def test_launch_schedule_in_the_node_sum_launch():
+    """The next solve's launch order (schedule.h: heaviest first by the last solve's PDHG iterations in
+    check-interval units) computed by the extra workgroup of the pipelined node-sum launch
+    (node_sums_kernel HEADX) or on its own launch (PHG_SCHED_FUSE=0): after every pipelined
+    iteration the order is a permutation of the scenarios whose buckets never increase along it for
+    one of the recent solves' counts, and the two paths give bit-identical PH states."""
+    import os
+    from mpisppy_amd import _lib
+
+    def run(fuse):
+        if fuse:
+            os.environ.pop("PHG_SCHED_FUSE", None)
+        else:
+            os.environ["PHG_SCHED_FUSE"] = "0"
+        try:
+            S = 3000
+            opts = {"solver_name": "phg", "PHIterLimit": 20, "defaultPHrho": 1.0, "convthresh": 1e-10,
+                    "verbose": False, "display_progress": False}
+            ph = PH(opts, farmer.scenario_names_creator(S), farmer.scenario_creator,
+                    scenario_creator_kwargs={"crops_multiplier": 10, "num_scens": S})
+            ph.PH_Prep()
+            ph.Iter0()
+            ph.current_solver_options = ph.iterk_solver_options
+            unit = ph._solver_opts()["pdhg_check_every"]
+            eng = ph.engine
+            recent = [eng.get_i32(_lib.I_ITERS)]
+            for k in range(9):
+                ph.update_and_solve(first=k == 0)
+                recent.append(eng.get_i32(_lib.I_ITERS))   # (a due schedule reads this solve's counts)
+                order = eng.get_i32(_lib.I_ORDER)
+                assert np.array_equal(np.sort(order), np.arange(S)), k
+                bad = [int((np.diff(np.minimum(it // unit, 4095)[order]) > 0).sum()) for it in recent[-5:]]
+                assert min(bad) == 0, (k, fuse, bad)
+            return ph.Ws().copy(), ph.nonants().copy(), ph.xbars().copy()
+        finally:
+            os.environ.pop("PHG_SCHED_FUSE", None)
+
+    a, b = run(True), run(False)
+    for u, v in zip(a, b):
+        np.testing.assert_array_equal(u, v)
