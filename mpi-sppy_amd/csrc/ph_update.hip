@@ -163,9 +163,10 @@ __device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
 
 // final node sums of elements [e_lo, e_hi) (rank `rank` of K): per node, its segments' partials in
 // segment order, written with the given store -- MODE 0: plain; 1: sc1, and x-bar / x-sq-bar too
-// (ph_step_kernel); 2: sc1, node sums only (other workgroups of the same launch read them)
+// (ph_step_kernel); 2: sc1, node sums only (other workgroups of the same launch read them); 3:
+// plain, and x-bar / x-sq-bar too when `xb` (the one-hop HEADX)
 template <int MODE>
-__device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum, int rank, int K) {
+__device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum, int rank, int K, bool xb = false) {
     const int tid = threadIdx.x;
     // elements [e_lo, e_hi) of this rank; T lanes per element (power of two <= 64), each summing
     // every T-th segment of the node, then a fixed xor-butterfly over the T lanes: wide enough to
@@ -198,7 +199,7 @@ __device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum,
             t2 += __shfl_xor(t2, o, 64);
         }
         if (e < e_hi && sub == 0) {
-            if (MODE >= 1) {
+            if (MODE == 1 || MODE == 2) {
                 publish(&nodesum[e], t1);
                 publish(&nodesum[a.N_tot + e], t2);
                 if (MODE == 1) {
@@ -208,6 +209,10 @@ __device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum,
             } else {
                 nodesum[e] = t1;
                 nodesum[a.N_tot + e] = t2;
+                if (MODE == 3 && xb) {
+                    a.xbar[e] = t1;
+                    a.xsqbar[e] = t2;
+                }
             }
         }
     }
@@ -245,6 +250,9 @@ __device__ void fold_conv_segment(const PhArgs& a, int b) {
     __syncthreads();
 }
 
+// virtual ranks up to which the HEADX ranks each form conv themselves (their LDS copy of the partials)
+constexpr int kHeadxOneHopP = 128;
+
 // the last workgroup's part of convergence_diff (declared here, defined below)
 __device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart);
 
@@ -252,6 +260,9 @@ __device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* con
 // the K ranks to finish (every node sum published) reduces the conv partials, computes conv
 // exactly as xbar_head_kernel does from the same buffer, publishes the gate and, unless conv is
 // below head_thr, copies the node sums into x-bar / x-sq-bar: one launch instead of two.
+//
+// (PhArgs::onehop -- PHG_HEADX_ONEHOP, default on -- for up to kHeadxOneHopP virtual ranks: the K ranks skip that second
+// meeting -- each computes conv itself and writes its own elements' x-bar; see below.)
 //
 // HEADX with PhArgs::sched_order set: the grid has one more column of workgroups, whose first
 // (blockIdx.x == n_seg, blockIdx.y == 0) computes the next solve's launch order (schedule.h) beside
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
         if ((int)blockIdx.x >= a.n_seg) {
             __shared__ int s_cnt[kSchedBuckets];
             __shared__ int s_wsum[4];
-            if (blockIdx.y == 0) schedule_block<256>(a.sched_iters, a.S, a.sched_unit, a.sched_order, s_cnt, s_wsum);
+            if (blockIdx.y == 0) schedule_block<256, 4>(a.sched_iters, a.S, a.sched_unit, a.sched_order, s_cnt, s_wsum);
             return;
         }
     }
@@ -284,6 +295,31 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
     } else {
         __shared__ double red256[256];
         __shared__ int s_last;
+        double* convpart = nodesum + 2 * (long)a.N_tot;
+        if (a.onehop && a.P <= kHeadxOneHopP) {
+            // one hop: every rank forms the conv partials and conv itself (conv_partials_final and
+            // conv_value_block over the same inputs in the same fixed order: the same bits in every
+            // rank) and writes the x-bar of its own elements, so the ranks never meet again --
+            // rank 0 stores the partials and publishes the gate; the counters are re-armed by the
+            // last rank out (finish_k)
+            __shared__ double s_cp[2 * kHeadxOneHopP + 3];
+            const int ncp = 2 * a.P + 3;
+            if (a.fold_conv) {
+                conv_partials_final(a, s_cp);
+            } else {
+                for (int i = threadIdx.x; i < ncp; i += 256) s_cp[i] = convpart[i];
+            }
+            __syncthreads();
+            const double conv = first ? INFINITY : conv_value_block(s_cp, a.P, red256);
+            if (rank == 0) {
+                if (a.fold_conv)
+                    for (int i = threadIdx.x; i < ncp; i += 256) convpart[i] = s_cp[i];
+                if (threadIdx.x == 0) publish_gate(conv, s_cp, a.P, a.gate, a.gate_host, a.gate_seq);
+            }
+            node_sum_final<3>(a, nodesum, rank, K, conv >= head_thr);
+            finish_k(a.ticket, a.ticket + 2, K);
+            return;
+        }
         node_sum_final<2>(a, nodesum, rank, K);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -297,7 +333,6 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
         }
         __syncthreads();
         if (!s_last) return;
-        double* convpart = nodesum + 2 * (long)a.N_tot;
         if (a.fold_conv) conv_partials_final(a, convpart);
         __syncthreads();
         const double conv = first ? INFINITY : conv_value_block(convpart, a.P, red256);

@@ -3209,9 +3209,9 @@ int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fu
         a.gate_host = h->gate_host;
         a.gate_seq = (double)(h->wait_seq = ++h->gate_seq);
         // a due launch schedule rides in this launch as one 256-thread workgroup on small shards,
-        // where it finishes under the node sums (farmer 1 250: 0.1016 vs 0.1039 ms per PH
-        // iteration); at 10 000 it outlasts them (32 vs 15 us) and keeps its own 1 024-thread
-        // launch.  PHG_SCHED_FUSE=0 / 1 forces either (A/B)
+        // where it finishes under the node sums (farmer 1 250: 0.1018 / 0.1020 vs 0.1027 / 0.1029 ms
+        // per PH iteration, 2 500: 0.1367 / 0.1376 vs 0.1378 / 0.1382; 5 000 within noise); at
+        // 10 000 it outlasts them (32 vs 15 us) and keeps its own 1 024-thread launch.  PHG_SCHED_FUSE=0 / 1 forces either (A/B)
         const char* esf = std::getenv("PHG_SCHED_FUSE");
         const int sfuse = esf ? std::atoi(esf) : -1;
         if (h->sched_pending && (sfuse == 1 || (sfuse < 0 && h->S <= kSchedFuseMaxS))) {
@@ -3222,6 +3222,10 @@ int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fu
             h->have_order = true;
         } else if (sched_flush(h)) {
             return -1;
+        }
+        {   // PHG_HEADX_ONEHOP=0: the ranks meet a second time and the last forms conv (A/B)
+            const char* eoh = std::getenv("PHG_HEADX_ONEHOP");
+            a.onehop = (eoh && std::atoi(eoh) == 0) ? 0 : 1;
         }
         CK(node_sums_head_launch(a, h->packed, convthresh, first, h->stream));
         h->fold_conv_pending = false;

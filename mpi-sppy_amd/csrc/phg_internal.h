@@ -242,6 +242,8 @@ struct PhArgs {
     const int* sched_iters;
     int* sched_order;
     int sched_unit;
+    // node_sums_kernel HEADX: one hand-off instead of two (every rank forms conv itself)
+    int onehop;
 };
 
 // The PH update fused into the end of a lane-local solve (ph_tail.h): mode 0 off; 1 one GPU (node

@@ -123,3 +123,26 @@ def test_launch_schedule_in_the_node_sum_launch():
     a, b = run(True), run(False)
     for u, v in zip(a, b):
         np.testing.assert_array_equal(u, v)
+
+
+def test_one_hop_node_sum_head_matches_two_hops():
+    """node_sums_kernel HEADX: every rank forming conv itself and writing its own x-bar (one hand-off,
+    the default) gives the state of the two-hand-off form (PHG_HEADX_ONEHOP=0) bit for bit, conv
+    history included."""
+    import os
+    runs = []
+    for v in ("0", None):
+        if v is None:
+            os.environ.pop("PHG_HEADX_ONEHOP", None)
+        else:
+            os.environ["PHG_HEADX_ONEHOP"] = v
+        try:
+            runs.append(_run(True, None, limit=12))
+        finally:
+            os.environ.pop("PHG_HEADX_ONEHOP", None)
+    a, b = runs
+    assert a._PHIter == b._PHIter
+    np.testing.assert_array_equal(a.conv_history, b.conv_history)
+    np.testing.assert_array_equal(a.Ws(), b.Ws())
+    np.testing.assert_array_equal(a.nonants(), b.nonants())
+    np.testing.assert_array_equal(a.xbars(), b.xbars())
