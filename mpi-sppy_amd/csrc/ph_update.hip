@@ -164,9 +164,11 @@ __device__ __forceinline__ void node_sum_partials(const PhArgs& a) {
 // final node sums of elements [e_lo, e_hi) (rank `rank` of K): per node, its segments' partials in
 // segment order, written with the given store -- MODE 0: plain; 1: sc1, and x-bar / x-sq-bar too
 // (ph_step_kernel); 2: sc1, node sums only (other workgroups of the same launch read them); 3:
-// plain, and x-bar / x-sq-bar too when `xb` (the one-hop HEADX)
+// plain, and kept in `stash` (LDS, [2][256]) when the rank has <= 256 elements (the one-hop HEADX
+// writes x-bar from there once it knows conv)
 template <int MODE>
-__device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum, int rank, int K, bool xb = false) {
+__device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum, int rank, int K,
+                                               double* stash = nullptr) {
     const int tid = threadIdx.x;
     // elements [e_lo, e_hi) of this rank; T lanes per element (power of two <= 64), each summing
     // every T-th segment of the node, then a fixed xor-butterfly over the T lanes: wide enough to
@@ -209,9 +211,9 @@ __device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum,
             } else {
                 nodesum[e] = t1;
                 nodesum[a.N_tot + e] = t2;
-                if (MODE == 3 && xb) {
-                    a.xbar[e] = t1;
-                    a.xsqbar[e] = t2;
+                if (MODE == 3 && ne <= 256) {
+                    stash[e - e_lo] = t1;
+                    stash[256 + e - e_lo] = t2;
                 }
             }
         }
@@ -221,14 +223,39 @@ __device__ __forceinline__ void node_sum_final(const PhArgs& a, double* nodesum,
 // Folded W update (PdhgArgs::fold_w): the solve prologue left each scenario's sum |x - xbar|
 // (conv_s) and the status of the solve that produced x (fold_st).  Conv segment b's partials:
 // fixed-order sums over its scenario range, published for conv_partials_final.
-__device__ void fold_conv_segment(const PhArgs& a, int b) {
+// FoldHead: a thread's first element of the segment, loaded ahead (node_sums_kernel issues it before
+// the node-sum pass over x, so the two load latencies overlap) and added in the same order as the loop
+struct FoldHead {
+    double v = 0.0;
+    int st = 0;
+    bool on = false;
+};
+
+__device__ __forceinline__ FoldHead fold_conv_head(const PhArgs& a, int b) {
+    FoldHead h;
+    const int s = a.cseg_s0[b] + (int)threadIdx.x;
+    if (s < a.cseg_s1[b]) {
+        h.v = a.conv_s[s];
+        h.st = a.fold_st[s];
+        h.on = true;
+    }
+    return h;
+}
+
+__device__ void fold_conv_segment(const PhArgs& a, int b, FoldHead h = FoldHead{}, bool pre = false) {
     __shared__ double red[4];
     __shared__ int bad[8];
     const int tid = threadIdx.x;
     const int s0 = a.cseg_s0[b], s1 = a.cseg_s1[b];
+    if (!pre) h = fold_conv_head(a, b);
     double acc = 0.0;
     int nb = 0, nn = 0;
-    for (int s = s0 + tid; s < s1; s += 256) {
+    if (h.on) {
+        acc += h.v;
+        nb += h.st != 0;
+        nn += h.st == 2;
+    }
+    for (int s = s0 + tid + 256; s < s1; s += 256) {
         acc += a.conv_s[s];
         const int st = a.fold_st[s];
         nb += st != 0;
@@ -253,8 +280,30 @@ __device__ void fold_conv_segment(const PhArgs& a, int b) {
 // virtual ranks up to which the HEADX ranks each form conv themselves (their LDS copy of the partials)
 constexpr int kHeadxOneHopP = 128;
 
+// a thread's conv segment (g = vr_first[0] + tid) loaded ahead for conv_partials_final (P = 1,
+// <= 256 segments: one per thread) -- the same element the loop would read, added in the same order
+struct ConvPre {
+    double v = 0.0;
+    int b = 0, n = 0;
+    bool on = false;
+};
+
+__device__ __forceinline__ ConvPre conv_pre_load(const PhArgs& a) {
+    ConvPre p;
+    const int g = a.vr_first[0] + (int)threadIdx.x;
+    if (g < a.vr_first[1]) {
+        p.v = a.csegpart[g];
+        p.on = true;
+    }
+    if ((int)threadIdx.x < a.n_cseg) {
+        p.b = a.csegbad[2 * threadIdx.x];
+        p.n = a.csegbad[2 * threadIdx.x + 1];
+    }
+    return p;
+}
+
 // the last workgroup's part of convergence_diff (declared here, defined below)
-__device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart);
+__device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart, const ConvPre* pre = nullptr);
 
 // HEADX (phg_ph_step on one GPU with the folded update): the x-bar head rides along -- the last of
 // the K ranks to finish (every node sum published) reduces the conv partials, computes conv
@@ -277,10 +326,16 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
             return;
         }
     }
-    // folded update pending: its conv segments ride along (the packed buffer's partials region)
-    if (a.fold_conv && blockIdx.y == 0)
-        for (int b = blockIdx.x; b < a.n_cseg; b += a.n_seg) fold_conv_segment(a, b);
+    // folded update pending: its conv segments ride along (the packed buffer's partials region);
+    // the first one's loads go out before the pass over x
+    const bool fold_here = a.fold_conv && blockIdx.y == 0 && (int)blockIdx.x < a.n_cseg;
+    FoldHead fh;
+    if (fold_here) fh = fold_conv_head(a, blockIdx.x);
     node_sum_partials<NTL>(a);
+    if (fold_here) {
+        fold_conv_segment(a, blockIdx.x, fh, true);
+        for (int b = blockIdx.x + a.n_seg; b < a.n_cseg; b += a.n_seg) fold_conv_segment(a, b);
+    }
     const int total = a.n_seg * (int)gridDim.y;
     const int K = min(a.n_final, total);
     const int rank = last_k_workgroups(a.ticket, K, total);
@@ -302,10 +357,18 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
             // rank) and writes the x-bar of its own elements, so the ranks never meet again --
             // rank 0 stores the partials and publishes the gate; the counters are re-armed by the
             // last rank out (finish_k)
+            // The node sums go first with the conv segments' partials already in flight (P = 1, one
+            // segment per thread: ConvPre), so the two load latencies overlap; x-bar is written
+            // from the LDS stash once conv is known.
             __shared__ double s_cp[2 * kHeadxOneHopP + 3];
+            __shared__ double s_xb[512];
             const int ncp = 2 * a.P + 3;
+            const bool pre = a.fold_conv && a.P == 1 && a.n_cseg <= 256;
+            ConvPre cpre;
+            if (pre) cpre = conv_pre_load(a);
+            node_sum_final<3>(a, nodesum, rank, K, s_xb);
             if (a.fold_conv) {
-                conv_partials_final(a, s_cp);
+                conv_partials_final(a, s_cp, pre ? &cpre : nullptr);
             } else {
                 for (int i = threadIdx.x; i < ncp; i += 256) s_cp[i] = convpart[i];
             }
@@ -316,7 +379,14 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
                     for (int i = threadIdx.x; i < ncp; i += 256) convpart[i] = s_cp[i];
                 if (threadIdx.x == 0) publish_gate(conv, s_cp, a.P, a.gate, a.gate_host, a.gate_seq);
             }
-            node_sum_final<3>(a, nodesum, rank, K, conv >= head_thr);
+            if (conv >= head_thr) {
+                const int e_lo = (int)((long)a.N_tot * rank / K), e_hi = (int)((long)a.N_tot * (rank + 1) / K);
+                const int ne = e_hi - e_lo;
+                for (int i = threadIdx.x; i < ne; i += 256) {
+                    a.xbar[e_lo + i] = ne <= 256 ? s_xb[i] : nodesum[e_lo + i];
+                    a.xsqbar[e_lo + i] = ne <= 256 ? s_xb[256 + i] : nodesum[a.N_tot + e_lo + i];
+                }
+            }
             finish_k(a.ticket, a.ticket + 2, K);
             return;
         }
@@ -351,10 +421,17 @@ __global__ __launch_bounds__(256) void node_sums_kernel(PhArgs a, double* nodesu
 }
 
 // fixed-order sum of v[first..last) by all 256 threads of the workgroup (same result in every thread)
+__device__ __forceinline__ double block_sum_reg(double t, double* red);
 __device__ __forceinline__ double block_sum_range(const double* v, int first, int last, double* red) {
     const int tid = threadIdx.x;
     double t = 0.0;
     for (int g = first + tid; g < last; g += 256) t += v[g];
+    return block_sum_reg(t, red);
+}
+
+// the fixed-order workgroup sum of every thread's t (block_sum_range's tree)
+__device__ __forceinline__ double block_sum_reg(double t, double* red) {
+    const int tid = threadIdx.x;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
     __syncthreads();
@@ -512,14 +589,21 @@ __device__ __forceinline__ void w_update_segment(const PhArgs& a, int b, const d
 
 // the last workgroup's part of convergence_diff: segment partials per virtual rank (fixed order)
 // into convpart[2v], convpart[2v+1] = (sum, count); the status counts; the flag
-__device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart) {
+__device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* convpart, const ConvPre* pre) {
     __syncthreads();
     __shared__ double red[4];
     __shared__ int bad[8];
     const int tid = threadIdx.x;
     for (int v = 0; v < a.P; ++v) {
         const int g0 = a.vr_first[v], g1 = a.vr_first[v + 1];
-        const double t = block_sum_range(a.csegpart, g0, g1, red);
+        double t;
+        if (pre) {   // (P = 1, one segment per thread, loaded ahead)
+            double u = 0.0;
+            if (pre->on) u += pre->v;
+            t = block_sum_reg(u, red);
+        } else {
+            t = block_sum_range(a.csegpart, g0, g1, red);
+        }
         if (tid == 0) {
             convpart[2 * v] = t;
             convpart[2 * v + 1] = g1 > g0 ? (double)(a.cseg_s1[g1 - 1] - a.cseg_s0[g0]) * (double)a.N : 0.0;
@@ -527,7 +611,12 @@ __device__ __forceinline__ void conv_partials_final(const PhArgs& a, double* con
     }
     {
         int tb = 0, tn = 0;
-        for (int g = tid; g < a.n_cseg; g += 256) { tb += a.csegbad[2 * g]; tn += a.csegbad[2 * g + 1]; }
+        if (pre) {
+            tb = pre->b;
+            tn = pre->n;
+        } else {
+            for (int g = tid; g < a.n_cseg; g += 256) { tb += a.csegbad[2 * g]; tn += a.csegbad[2 * g + 1]; }
+        }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             tb += __shfl_xor(tb, o, 64);

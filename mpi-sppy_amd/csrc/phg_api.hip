@@ -1076,7 +1076,9 @@ static int build_ph_tables(phg_handle* h, const phg_batch* b) {
         long loads = 0;
         for (int g = 0; g < b->n_nodes; ++g)   // nodes without local scenarios have no segments
             if (node_level[g] >= 0) loads += 2L * (first[g + 1] - first[g]) * b->level_len[node_level[g]];
-        long per = 2048;   // PHG_NFINAL_LOADS: partial loads per final workgroup (tuning knob)
+        // PHG_NFINAL_LOADS: partial loads per final workgroup (tuning knob; 1 024 from 2 048 in round
+        // 6: farmer 10 000's node-sum head 12.5 vs 13.3 us, K = 10 vs 5 ranks; 1 250 unchanged)
+        long per = 1024;
         if (const char* ev = std::getenv("PHG_NFINAL_LOADS")) per = std::max(1L, std::atol(ev));
         a.n_final = (int)std::min<long>(128, std::max<long>(1, (loads + per - 1) / per));
     }

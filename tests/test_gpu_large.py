@@ -436,8 +436,10 @@ def test_wave_kernel_matches_block_kernel():
     o.Update_W()
     res = {}
     for layout in ("wave", "block"):
-        # the same check interval on both (the default is by layout: phbase.check_every_default)
-        ph = PH(_opts(pdhg_layout=layout, pdhg_check_every=32), sslp.scenario_names_creator(S), sslp.scenario_creator)
+        # the same check interval and artificial-restart fraction on both (the defaults are by
+        # layout: phbase.check_every_default, beta_artificial_default)
+        ph = PH(_opts(pdhg_layout=layout, pdhg_check_every=32, pdhg_beta_artificial=0.15), sslp.scenario_names_creator(S),
+                sslp.scenario_creator)
         ph.PH_Prep()
         assert ph.engine.layout == layout
         ph.Iter0()
