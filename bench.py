@@ -374,12 +374,19 @@ def main():
         except Exception:
             traffic = None
     valu_pmc = None
-    vpath = os.path.join(ROOT, "profiles", "r05", "pmc_valu_r05.json")
+    vpath = os.path.join(ROOT, "profiles", "r06", "pmc_valu_mix.json")
     if args.case == "farmer" and eng.layout == "local" and S_loc == 10000 and os.path.exists(vpath):
         try:
             vj = json.load(open(vpath))
-            valu_pmc = {"valu_issue_utilisation": vj["valu_issue_utilisation"],
-                        "fp64_fma_share_of_valu": vj["fp64_fma_share_of_valu"], "file": "profiles/r05/pmc_valu_r05.json"}
+            im = vj["issue_model"]
+            valu_pmc = {"issue_utilisation": round(im["issue_utilisation"], 4),
+                        "issue_model": "fp64 wave64 instruction 4 SIMD cycles, 32-bit 2",
+                        "fp64_share_of_valu": round(vj["shares_of_valu"]["fp64 (fma/add/mul/trans)"], 4),
+                        "fp64_fma_share_of_valu": round(vj["shares_of_valu"]["fp64 fma"], 4),
+                        "fp64_share_of_issue_cycles": round(im["fp64_cycles_share"], 4),
+                        "valu_per_wave_iteration": round(vj["valu_per_wave_iteration_counted"], 1),
+                        "isa_valu_per_pdhg_iteration": vj["isa_per_pdhg_iteration"]["valu"],
+                        "file": "profiles/r06/pmc_valu_mix.json"}
         except Exception:
             valu_pmc = None
     # PH update, algorithmic bytes:
@@ -474,8 +481,9 @@ def main():
                       "nnz_distinct": nnz_distinct, "tflops_fp64": round(achieved_tf, 4),
                       "valu_frac_fp64": round(achieved_tf / FP64_PEAK_TFLOPS, 5)}) | {
                      "traffic": traffic,
-                     # VALU issue measured by PMC on the headline kernel (profiles/r05/pmc_valu_r05.json:
-                     # VALU instructions x 4 cycles / all SIMDs' cycles over the launch), when this is it
+                     # VALU issue measured by PMC on the headline kernel (profiles/r06/pmc_valu_mix.json:
+                     # class counters priced 4 cycles per fp64 / 2 per 32-bit wave instruction, over all
+                     # SIMDs' cycles of the launch), when this is it
                      "valu_issue_pmc": valu_pmc,
                      # measured HBM rate of the same kernel: PMC bytes per launch / launch duration
                      "hbm_measured_GBs": round(traffic / avg_launch_s / 1e9, 2) if traffic else None,
