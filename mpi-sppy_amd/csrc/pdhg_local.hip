@@ -73,6 +73,9 @@ constexpr size_t local_lds_bytes() {
 #ifndef PHG_LOCAL_WAVES
 #define PHG_LOCAL_WAVES 2
 #endif
+#ifndef PHG_SEQ_CHECK
+#define PHG_SEQ_CHECK 0
+#endif
 
 // (xs dc) - xbar, each operation rounded on its own (the folded W update must see the bits of the
 // epilogue's xN = xs dc)
@@ -264,9 +267,12 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
     // [2] ||pr||^2 unscaled, [3] ||dres||^2 unscaled, [4] primal objective, [5] dual objective.  The iterate is given element-wise (xf, atf: column k; yf, axf: local row r;
     // axdp: coupling row d's LOCAL partial of A x) so the average iterate is never materialised in
     // registers.  Padded column / row slots hold zeros everywhere, so no per-element branches.
-    // element-by-element order in the check (see kkt_part); dropped in the lone-wave build
+    // element-by-element order in the check (see kkt_part); dropped in the lone-wave build, and
+    // since round 6 in the two-wave build too (PHG_SEQ_CHECK=0: the check then fits in 212 VGPRs
+    // without spills; farmer 10k time to conv 0.775-0.777 vs 0.784 s, the same 5 185 PH iterations
+    // and bits, the per-iteration line within noise -- profiles/r06/seq_check_ab.json)
     auto sq = []() {
-        if constexpr (WV > 1) seq();
+        if constexpr (WV > 1 && PHG_SEQ_CHECK) seq();
     };
     constexpr int KT = 5 + DD;   // reduced values per iterate
     // slot of coupling row d's A x partial: 1 (free in the reduced vector), then 6, 7, ...
