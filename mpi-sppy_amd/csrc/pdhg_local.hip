@@ -775,6 +775,8 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         // the running sums of the average iterate take every second iterate only (the average of
         // the even iterates: still an ergodic PDHG average, and a restart candidate like any other
         // point) -- 7 of ~62 fp64 instructions per PDHG iteration on farmer saved in the other step.
+        // (Every fourth iterate, round 6: the xhat evaluation's fixed-nonant solves of farmer 10k
+        // then no longer all reach the tolerance -- test_farmer_converged_ph_vs_ef[10000] -- so no.)
         // The only loop compiled: with the every-iterate and windowed loops beside it the scheduler
         // did worse (end of round 4: 0.2623 vs 0.2666 ms per launch, the same iterations bit for bit)
 #pragma unroll 1
