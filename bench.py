@@ -27,7 +27,7 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 dense peak: the VALU rate (v_fma_f64, 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak
 
 
-DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_r05.json")
+DEFAULT_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_r06.json")
 
 
 def parse():
