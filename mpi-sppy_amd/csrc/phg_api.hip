@@ -397,8 +397,11 @@ static void swap_state(phg_handle* h) {
 }
 
 // the due launch schedule on a launch of its own (phg_handle::sched_pending)
-// largest shard whose launch schedule rides in the node-sum launch (phg_ph_step)
-constexpr int kSchedFuseMaxS = 4096;
+// largest shard whose launch schedule rides in the node-sum launch (phg_ph_step): measured up to
+// farmer 10 000 (the head with the sort 16.0 us on average against 13.6 + 11.1 us every 4th
+// iteration for the two launches; time to conv 0.775 / 0.776 vs 0.781 / 0.780 s); beyond 16 384 the
+// 1 024-thread launch (unmeasured there)
+constexpr int kSchedFuseMaxS = 16384;
 
 static int sched_flush(phg_handle* h) {
     if (!h->sched_pending) return 0;
@@ -3210,10 +3213,10 @@ int phg_ph_step(phg_handle* h, double convthresh, int32_t first, int32_t* out_fu
         a.gate = h->gate;
         a.gate_host = h->gate_host;
         a.gate_seq = (double)(h->wait_seq = ++h->gate_seq);
-        // a due launch schedule rides in this launch as one 256-thread workgroup on small shards,
-        // where it finishes under the node sums (farmer 1 250: 0.1018 / 0.1020 vs 0.1027 / 0.1029 ms
-        // per PH iteration, 2 500: 0.1367 / 0.1376 vs 0.1378 / 0.1382; 5 000 within noise); at
-        // 10 000 it outlasts them (32 vs 15 us) and keeps its own 1 024-thread launch.  PHG_SCHED_FUSE=0 / 1 forces either (A/B)
+        // a due launch schedule rides in this launch as one 256-thread workgroup (up to
+        // kSchedFuseMaxS scenarios): farmer 1 250: 0.1018 / 0.1020 vs 0.1027 / 0.1029 ms per PH
+        // iteration, 2 500: 0.1367 / 0.1376 vs 0.1378 / 0.1382, 10 000: see kSchedFuseMaxS.
+        // PHG_SCHED_FUSE=0 / 1 forces either (A/B)
         const char* esf = std::getenv("PHG_SCHED_FUSE");
         const int sfuse = esf ? std::atoi(esf) : -1;
         if (h->sched_pending && (sfuse == 1 || (sfuse < 0 && h->S <= kSchedFuseMaxS))) {

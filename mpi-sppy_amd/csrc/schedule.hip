@@ -1,6 +1,6 @@
 // schedule.hip -- the scenario launch order for the next batched solve, on its own launch (one
 // 1 024-thread workgroup; the sort itself is schedule.h).  Stream-ordered behind the solve, no host
-// round trip.  On one GPU with the folded update, shards of <= 4 096 scenarios, the pipelined
+// round trip.  On one GPU with the folded update, shards of <= 16 384 scenarios, the pipelined
 // node-sum launch carries the same sort as an extra 256-thread workgroup instead (ph_update.hip
 // node_sums_kernel HEADX, phg_api.hip sched_pending), so no launch of its own is paid there.
 #include "schedule.h"
