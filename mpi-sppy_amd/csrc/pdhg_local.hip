@@ -829,13 +829,17 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         const bool restart = live && ((cand <= a.beta_suf * a.beta_suf * krst) ||
                                       (cand <= a.beta_nec * a.beta_nec * krst && cand > GS(CI::SC + CI::KPREV)) ||
                                       ((double)since >= a.beta_art * (double)it));
-        if constexpr (PROF) {   // PHG_WATCH_SCEN (diagnostic): one scenario's restart / primal-weight history
+#ifdef PHG_LOCAL_WATCH
+        if constexpr (PROF) {   // PHG_WATCH_SCEN (diagnostic build, -DPHG_LOCAL_WATCH): one scenario's
+                                // restart / primal-weight history.  Not in the default PROF build: the
+                                // printf's registers spilled it (~2 KB per lane) and distorted the splits
             if (live && gl == 0 && s == a.watch)
                 printf("PHG_WATCH s %d it %d since %d avg %d kc %.6e ka %.6e krst %.6e kprev %.6e rst %d ua %d "
                        "om %.6e pres2 %.6e dres2 %.6e tp %.3e td %.3e pobj %.15e dobj %.15e\n",
                        s, it, since, (int)avg, k_cur, k_avg, krst, GS(CI::SC + CI::KPREV), (int)restart, (int)use_avg,
                        omega, oc[2], oc[3], GS(CI::SC + CI::TP), GS(CI::SC + CI::TD), oc[4], oc[5]);
         }
+#endif
         if (live) GS(CI::SC + CI::KPREV) = cand;
         const unsigned long long pf_r0 = PROF ? clock64() : 0ull;
         if (wave_any(restart)) {
