@@ -180,6 +180,17 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
     double roff[RPL];
 #pragma unroll
     for (int r = 0; r < RPL; ++r) roff[r] = 0.0;
+    // The same for the coupling rows (bits 48 + d lower, 52 + d upper): their offset -b rides on the
+    // group's lane 0 only (roffd: -b there, 0 elsewhere), so the group all-reduce returns A x - b.
+    // A coupling row whose columns are all nonants (farmer's total acreage) is freed when the
+    // nonants are fixed, so its finite side is in BF only for the variant the host picks for solves
+    // WITHOUT fixed nonants (phg_api.hip local_variant_free)
+    auto cone_lo = [&](int d) { return ((BF >> (48 + d)) & 1ull) && ((BI >> (52 + d)) & 1ull); };
+    auto cone_hi = [&](int d) { return ((BF >> (52 + d)) & 1ull) && ((BI >> (48 + d)) & 1ull); };
+    auto cone_sided = [&](int d) { return cone_lo(d) || cone_hi(d); };
+    double roffd[DD];
+#pragma unroll
+    for (int d = 0; d < DD; ++d) roffd[d] = 0.0;
     // row r of the block times a column vector f(k) (first term a product, then FMAs; one-sided rows
     // in offset form: every term an FMA onto -b)
     auto brow = [&](int r, auto f) {
@@ -205,6 +216,16 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
             if (con(d, k)) { acc = first ? cf[d][k] * f(k) : fma(cf[d][k], f(k), acc); first = false; }
         return acc;
     };
+    // an iterate's coupling partial, in offset form on one-sided coupling rows (every term an FMA
+    // onto roffd)
+    auto crow_it = [&](int d, auto f) {
+        if (!cone_sided(d)) return crow(d, f);
+        double acc = roffd[d];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if (con(d, k)) acc = fma(cf[d][k], f(k), acc);
+        return acc;
+    };
     // column k of [block; coupling]^T times (row vector g(r), coupling vector h(d))
     auto bcol = [&](int k, auto g, auto h) {
         double acc = 0.0;
@@ -223,7 +244,7 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         if constexpr (D > 0) {
             double t[D];
 #pragma unroll
-            for (int d = 0; d < D; ++d) t[d] = crow(d, [&](int k) { return xx[k]; });
+            for (int d = 0; d < D; ++d) t[d] = crow_it(d, [&](int k) { return xx[k]; });
             gsum_many<LPS, D>(t);
 #pragma unroll
             for (int d = 0; d < D; ++d) od[d] = t[d];
@@ -320,13 +341,17 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         for (int d = 0; d < D; ++d) t[cslot(d)] = axdp(d);
     };
     // replicated coupling rows, added once after the group reduction
-    auto kkt_coupling = [&](double* t, auto ydf, double scale) {
+    // (off: the activities given are an iterate's, in offset form on one-sided coupling rows; the
+    // average's are plain sums)
+    auto kkt_coupling = [&](double* t, auto ydf, double scale, bool off) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             sq();
             const double axx = t[cslot(d)] * scale, yy = ydf(d);
             const double bl = GS(CI::DLO + d), bu = GS(CI::DHI + d);
-            const double pr = axx - clampd(axx, bl, bu);
+            const double pr = cone_lo(d) ? vmin(off ? axx : axx - bl, 0.0)
+                            : cone_hi(d) ? vmax(off ? axx : axx - bu, 0.0)
+                                         : axx - clampd(axx, bl, bu);
             t[0] = fma(GS(CI::SC + CI::W2), pr * pr, t[0]);
             const double pu = pr * GS(CI::IDRD + d);
             t[2] += pu * pu;
@@ -369,11 +394,11 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
         }
 #pragma unroll
         for (int d = 0; d < D; ++d) t[cslot(d)] = axd[d];
-        kkt_coupling(t, [&](int d) { return yd[d]; }, 1.0);
+        kkt_coupling(t, [&](int d) { return yd[d]; }, 1.0, true);
 #pragma unroll
         for (int u = 0; u < 6; ++u) oc[u] = t[u];
         if (avg) {
-            kkt_coupling(t + KT, [&](int d) { return ydsum[d] * inv; }, inv);
+            kkt_coupling(t + KT, [&](int d) { return ydsum[d] * inv; }, inv, false);
 #pragma unroll
             for (int u = 0; u < 6; ++u) oa[u] = t[KT + u];
         }
@@ -550,6 +575,7 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
             axd[d] = ydsum[d] = 0.0;
             dlo[d] = lo;
             dhi[d] = hi;
+            roffd[d] = gl == 0 ? (cone_lo(d) ? -lo : cone_hi(d) ? -hi : 0.0) : 0.0;
             GS(CI::IDRD + d) = ci[d][0];
             GS(CI::YDR + d) = yd[d];
             GS(CI::DLO + d) = lo;
@@ -765,8 +791,14 @@ __global__ __launch_bounds__(64, WV) void pdhg_local_kernel(PdhgArgs a) {
             }
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                const double g = yd[d] - sig * (2.0 * axdn[d] - axd[d]);
-                yd[d] = dproj(g, dhi[d], dlo[d], 48 + d, 52 + d);
+                if (cone_lo(d)) {
+                    yd[d] = vmax(fma(-sig, fma(2.0, axdn[d], -axd[d]), yd[d]), 0.0);
+                } else if (cone_hi(d)) {
+                    yd[d] = vmin(fma(-sig, fma(2.0, axdn[d], -axd[d]), yd[d]), 0.0);
+                } else {
+                    const double g = yd[d] - sig * (2.0 * axdn[d] - axd[d]);
+                    yd[d] = dproj(g, dhi[d], dlo[d], 48 + d, 52 + d);
+                }
                 axd[d] = axdn[d];
                 if constexpr (SUM) ydsum[d] += yd[d];
             }
@@ -1006,8 +1038,9 @@ constexpr int local_loop_ops(int LPS, int CPL, int RPL, int D, unsigned MB, unsi
     for (int d = 0; d < D; ++d) {
         int e = 0;
         for (int k = 0; k < CPL; ++k) e += con(d, k);
-        ops += 2 * ((e > 0 ? 2 * e - 1 : 0) + lg);
-        ops += 2 * (4 + (inf(48 + d) ? 0 : 1) + (inf(52 + d) ? 0 : 1) + 1);
+        const bool one = (finb(48 + d) && inf(52 + d)) || (finb(52 + d) && inf(48 + d));   // offset form
+        ops += 2 * ((one ? 2 * e : (e > 0 ? 2 * e - 1 : 0)) + lg);
+        ops += 2 * (one ? 5 : 4 + (inf(48 + d) ? 0 : 1) + (inf(52 + d) ? 0 : 1) + 1);
         ops += 1;
     }
     return ops * 50;
@@ -1076,6 +1109,12 @@ static const LocalVariant kLocalVariants[] = {
     PHG_LM1(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
     PHG_LM1(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
     PHG_LM1(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF, 0x1u),
+    // ... and, for solves whose nonants are NOT fixed (phg_api.hip local_variant_free), the total-
+    // acreage coupling row's finite upper side: its A x in offset form, one dual-step instruction
+    // fewer per PDHG iteration
+    PHG_LM1(16, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF | (1ull << 52), 0x1u),
+    PHG_LM1(32, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF | (1ull << 52), 0x1u),
+    PHG_LM1(64, 4, 2, 1, 0x7Fu, 0x1u, PHG_FARMER_BI, PHG_FARMER_BF | (1ull << 52), 0x1u),
     // hydro's: no row local to a lane (the block slot dropped), all 10 coupling slots
     PHG_LM1(16, 1, 1, 10, 0x0u, 0x3FFu, 0ull, 0ull, 0x1u),
 };

@@ -116,6 +116,9 @@ struct phg_handle {
     double sense = 1.0;
     int variant = -1;          // gather kernel variant (pdhg.hip), or
     int local_variant = -1;    // lane-local kernel variant (pdhg_local.hip); preferred when >= 0
+    // the variant for solves that do not fix the nonants (phg_opts.fix_nonants == 0): its finite
+    // bound sides may include rows of nonants only, which fixing frees (local_fin_mask)
+    int local_variant_free = -1;
     int local_shape_v = -1;    // its shape's generic entry (pdhg_local_pick_masked re-picks from it)
     std::vector<int> lp_col_of, lp_row_of, lp_cpl_row;   // host copy of the lane plan (bound masks)
     // host copy of the presolved batch: the safe-bound pass's implied bounds are computed from it at
@@ -830,7 +833,10 @@ static unsigned long long local_inf_mask(const phg_batch* b, const LocalPlan& P,
 // termination check then tests them at compile time, pdhg_local.hip BF).  Fixing the nonants keeps a
 // finite column side finite (fixed_box); a row all of whose columns are nonants becomes free when
 // they are fixed (row_bounds), so such rows never count as finite here.  Same bit layout as BI.
-static unsigned long long local_fin_mask(const phg_batch* b, const LocalPlan& P, int LPS, int CPL, int RPL, int D) {
+// nonant_fix false: the mask for solves that never fix the nonants (rows of nonants only may then
+// count as finite: phg_handle::local_variant_free)
+static unsigned long long local_fin_mask(const phg_batch* b, const LocalPlan& P, int LPS, int CPL, int RPL, int D,
+                                         bool nonant_fix = true) {
     std::vector<char> isn(b->n, 0);
     for (int k = 0; k < b->N; ++k) isn[b->nonant_col[k]] = 1;
     auto all_fin = [&](const double* v, int stride, int idx) {
@@ -839,6 +845,7 @@ static unsigned long long local_fin_mask(const phg_batch* b, const LocalPlan& P,
         return true;
     };
     auto fixable = [&](int i) {   // every column of row i a nonant
+        if (!nonant_fix) return false;
         for (int p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
             if (!isn[b->colidx[p]]) return false;
         return b->rowptr[i + 1] > b->rowptr[i];
@@ -922,6 +929,11 @@ static int pick_local_variant(const phg_batch* b, LocalPlan& plan, int* sh) {
     return -1;
 }
 
+// the free-solve variant only where its lane image is the same (same slot masks): else the safe one
+static int local_pick_free(int safe, int free_v) {
+    return pdhg_local_image_items(free_v) == pdhg_local_image_items(safe) ? free_v : safe;
+}
+
 static int build_local_layout(phg_handle* h, const phg_batch* b, bool any_shape) {
     int sh[4];
     LocalPlan plan;
@@ -941,6 +953,8 @@ static int build_local_layout(phg_handle* h, const phg_batch* b, bool any_shape)
         const unsigned long long bf = local_fin_mask(b, plan, LPS, CPL, RPL, D);
         const unsigned qm = local_quad_mask(b, plan, LPS, CPL);
         h->local_variant = (gen && std::atoi(gen)) ? v : pdhg_local_pick_masked(v, mb, mc, bi, bf, qm);
+        h->local_variant_free = local_pick_free(h->local_variant, (gen && std::atoi(gen)) ? v :
+            pdhg_local_pick_masked(v, mb, mc, bi, local_fin_mask(b, plan, LPS, CPL, RPL, D, false), qm));
         h->local_shape_v = v;
         h->lp_col_of = plan.col_of;
         h->lp_row_of = plan.row_of;
@@ -2618,10 +2632,11 @@ int phg_local_info(phg_handle* h, int32_t* o) {
     if (!h || !h->loaded || !o) return fail("phg_local_info: no batch loaded");
     if (h->local_variant < 0) return fail("phg_local_info: the batch does not use the lane-local layout");
     CK(hipSetDevice(h->device));
-    o[0] = h->local_variant;
+    // (the variant PH's solves run: the nonants are not fixed there)
+    o[0] = h->local_variant_free;
     o[1] = h->lshape[0];
-    o[2] = pdhg_local_lone(h->local_variant, h->S) ? 1 : 0;
-    o[3] = pdhg_local_loop_ops(h->local_variant);
+    o[2] = pdhg_local_lone(h->local_variant_free, h->S) ? 1 : 0;
+    o[3] = pdhg_local_loop_ops(h->local_variant_free);
     return 0;
 }
 
@@ -3018,7 +3033,7 @@ int phg_solve(phg_handle* h, int32_t w_on, int32_t prox_on, const phg_opts* o) {
         }
         if (lprof) CK(hipMemsetAsync(pbuf, 0, pcap * sizeof(unsigned long long), h->stream));
         a.prof = lprof ? pbuf : nullptr;
-        CK(pdhg_local_launch(h->local_variant, a, h->stream));
+        CK(pdhg_local_launch(o->fix_nonants ? h->local_variant : h->local_variant_free, a, h->stream));
         if (lprof) {
             std::vector<unsigned long long> hb(pcap);
             CK(hipMemcpyAsync(hb.data(), pbuf, pcap * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
@@ -3298,6 +3313,9 @@ int phg_set_col_bounds(phg_handle* h, const double* col_lo, const double* col_hi
         const char* gen = std::getenv("PHG_LOCAL_GENERIC");
         const int v2 = (gen && std::atoi(gen)) ? h->local_shape_v
                        : pdhg_local_pick_masked(h->local_shape_v, h->local_masks[0], h->local_masks[1], bi, bf, qm);
+        const unsigned long long bff = local_fin_mask(&v, plan, sh[0], sh[1], sh[2], sh[3], false);
+        const int v2f = (gen && std::atoi(gen)) ? h->local_shape_v
+                        : pdhg_local_pick_masked(h->local_shape_v, h->local_masks[0], h->local_masks[1], bi, bff, qm);
         const int ni = pdhg_local_image_items(v2);
         if (ni > h->loc.ni) {
             double* img;
@@ -3305,6 +3323,7 @@ int phg_set_col_bounds(phg_handle* h, const double* col_lo, const double* col_hi
             h->loc.img = img;
         }
         h->local_variant = v2;
+        h->local_variant_free = local_pick_free(v2, v2f);
         h->loc.ni = ni;
         PdhgArgs ia{};
         ia.S = S; ia.n = n; ia.m = h->m; ia.nnz = h->nnz;

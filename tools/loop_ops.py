@@ -40,8 +40,9 @@ def loop_ops(LPS, CPL, RPL, D, MB, MC, BI, BF):
     lg = LPS.bit_length() - 1
     for d in range(D):
         e = sum(con(d, k) for k in range(CPL))
-        ops += 2 * ((2 * e - 1 if e else 0) + lg)
-        ops += 2 * (4 + (0 if inf(48 + d) else 1) + (0 if inf(52 + d) else 1) + 1)
+        one = (finb(48 + d) and inf(52 + d)) or (finb(52 + d) and inf(48 + d))
+        ops += 2 * ((2 * e if one else (2 * e - 1 if e else 0)) + lg)
+        ops += 2 * (5 if one else 4 + (0 if inf(48 + d) else 1) + (0 if inf(52 + d) else 1) + 1)
         ops += 1
     return ops * 50
 
@@ -66,16 +67,17 @@ def main():
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
                         os.path.join(ROOT, "mpi-sppy_amd", "csrc", "pdhg_local.hip"), "-o", out], check=True)
         asm = open(out).read()
-    for lps in (16, 32, 64):
-        for wv in (2, 1):
-            name = (f"_ZN3phg17pdhg_local_kernelILi{lps}ELi4ELi2ELi1ELb0ELj127ELj1ELy{FARMER_BI}ELy{FARMER_BF}ELj1ELi{wv}EEEvNS_8PdhgArgsE")
-            if name + ":" not in asm:
-                continue
-            c = isa_counts(asm, name)
-            want = loop_ops(lps, 4, 2, 1, 0x7F, 0x1, FARMER_BI, FARMER_BF)
-            print(json.dumps({"variant": f"farmer LPS={lps} WV={wv}", **c,
-                              "isa_ops_per_lane_iter": c["ops_per_2_iters"] / 2,
-                              "local_loop_ops_per_lane_iter": want / 100}))
+    for bf, tag in ((FARMER_BF, ""), (FARMER_BF | (1 << 52), " free")):
+        for lps in (16, 32, 64):
+            for wv in (2, 1):
+                name = (f"_ZN3phg17pdhg_local_kernelILi{lps}ELi4ELi2ELi1ELb0ELj127ELj1ELy{FARMER_BI}ELy{bf}ELj1ELi{wv}EEEvNS_8PdhgArgsE")
+                if name + ":" not in asm:
+                    continue
+                c = isa_counts(asm, name)
+                want = loop_ops(lps, 4, 2, 1, 0x7F, 0x1, FARMER_BI, bf)
+                print(json.dumps({"variant": f"farmer{tag} LPS={lps} WV={wv}", **c,
+                                  "isa_ops_per_lane_iter": c["ops_per_2_iters"] / 2,
+                                  "local_loop_ops_per_lane_iter": want / 100}))
 
 
 if __name__ == "__main__":
