@@ -23,8 +23,9 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import loop_ops  # noqa: E402
 
 KERNEL = "pdhg_local_kernel<32, 4, 2, 1, false, 127u, 1u"
+# the variant PH's solves run (free nonants: the coupling row's finite side compiled in, round 6)
 SYMBOL = (f"_ZN3phg17pdhg_local_kernelILi32ELi4ELi2ELi1ELb0ELj127ELj1ELy{loop_ops.FARMER_BI}"
-          f"ELy{loop_ops.FARMER_BF}ELj1ELi2EEEvNS_8PdhgArgsE")
+          f"ELy{loop_ops.FARMER_BF | (1 << 52)}ELj1ELi2EEEvNS_8PdhgArgsE")
 F64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_TRANS_F64")
 
 
