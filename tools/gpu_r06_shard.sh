@@ -1,7 +1,7 @@
 # round 6 shard table: farmer cm=10 per-GPU shard sizes, 2 runs each, bench defaults, no conv leg
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06_shard; mkdir -p $O
+O=gpurun_out/r06_shard2; mkdir -p $O
 for rep in 1 2; do
   for sc in 10000 5000 2500 1250; do
     timeout -k 10 300 python -u bench.py --cpu-seconds 0 --conv-iters 0 --scen $sc > $O/s${sc}_$rep.json 2> $O/s${sc}_$rep.err || { tail -5 $O/s${sc}_$rep.err; exit 1; }
